@@ -1,0 +1,193 @@
+/*
+ * pcp.h -- C-ABI of libpcp, the MI355X (gfx950) implementation of the kNN-driven geometry
+ * hot path of RioWong/PointCloudProcess.
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int status codes (0 = OK, < 0 =
+ * error; pcp_last_error(ctx) has the message).  No torch / HIP types in any signature:
+ * streams are passed as `void*` (a hipStream_t, NULL = the device's default stream).
+ *
+ * Memory: every array argument named *_dev is DEVICE memory (hipMalloc'd, or a torch
+ * tensor's data_ptr()); host arrays are named *_host.  pcp_malloc/pcp_memcpy_* let a host
+ * caller (include/pcp_pcl.hpp, the drop-in C++ shim) stage data without including HIP.
+ *
+ * Each entry point names the reference interface it replaces (file:line in the reference
+ * tree).  The C++ shim that restores the reference's own class signatures on top of this
+ * ABI is include/pcp_pcl.hpp; bindings for other hosts are in INTEGRATION.md.
+ */
+#ifndef PCP_H
+#define PCP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCP_ABI_VERSION 1
+
+/* ----------------------------------------------------------------------- status codes */
+enum pcp_status {
+    PCP_OK = 0,
+    PCP_ERR_ARG = -1,         /* bad argument (null handle, negative size, k <= 0, ...) */
+    PCP_ERR_HIP = -2,         /* a HIP runtime call failed */
+    PCP_ERR_NOMEM = -3,       /* device allocation failed */
+    PCP_ERR_EMPTY = -4,       /* empty input where the reference would crash / return */
+    PCP_ERR_UNSUPPORTED = -5, /* option not implemented (e.g. do_affine) */
+    PCP_ERR_ICP = -6,         /* ICP failed: < 3 correspondences (ICP.h:26-28 err < 0) */
+    PCP_ERR_CAPACITY = -7     /* caller-provided output buffer too small */
+};
+
+/* ----------------------------------------------------------------------- point layout */
+/* PointXYZRGBA (point_type.h:9-82): 48-byte stride, x/y/z doubles at 0/8/16, data[3] at
+ * 24, rgba u32 at 32, stamp_id u32 at 36, 8 pad bytes. */
+#define PCP_AOS48_STRIDE 48
+
+/* PlanSegment subset written by the normals kernel (data_struct.h:188-198). */
+typedef struct pcp_plane {
+    float normal_x, normal_y, normal_z;
+    float min_value;  /* lambda3, calculate_feature.cpp:198 */
+    float curvature;  /* lambda3/(l1+l2+l3), calculate_feature.cpp:199 */
+    float distance;   /* -(n . mean), calculate_feature.cpp:197 */
+} pcp_plane;
+
+/* ----------------------------------------------------------------------- context */
+typedef struct pcp_ctx pcp_ctx;     /* device, stream, scratch arena, last error */
+typedef struct pcp_index pcp_index; /* device-resident uniform-grid index over a cloud */
+typedef struct pcp_icp pcp_icp;     /* device-resident ICP query set */
+
+int         pcp_abi_version(void);
+int         pcp_ctx_create(int device, void* stream, pcp_ctx** out);
+int         pcp_ctx_destroy(pcp_ctx* ctx);
+int         pcp_ctx_set_stream(pcp_ctx* ctx, void* stream);
+void*       pcp_ctx_stream(pcp_ctx* ctx);
+const char* pcp_last_error(const pcp_ctx* ctx);
+int         pcp_sync(pcp_ctx* ctx);
+
+int pcp_malloc(pcp_ctx* ctx, void** dev_ptr, size_t bytes);
+int pcp_free(pcp_ctx* ctx, void* dev_ptr);
+int pcp_memcpy_h2d(pcp_ctx* ctx, void* dst_dev, const void* src_host, size_t bytes);
+int pcp_memcpy_d2h(pcp_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
+int pcp_memset(pcp_ctx* ctx, void* dst_dev, int value, size_t bytes);
+
+/* ----------------------------------------------------------------------- K: spatial index */
+/* Replaces KdTreeFLANN<PointT>::setInputCloud (kd_tree.h:772-798) + convertCloudToArray
+ * (kd_tree.h:928-997): drops non-finite points, keeps index_mapping_, identity when no
+ * drop and no `indices`.  xyz_dev: doubles with `stride_bytes` between points (48 for
+ * AoS48, 24 for packed xyz).  indices_dev: optional subset (NULL = whole cloud).
+ * cell_size <= 0 picks a size from the data.  The index owns a device copy of the points. */
+int pcp_index_build_f64(pcp_ctx* ctx, const double* xyz_dev, size_t stride_bytes, int64_t n,
+                        const int32_t* indices_dev, int64_t n_indices, double cell_size,
+                        pcp_index** out);
+/* fp32 variant (trimesh2 float vertices, point_cloud_helper.cpp:89-104, the ICP target). */
+int pcp_index_build_f32(pcp_ctx* ctx, const float* xyz_dev, size_t stride_bytes, int64_t n,
+                        double cell_size, pcp_index** out);
+int pcp_index_destroy(pcp_index* index);
+int64_t pcp_index_size(const pcp_index* index);          /* total_nr_points_ */
+int pcp_index_identity_mapping(const pcp_index* index);  /* identity_mapping_ */
+double pcp_index_cell_size(const pcp_index* index);
+int64_t pcp_index_cells(const pcp_index* index);         /* allocated cell slots */
+/* Spatially sorted copy of the indexed points: fp32 index -> float4 {x,y,z,bits(idx)};
+ * fp64 index -> double4 {x,y,z,(double)internal j}. Borrowed device pointer. */
+const void* pcp_index_sorted_points(const pcp_index* index);
+
+/* Batch KdTreeFLANN::nearestKSearch (kd_tree.h:814-845), exact fp64: k clamped to the
+ * index size, rows ascending by (d2, internal j), d2 = ((0+d0^2)+d1^2)+d2^2 (FLANN
+ * L2_Simple<double>), indices mapped through index_mapping_.  Outputs are nq*k; entries
+ * past the clamped k are -1 / +inf.  Per-query output count in out_n_dev (optional). */
+int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_stride_bytes,
+            int64_t nq, int k, int32_t* out_idx_dev, double* out_d2_dev);
+
+/* Batch KdTreeFLANN::radiusSearch (kd_tree.h:863-903): d2 < radius*radius (strict),
+ * sorted by (d2, internal j), truncated to max_nn (0 or > size = unlimited).
+ * Two-phase CSR: pcp_radius_count writes per-query counts; the caller scans them into
+ * offsets (nq+1, int64) and calls pcp_radius_fill. */
+int pcp_radius_count(pcp_ctx* ctx, const pcp_index* index, const double* q_dev,
+                     size_t q_stride_bytes, int64_t nq, double radius, uint32_t max_nn,
+                     int32_t* out_count_dev);
+int pcp_radius_fill(pcp_ctx* ctx, const pcp_index* index, const double* q_dev,
+                    size_t q_stride_bytes, int64_t nq, double radius, uint32_t max_nn,
+                    const int64_t* offsets_dev, int32_t* out_idx_dev, double* out_d2_dev);
+/* Exclusive scan helper for the CSR offsets: offsets[0]=0 ... offsets[nq]=total. */
+int pcp_scan_counts(pcp_ctx* ctx, const int32_t* count_dev, int64_t n, int64_t* offsets_dev,
+                    int64_t* total_host);
+
+/* Brute-force kNN (BASELINE config 2): fp32 MFMA ranking of |p|^2 - 2 q.p over LDS tiles,
+ * certified + re-ranked in fp64, falling back to an exact fp64 scan for any query whose
+ * candidate set cannot be certified.  Same output contract as pcp_knn (no index). */
+int pcp_knn_bruteforce(pcp_ctx* ctx, const double* target_dev, size_t t_stride_bytes,
+                       int64_t nt, const double* q_dev, size_t q_stride_bytes, int64_t nq,
+                       int k, int32_t* out_idx_dev, double* out_d2_dev);
+
+/* kd_tree_lod KdTree::nearestKSearch (kd_tree_lod/kd_tree.cpp:78-117) over an AoS48 cloud:
+ * integer-truncated centroid, float search, first j with point_dis2 <= FLT_EPSILON
+ * (else -1), k_dis2 = residual of the last scanned j (reference quirk). */
+int pcp_knn_lod(pcp_ctx* ctx, const void* cloud_aos48_dev, int64_t n, const void* q_aos48_dev,
+                int64_t nq, int k, int32_t* out_idx_dev, double* out_d2_dev);
+
+/* ----------------------------------------------------------------------- V: cloud ops */
+/* PointCloudHelper::getMinMax3D(cloud, Vector4d&, Vector4d&) (point_cloud_helper.h:59-90). */
+int pcp_minmax_aos48(pcp_ctx* ctx, const void* in_dev, int64_t n, int is_dense,
+                     double min_host[4], double max_host[4]);
+/* compute3DCentroid (point_cloud_helper.h:193-230).  The GPU sum is a fixed-order tree,
+ * not the reference's sequential left fold. */
+int pcp_centroid_aos48(pcp_ctx* ctx, const void* in_dev, int64_t n, int is_dense,
+                       double c_host[4], uint32_t* count_host);
+/* transformPointCloud (point_cloud_helper.h:92-127), row-major 4x4, in == out allowed. */
+int pcp_transform_aos48(pcp_ctx* ctx, const void* in_dev, void* out_dev, int64_t n,
+                        int is_dense, const double T_host[16]);
+
+/* VoxelGrid<PointXYZRGBA>::filter -> applyFilter (voxel_grid.h:811-1056) with
+ * setLeafSize(l[0],l[1],l[2]) (voxel_grid.h:538-549) and setDownsampleAllData.
+ * out_dev must hold n points; *n_out receives the voxel count; out_voxel_idx_dev
+ * (optional) receives each output's u32 linear voxel index. */
+int pcp_voxel_filter(pcp_ctx* ctx, const void* in_aos48_dev, int64_t n, int is_dense,
+                     const double leaf_host[3], int downsample_all_data, void* out_aos48_dev,
+                     int64_t* n_out, uint32_t* out_voxel_idx_dev);
+/* PointCloudHelper::remove_duplicate(cloud, float leaf) (point_cloud_helper.cpp:42-63). */
+int pcp_remove_duplicate(pcp_ctx* ctx, const void* in_aos48_dev, int64_t n, int is_dense,
+                         float leaf, void* out_aos48_dev, int64_t* n_out);
+
+/* ----------------------------------------------------------------------- F: normals */
+/* Per-point PCA normals over the kNN(k) neighbourhood of every indexed point
+ * (calculate_feature.cpp:233 neighbourhood + calculate_plan_parameter_h_points
+ * :119-206).  Output in caller-index order (n = size of the cloud passed to the build,
+ * points dropped as non-finite get {0,0,0,1}); sign: largest-|.| component positive. */
+int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* index, int k, pcp_plane* out_dev,
+                    int64_t n_out);
+
+/* ----------------------------------------------------------------------- I: ICP */
+/* ICP correspondence/transform loop (point_cloud_helper.cpp:75-166 get_rot_icp ->
+ * trimesh2 ICP(), point_cloud_closure + main_blend callers).  The target is an fp32
+ * index (pcp_index_build_f32); the query set is sorted spatially once here. */
+int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q_dev,
+                   size_t q_stride_bytes, int64_t nq, pcp_icp** out);
+int pcp_icp_destroy(pcp_icp* icp);
+/* One iteration at pose T (row-major 4x4 double, cast to fp32 for the kernel):
+ * correspondences within rmax + the 24 accumulators written to acc_dev
+ * (device, 24 doubles).  corr_idx_dev / corr_d2_dev (optional, nq each) receive the
+ * winner per query in the ORIGINAL query order (-1 / +inf when rejected). */
+int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T_host[16], float rmax,
+                 double* acc_dev, int32_t* corr_idx_dev, float* corr_d2_dev);
+/* Host Kabsch/Umeyama solve of the increment dT from 24 accumulators (host memory). */
+int pcp_icp_solve(const double acc_host[24], int do_scale, double dT_host[16]);
+/* Full loop: T_inout (row-major), `iters` iterations (stops early when the increment's
+ * rotation and translation fall below eps, eps <= 0 = never).  *err = RMS distance of
+ * the last iteration's correspondences. */
+int pcp_icp_run(pcp_ctx* ctx, pcp_icp* icp, double T_inout[16], float rmax, int iters,
+                int do_scale, double eps, float* err);
+/* Device time (ms) of the last pcp_icp_step/pcp_icp_run correspondence kernels
+ * (sum over iterations) and the number of launches it covers, from hipEvents. */
+int pcp_icp_last_kernel_ms(const pcp_icp* icp, double* ms, int* launches);
+
+/* PointCloudHelper::get_rot_icp (point_cloud_helper.cpp:75-166) on AoS48 clouds:
+ * joint centroid, float cast, ICP(query = temp -> target = src), un-centring
+ * t' = t - R c + c.  mat_rot row-major.  Returns PCP_OK and *err (< 0 on failure). */
+int pcp_get_rot_icp(pcp_ctx* ctx, const void* src_aos48_dev, int64_t ns,
+                    const void* temp_aos48_dev, int64_t nt, double mat_rot_host[16],
+                    float rmax, int iters, int do_scale, double cell_size, float* err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCP_H */

@@ -1,0 +1,104 @@
+// Shared internals of libpcp (HIP, gfx950).  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/pcp.h"
+
+struct pcp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string last_error;
+    // grow-only scratch arena (one per context; contexts are not shared across threads)
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+};
+
+namespace pcp {
+
+int set_error(pcp_ctx* ctx, int code, const char* fmt, ...);
+int hip_fail(pcp_ctx* ctx, hipError_t e, const char* what, const char* file, int line);
+// scratch of at least `bytes` (invalidates earlier scratch pointers)
+int scratch(pcp_ctx* ctx, size_t bytes, void** out);
+
+#define PCP_HIP(ctx, expr)                                                           \
+    do {                                                                             \
+        hipError_t _e = (expr);                                                      \
+        if (_e != hipSuccess) return ::pcp::hip_fail((ctx), _e, #expr, __FILE__, __LINE__); \
+    } while (0)
+
+#define PCP_TRY(expr)                 \
+    do {                              \
+        int _rc = (expr);             \
+        if (_rc != PCP_OK) return _rc; \
+    } while (0)
+
+#define PCP_LAUNCH_CHECK(ctx) PCP_HIP(ctx, hipGetLastError())
+
+template <typename T>
+int dmalloc(pcp_ctx* ctx, T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return set_error(ctx, PCP_ERR_NOMEM, "hipMalloc(%zu bytes) failed: %s",
+                         count * sizeof(T), hipGetErrorString(e));
+    }
+    return PCP_OK;
+}
+
+inline unsigned grid_for(int64_t n, int block, int64_t cap = 1 << 20) {
+    int64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ bool finite3(double x, double y, double z) {
+    return isfinite(x) && isfinite(y) && isfinite(z);
+}
+
+// Exclusive scan of `n` uint32 values in place (values' total must fit uint32).
+// Returns the total through *total_dev (device, optional) and *total_host (optional, syncs).
+int scan_u32_inplace(pcp_ctx* ctx, uint32_t* data, int64_t n, uint32_t* total_host);
+// Exclusive scan of int32 counts into int64 offsets (n+1 entries).
+int scan_i32_to_i64(pcp_ctx* ctx, const int32_t* in, int64_t n, int64_t* out, int64_t* total_host);
+
+// ---------------------------------------------------------------- grid description
+// Uniform grid of cubic cells, grouped into 4x4x4 bricks.  A dense brick table maps a
+// brick to a slot (or -1); each slot owns 64 consecutive entries of cell_start, so the
+// points of cell (slot, local) are sorted[cell_start[64*slot+local] .. cell_start[.. +1]).
+struct GridDesc {
+    double o[3];      // origin (bbox min)
+    double h, inv_h;  // cell size
+    float of[3];
+    float hf, inv_hf;
+    int n[3];         // cells per axis
+    int nb[3];        // bricks per axis
+    int64_t nbricks;
+    int64_t nslots;
+    const int32_t* brick;     // nbricks
+    const uint32_t* cstart;   // 64*nslots + 1
+};
+
+}  // namespace pcp
+
+struct pcp_index {
+    int is_f64 = 0;
+    pcp::GridDesc g{};
+    int64_t n_in = 0;        // size of the cloud passed in (n, or n_indices)
+    int64_t n = 0;           // valid points (total_nr_points_)
+    int identity = 0;
+    int32_t* brick = nullptr;
+    uint32_t* cstart = nullptr;
+    void* pts = nullptr;        // float4[n] or double4[n], sorted by (slot, local cell)
+    int32_t* mapping = nullptr; // internal j -> caller index (n)
+    int32_t* sorted_j = nullptr; // sorted position -> internal j (n)
+    pcp_ctx* owner = nullptr;
+};

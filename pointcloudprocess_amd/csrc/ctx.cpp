@@ -1,0 +1,132 @@
+// Context, error and memory helpers of the C-ABI (host code, built by hipcc).
+#include <cstdarg>
+#include <cstring>
+
+#include "common.hpp"
+
+namespace pcp {
+
+int set_error(pcp_ctx* ctx, int code, const char* fmt, ...) {
+    if (ctx) {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        ctx->last_error = buf;
+    }
+    return code;
+}
+
+int hip_fail(pcp_ctx* ctx, hipError_t e, const char* what, const char* file, int line) {
+    (void)hipGetLastError();
+    return set_error(ctx, e == hipErrorOutOfMemory ? PCP_ERR_NOMEM : PCP_ERR_HIP,
+                     "%s failed: %s (%s:%d)", what, hipGetErrorString(e), file, line);
+}
+
+int scratch(pcp_ctx* ctx, size_t bytes, void** out) {
+    if (bytes > ctx->scratch_bytes) {
+        if (ctx->scratch) {
+            PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            PCP_HIP(ctx, hipFree(ctx->scratch));
+            ctx->scratch = nullptr;
+            ctx->scratch_bytes = 0;
+        }
+        size_t want = bytes + bytes / 4 + 4096;
+        hipError_t e = hipMalloc(&ctx->scratch, want);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return set_error(ctx, PCP_ERR_NOMEM, "scratch hipMalloc(%zu) failed", want);
+        }
+        ctx->scratch_bytes = want;
+    }
+    *out = ctx->scratch;
+    return PCP_OK;
+}
+
+}  // namespace pcp
+
+extern "C" {
+
+int pcp_abi_version(void) { return PCP_ABI_VERSION; }
+
+int pcp_ctx_create(int device, void* stream, pcp_ctx** out) {
+    if (!out) return PCP_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return PCP_ERR_HIP;
+    }
+    if (device < 0 || device >= ndev) return PCP_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return PCP_ERR_HIP;
+    pcp_ctx* c = new pcp_ctx();
+    c->device = device;
+    c->stream = (hipStream_t)stream;  // NULL = the device's default (null) stream
+    *out = c;
+    return PCP_OK;
+}
+
+int pcp_ctx_destroy(pcp_ctx* ctx) {
+    if (!ctx) return PCP_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return PCP_OK;
+}
+
+int pcp_ctx_set_stream(pcp_ctx* ctx, void* stream) {
+    if (!ctx) return PCP_ERR_ARG;
+    if (ctx->own_stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+        ctx->own_stream = false;
+    }
+    ctx->stream = (hipStream_t)stream;
+    return PCP_OK;
+}
+
+void* pcp_ctx_stream(pcp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+const char* pcp_last_error(const pcp_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null ctx"; }
+
+int pcp_sync(pcp_ctx* ctx) {
+    if (!ctx) return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PCP_OK;
+}
+
+int pcp_malloc(pcp_ctx* ctx, void** p, size_t bytes) {
+    if (!ctx || !p) return PCP_ERR_ARG;
+    return pcp::dmalloc(ctx, (char**)p, bytes);
+}
+
+int pcp_free(pcp_ctx* ctx, void* p) {
+    if (!ctx) return PCP_ERR_ARG;
+    if (p) PCP_HIP(ctx, hipFree(p));
+    return PCP_OK;
+}
+
+int pcp_memcpy_h2d(pcp_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx || (bytes && (!dst || !src))) return PCP_ERR_ARG;
+    if (bytes) PCP_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PCP_OK;
+}
+
+int pcp_memcpy_d2h(pcp_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx || (bytes && (!dst || !src))) return PCP_ERR_ARG;
+    if (bytes) PCP_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PCP_OK;
+}
+
+int pcp_memset(pcp_ctx* ctx, void* dst, int value, size_t bytes) {
+    if (!ctx || (bytes && !dst)) return PCP_ERR_ARG;
+    if (bytes) PCP_HIP(ctx, hipMemsetAsync(dst, value, bytes, ctx->stream));
+    return PCP_OK;
+}
+
+}  // extern "C"

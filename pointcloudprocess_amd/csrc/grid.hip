@@ -1,0 +1,362 @@
+// Uniform-grid index build (replaces KdTreeFLANN::setInputCloud, kd_tree.h:772-798,
+// and the trimesh2 KDtree constructions at point_cloud_helper.cpp:110-111).
+//
+// Build = compaction of finite points (index_mapping_) -> bbox -> brick marking ->
+// brick-slot scan -> per-cell counting (atomics) -> cell-start scan -> scatter into
+// cell order.  All passes are HBM streams over the points; the only host round trips
+// are the bbox (to size the brick table) and the slot count.
+#include <cmath>
+#include <vector>
+
+#include "grid.hpp"
+
+namespace pcp {
+namespace {
+
+constexpr int kB = 256;
+
+template <typename T>
+__device__ __forceinline__ const T* pt_ptr(const T* base, size_t stride_bytes, int64_t i) {
+    return (const T*)((const char*)base + (size_t)i * stride_bytes);
+}
+
+// validity flags of the (optionally indexed) input
+template <typename T>
+__global__ void k_valid(const T* xyz, size_t stride, int64_t n_in, const int32_t* indices,
+                        uint32_t* flag) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_in;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t ci = indices ? indices[i] : i;
+        const T* p = pt_ptr(xyz, stride, ci);
+        flag[i] = (isfinite((double)p[0]) && isfinite((double)p[1]) && isfinite((double)p[2])) ? 1u : 0u;
+    }
+}
+
+// compaction: internal j = exclusive prefix of the flags (convertCloudToArray order)
+template <typename T>
+__global__ void k_compact(const T* xyz, size_t stride, int64_t n_in, const int32_t* indices,
+                          const uint32_t* pos, const uint32_t* flagbits, T* cxyz, int32_t* mapping) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_in;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (!((flagbits[i >> 5] >> (i & 31)) & 1u)) continue;
+        int64_t ci = indices ? indices[i] : i;
+        const T* p = pt_ptr(xyz, stride, ci);
+        uint32_t j = pos[i];
+        cxyz[3 * (int64_t)j + 0] = p[0];
+        cxyz[3 * (int64_t)j + 1] = p[1];
+        cxyz[3 * (int64_t)j + 2] = p[2];
+        mapping[j] = (int32_t)ci;
+    }
+}
+
+__global__ void k_pack_bits(const uint32_t* flag, int64_t n, uint32_t* bits) {
+    int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t nw = (n + 31) / 32;
+    if (w >= nw) return;
+    uint32_t v = 0;
+    for (int b = 0; b < 32; b++) {
+        int64_t i = w * 32 + b;
+        if (i < n && flag[i]) v |= 1u << b;
+    }
+    bits[w] = v;
+}
+
+template <typename T>
+__global__ void k_minmax(const T* cxyz, int64_t n, double* part) {
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        for (int a = 0; a < 3; a++) {
+            double v = (double)cxyz[3 * i + a];
+            mn[a] = fmin(mn[a], v);
+            mx[a] = fmax(mx[a], v);
+        }
+    }
+    __shared__ double s[6][kB];
+    for (int a = 0; a < 3; a++) { s[a][threadIdx.x] = mn[a]; s[3 + a][threadIdx.x] = mx[a]; }
+    __syncthreads();
+    for (int w = kB / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int a = 0; a < 3; a++) {
+                s[a][threadIdx.x] = fmin(s[a][threadIdx.x], s[a][threadIdx.x + w]);
+                s[3 + a][threadIdx.x] = fmax(s[3 + a][threadIdx.x], s[3 + a][threadIdx.x + w]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int a = 0; a < 6; a++) part[blockIdx.x * 6 + a] = s[a][0];
+}
+
+template <typename T>
+__device__ __forceinline__ void cell_of_point(const GridDesc& g, const T* p, int& cx, int& cy, int& cz) {
+    cx = clampi(cell_i<T>(g, p[0], 0), 0, g.n[0] - 1);
+    cy = clampi(cell_i<T>(g, p[1], 1), 0, g.n[1] - 1);
+    cz = clampi(cell_i<T>(g, p[2], 2), 0, g.n[2] - 1);
+}
+
+template <typename T>
+__global__ void k_mark(GridDesc g, const T* cxyz, int64_t n, int32_t* brick) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int cx, cy, cz;
+        cell_of_point<T>(g, cxyz + 3 * i, cx, cy, cz);
+        brick[brick_of(g, cx, cy, cz)] = 1;
+    }
+}
+
+__global__ void k_brick_bits(const int32_t* brick, int64_t nb, uint32_t* bits) {
+    int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (w >= (nb + 31) / 32) return;
+    uint32_t v = 0;
+    for (int b = 0; b < 32; b++) {
+        int64_t i = w * 32 + b;
+        if (i < nb && brick[i] != 0) v |= 1u << b;
+    }
+    bits[w] = v;
+}
+
+__global__ void k_brick_final(int32_t* brick, int64_t nb, const uint32_t* bits) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nb;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        bool on = (bits[i >> 5] >> (i & 31)) & 1u;
+        brick[i] = on ? brick[i] : -1;  // brick[] holds the exclusive prefix = slot id
+    }
+}
+
+template <typename T>
+__global__ void k_count(GridDesc g, const T* cxyz, int64_t n, uint32_t* count, uint32_t* rank) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int cx, cy, cz;
+        cell_of_point<T>(g, cxyz + 3 * i, cx, cy, cz);
+        int64_t c = (int64_t)g.brick[brick_of(g, cx, cy, cz)] * 64 + local_of(cx, cy, cz);
+        rank[i] = atomicAdd(&count[c], 1u);
+    }
+}
+
+__global__ void k_nonempty(const uint32_t* count, int64_t ncells, unsigned long long* out) {
+    unsigned long long local = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ncells;
+         i += (int64_t)gridDim.x * blockDim.x)
+        local += count[i] ? 1 : 0;
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, local);
+}
+
+template <typename T>
+__global__ void k_scatter(GridDesc g, const T* cxyz, int64_t n, const uint32_t* rank,
+                          const int32_t* mapping, typename Real<T>::V4* pts, int32_t* sorted_j,
+                          int is_f64) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int cx, cy, cz;
+        const T* p = cxyz + 3 * i;
+        cell_of_point<T>(g, p, cx, cy, cz);
+        int64_t c = (int64_t)g.brick[brick_of(g, cx, cy, cz)] * 64 + local_of(cx, cy, cz);
+        uint32_t dst = g.cstart[c] + rank[i];
+        typename Real<T>::V4 v;
+        v.x = p[0]; v.y = p[1]; v.z = p[2];
+        if (is_f64) v.w = (T)(double)i;                     // internal j (FLANN tie order)
+        else v.w = (T)__int_as_float(mapping[i]);            // caller index bits (ICP)
+        pts[dst] = v;
+        sorted_j[dst] = (int32_t)i;
+    }
+}
+
+// Grid geometry for a cell size.  Returns false when the brick table would exceed the cap.
+bool make_geometry(GridDesc& g, const double mn[3], const double mx[3], double h, int64_t cap) {
+    g.h = h;
+    g.inv_h = 1.0 / h;
+    g.hf = (float)h;
+    g.inv_hf = (float)(1.0 / h);
+    int64_t nb = 1;
+    for (int a = 0; a < 3; a++) {
+        g.o[a] = mn[a];
+        g.of[a] = (float)mn[a];
+        double ext = (mx[a] - mn[a]) / h;
+        if (!(ext < 4.0e8)) return false;
+        int64_t na = (int64_t)std::floor(ext) + 2;  // +1 for the max point, +1 guard for rounding
+        g.n[a] = (int)na;
+        g.nb[a] = (int)((na + 3) / 4);
+        nb *= g.nb[a];
+        if (nb > cap) return false;
+    }
+    g.nbricks = nb;
+    return true;
+}
+
+template <typename T>
+int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const int32_t* indices,
+               double cell_size, int is_f64, pcp_index** out) {
+    if (!ctx || !out || n_in < 0 || (n_in > 0 && !xyz)) return PCP_ERR_ARG;
+    if (n_in >= (int64_t)1 << 31) return set_error(ctx, PCP_ERR_ARG, "index supports < 2^31 points");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    pcp_index* ix = new pcp_index();
+    ix->is_f64 = is_f64;
+    ix->owner = ctx;
+    ix->n_in = n_in;
+    auto fail = [&](int rc) { pcp_index_destroy(ix); return rc; };
+
+    // ---- compaction (convertCloudToArray)
+    uint32_t* flag = nullptr;
+    uint32_t* bits = nullptr;
+    T* cxyz = nullptr;
+    int rc;
+    const int64_t nw = (n_in + 31) / 32;
+    if ((rc = dmalloc(ctx, &flag, n_in + 1)) || (rc = dmalloc(ctx, &bits, nw + 1))) {
+        hipFree(flag); hipFree(bits);
+        return fail(rc);
+    }
+    uint32_t nvalid = 0;
+    if (n_in > 0) {
+        hipLaunchKernelGGL(k_valid<T>, dim3(grid_for(n_in, kB)), dim3(kB), 0, st, xyz, stride, n_in, indices, flag);
+        hipLaunchKernelGGL(k_pack_bits, dim3(grid_for(nw, kB)), dim3(kB), 0, st, flag, n_in, bits);
+        rc = scan_u32_inplace(ctx, flag, n_in, &nvalid);
+        if (rc) { hipFree(flag); hipFree(bits); return fail(rc); }
+    }
+    ix->n = nvalid;
+    ix->identity = (indices == nullptr && (int64_t)nvalid == n_in) ? 1 : 0;
+    if ((rc = dmalloc(ctx, &cxyz, 3 * (size_t)(nvalid + 1))) || (rc = dmalloc(ctx, &ix->mapping, nvalid + 1))) {
+        hipFree(flag); hipFree(bits); hipFree(cxyz);
+        return fail(rc);
+    }
+    if (n_in > 0)
+        hipLaunchKernelGGL(k_compact<T>, dim3(grid_for(n_in, kB)), dim3(kB), 0, st, xyz, stride, n_in,
+                           indices, flag, bits, cxyz, ix->mapping);
+    hipFree(flag);
+    hipFree(bits);  // (stream-ordered frees are safe: hipFree synchronises)
+    const int64_t n = nvalid;
+
+    // ---- bbox
+    double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
+    if (n > 0) {
+        const unsigned nbk = grid_for(n, kB, 1024);
+        double* part;
+        if ((rc = dmalloc(ctx, &part, 6 * (size_t)nbk))) { hipFree(cxyz); return fail(rc); }
+        hipLaunchKernelGGL(k_minmax<T>, dim3(nbk), dim3(kB), 0, st, cxyz, n, part);
+        std::vector<double> hp(6 * nbk);
+        hipMemcpyAsync(hp.data(), part, hp.size() * sizeof(double), hipMemcpyDeviceToHost, st);
+        hipError_t e = hipStreamSynchronize(st);
+        hipFree(part);
+        if (e != hipSuccess) { hipFree(cxyz); return fail(hip_fail(ctx, e, "bbox", __FILE__, __LINE__)); }
+        for (int a = 0; a < 3; a++) { mn[a] = INFINITY; mx[a] = -INFINITY; }
+        for (unsigned b = 0; b < nbk; b++)
+            for (int a = 0; a < 3; a++) {
+                mn[a] = std::fmin(mn[a], hp[6 * b + a]);
+                mx[a] = std::fmax(mx[a], hp[6 * b + 3 + a]);
+            }
+    }
+
+    // ---- cell size: given, or a density estimate refined once from the measured occupancy
+    const int64_t cap = std::max<int64_t>((int64_t)1 << 24, 8 * n);
+    double ext[3];
+    for (int a = 0; a < 3; a++) ext[a] = std::max(mx[a] - mn[a], 1e-9);
+    const bool auto_h = !(cell_size > 0);
+    double h = cell_size;
+    if (auto_h) {
+        const double target = 4.0;  // points per non-empty cell
+        h = std::cbrt(ext[0] * ext[1] * ext[2] * target / std::max<double>((double)n, 1.0));
+        double emax = std::max(ext[0], std::max(ext[1], ext[2]));
+        if (!(h > emax * 1e-7)) h = emax * 1e-7;
+        if (!(h > 0)) h = 1.0;
+    }
+    uint32_t* count = nullptr;
+    uint32_t* rank = nullptr;
+    if ((rc = dmalloc(ctx, &rank, n + 1))) { hipFree(cxyz); return fail(rc); }
+    for (int attempt = 0; attempt < 3; attempt++) {
+        GridDesc g{};
+        while (!make_geometry(g, mn, mx, h, cap)) h *= 2.0;
+        hipFree(ix->brick); ix->brick = nullptr;
+        hipFree(count); count = nullptr;
+        if ((rc = dmalloc(ctx, &ix->brick, g.nbricks))) break;
+        PCP_HIP(ctx, hipMemsetAsync(ix->brick, 0, (size_t)g.nbricks * sizeof(int32_t), st));
+        if (n > 0) hipLaunchKernelGGL(k_mark<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, ix->brick);
+        const int64_t nbw = (g.nbricks + 31) / 32;
+        uint32_t* bbits;
+        if ((rc = dmalloc(ctx, &bbits, nbw + 1))) break;
+        hipLaunchKernelGGL(k_brick_bits, dim3(grid_for(nbw, kB)), dim3(kB), 0, st, ix->brick, g.nbricks, bbits);
+        uint32_t nslots = 0;
+        rc = scan_u32_inplace(ctx, (uint32_t*)ix->brick, g.nbricks, &nslots);
+        if (rc) { hipFree(bbits); break; }
+        hipLaunchKernelGGL(k_brick_final, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks, bbits);
+        hipFree(bbits);
+        g.nslots = nslots;
+        g.brick = ix->brick;
+        const int64_t ncells = (int64_t)nslots * 64;
+        if ((rc = dmalloc(ctx, &count, ncells + 1))) break;
+        PCP_HIP(ctx, hipMemsetAsync(count, 0, (size_t)(ncells + 1) * sizeof(uint32_t), st));
+        if (n > 0) hipLaunchKernelGGL(k_count<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, count, rank);
+        if (auto_h && attempt < 2 && n > 0) {
+            unsigned long long* d_ne;
+            if ((rc = dmalloc(ctx, &d_ne, 1))) break;
+            PCP_HIP(ctx, hipMemsetAsync(d_ne, 0, sizeof(unsigned long long), st));
+            hipLaunchKernelGGL(k_nonempty, dim3(grid_for(ncells, kB, 4096)), dim3(kB), 0, st, count, ncells, d_ne);
+            unsigned long long ne = 0;
+            hipMemcpyAsync(&ne, d_ne, sizeof(ne), hipMemcpyDeviceToHost, st);
+            hipStreamSynchronize(st);
+            hipFree(d_ne);
+            double occ = (double)n / std::max(1.0, (double)ne);
+            if (occ > 12.0) { h *= std::sqrt(4.0 / occ); continue; }   // surface-like data
+            if (occ < 1.5) { h *= std::cbrt(4.0 / occ); continue; }    // sparser than assumed
+        }
+        // ---- cell starts + scatter
+        rc = scan_u32_inplace(ctx, count, ncells + 1, nullptr);
+        if (rc) break;
+        g.cstart = count;
+        ix->g = g;
+        ix->cstart = count;
+        count = nullptr;
+        using V4 = typename Real<T>::V4;
+        if ((rc = dmalloc(ctx, (V4**)&ix->pts, n + 1)) || (rc = dmalloc(ctx, &ix->sorted_j, n + 1))) break;
+        if (n > 0)
+            hipLaunchKernelGGL(k_scatter<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, rank,
+                               ix->mapping, (V4*)ix->pts, ix->sorted_j, is_f64);
+        break;
+    }
+    hipFree(count);
+    hipFree(rank);
+    hipFree(cxyz);
+    if (rc) return fail(rc);
+    PCP_HIP(ctx, hipGetLastError());
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    *out = ix;
+    return PCP_OK;
+}
+
+}  // namespace
+}  // namespace pcp
+
+extern "C" {
+
+int pcp_index_build_f64(pcp_ctx* ctx, const double* xyz, size_t stride, int64_t n,
+                        const int32_t* indices, int64_t n_indices, double cell_size, pcp_index** out) {
+    if (stride == 0) stride = 3 * sizeof(double);
+    return pcp::build_impl<double>(ctx, xyz, stride, indices ? n_indices : n, indices, cell_size, 1, out);
+}
+
+int pcp_index_build_f32(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size,
+                        pcp_index** out) {
+    if (stride == 0) stride = 3 * sizeof(float);
+    return pcp::build_impl<float>(ctx, xyz, stride, n, nullptr, cell_size, 0, out);
+}
+
+int pcp_index_destroy(pcp_index* ix) {
+    if (!ix) return PCP_ERR_ARG;
+    if (ix->owner) (void)hipSetDevice(ix->owner->device);
+    hipFree(ix->brick);
+    hipFree(ix->cstart);
+    hipFree(ix->pts);
+    hipFree(ix->mapping);
+    hipFree(ix->sorted_j);
+    delete ix;
+    return PCP_OK;
+}
+
+int64_t pcp_index_size(const pcp_index* ix) { return ix ? ix->n : -1; }
+int pcp_index_identity_mapping(const pcp_index* ix) { return ix ? ix->identity : 0; }
+double pcp_index_cell_size(const pcp_index* ix) { return ix ? ix->g.h : 0.0; }
+int64_t pcp_index_cells(const pcp_index* ix) { return ix ? ix->g.nslots * 64 : 0; }
+const void* pcp_index_sorted_points(const pcp_index* ix) { return ix ? ix->pts : nullptr; }
+
+}  // extern "C"

@@ -1,0 +1,118 @@
+// Device-side view of the uniform-grid index and the exact ring search shared by the
+// kNN / radius / normals / ICP kernels.
+//
+// Cells: c_a = floor((v_a - o_a) * inv_h) in the index precision (float for the fp32
+// ICP index, double for the fp64 FLANN-contract index), identical in build and search.
+// Bricks of 4x4x4 cells; brick table -> slot; cell (slot, local) owns sorted points
+// [cstart[64*slot+local], cstart[64*slot+local+1]).
+#pragma once
+#include "common.hpp"
+
+namespace pcp {
+
+template <typename T> struct Real;
+template <> struct Real<float> {
+    using V4 = float4;
+    __device__ static float floor_(float x) { return floorf(x); }
+};
+template <> struct Real<double> {
+    using V4 = double4;
+    __device__ static double floor_(double x) { return floor(x); }
+};
+
+template <typename T> __device__ __forceinline__ T g_o(const GridDesc& g, int a);
+template <> __device__ __forceinline__ float g_o<float>(const GridDesc& g, int a) { return g.of[a]; }
+template <> __device__ __forceinline__ double g_o<double>(const GridDesc& g, int a) { return g.o[a]; }
+template <typename T> __device__ __forceinline__ T g_inv(const GridDesc& g);
+template <> __device__ __forceinline__ float g_inv<float>(const GridDesc& g) { return g.inv_hf; }
+template <> __device__ __forceinline__ double g_inv<double>(const GridDesc& g) { return g.inv_h; }
+
+// continuous cell coordinate (unclamped, saturated to +-2^30 to keep int conversion safe)
+template <typename T>
+__device__ __forceinline__ T cell_f(const GridDesc& g, T v, int a) {
+    T f = (v - g_o<T>(g, a)) * g_inv<T>(g);
+    f = f < (T)-1073741824.0 ? (T)-1073741824.0 : f;
+    f = f > (T)1073741824.0 ? (T)1073741824.0 : f;
+    return f;
+}
+
+template <typename T>
+__device__ __forceinline__ int cell_i(const GridDesc& g, T v, int a) {
+    return (int)Real<T>::floor_(cell_f<T>(g, v, a));
+}
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__device__ __forceinline__ int64_t brick_of(const GridDesc& g, int cx, int cy, int cz) {
+    return ((int64_t)(cz >> 2) * g.nb[1] + (cy >> 2)) * g.nb[0] + (cx >> 2);
+}
+__device__ __forceinline__ int local_of(int cx, int cy, int cz) {
+    return (cx & 3) | ((cy & 3) << 2) | ((cz & 3) << 4);
+}
+
+// point range of an in-range cell; returns false when the cell is empty
+__device__ __forceinline__ bool cell_range(const GridDesc& g, int cx, int cy, int cz,
+                                           uint32_t& s, uint32_t& e) {
+    const int32_t slot = g.brick[brick_of(g, cx, cy, cz)];
+    if (slot < 0) return false;
+    const int64_t c = (int64_t)slot * 64 + local_of(cx, cy, cz);
+    s = g.cstart[c];
+    e = g.cstart[c + 1];
+    return e > s;
+}
+
+// Exact ring search over cells in order of Chebyshev distance from the query's cell.
+//   V::bound()       current pruning radius^2 (in the index precision's units), may shrink
+//   V::visit(s, e)   scan sorted points [s,e)
+// Cells (and whole rings) whose box distance exceeds bound() (with a conservative margin
+// `mc` in cell units covering floor() rounding of both the cells and the query) are skipped
+// without touching memory.  Visiting order never changes the result: visitors keep a
+// lexicographic (d2, index) order.
+template <typename T, typename Vis>
+__device__ __forceinline__ void ring_search(const GridDesc& g, T qx, T qy, T qz, T mc, Vis& vis) {
+    const T fx = cell_f<T>(g, qx, 0), fy = cell_f<T>(g, qy, 1), fz = cell_f<T>(g, qz, 2);
+    const int cx = (int)Real<T>::floor_(fx), cy = (int)Real<T>::floor_(fy), cz = (int)Real<T>::floor_(fz);
+    // offsets inside the query's own cell
+    const T lx = fx - (T)cx, ly = fy - (T)cy, lz = fz - (T)cz;
+    const T h = (T)g.h;
+    const T dmin = fmin(fmin(fmin(lx, (T)1 - lx), fmin(ly, (T)1 - ly)), fmin(lz, (T)1 - lz));
+    // the furthest ring that can still intersect the grid
+    int far = 0;
+    far = max(far, max(cx - (g.n[0] - 1), -cx));
+    far = max(far, max(cy - (g.n[1] - 1), -cy));
+    far = max(far, max(cz - (g.n[2] - 1), -cz));
+    const int rmax = far + max(g.n[0], max(g.n[1], g.n[2]));
+    for (int s = 0; s <= rmax; s++) {
+        if (s > 0) {
+            const T rmin = ((T)(s - 1) + dmin - mc);
+            if (rmin > (T)0 && rmin * rmin * h * h > vis.bound()) break;
+        }
+        const int z0 = max(cz - s, 0), z1 = min(cz + s, g.n[2] - 1);
+        const int y0 = max(cy - s, 0), y1 = min(cy + s, g.n[1] - 1);
+        const int x0 = max(cx - s, 0), x1 = min(cx + s, g.n[0] - 1);
+        if (z0 > z1 || y0 > y1 || x0 > x1) continue;
+        for (int z = z0; z <= z1; z++) {
+            const bool zface = (z == cz - s) || (z == cz + s);
+            const T gz = z < cz ? (lz + (T)(cz - z - 1)) : (z > cz ? ((T)1 - lz + (T)(z - cz - 1)) : (T)0);
+            const T gz2 = gz > mc ? (gz - mc) * (gz - mc) : (T)0;
+            if (gz2 * h * h > vis.bound()) continue;
+            for (int y = y0; y <= y1; y++) {
+                const bool yface = zface || (y == cy - s) || (y == cy + s);
+                const T gy = y < cy ? (ly + (T)(cy - y - 1)) : (y > cy ? ((T)1 - ly + (T)(y - cy - 1)) : (T)0);
+                const T gyz2 = gz2 + (gy > mc ? (gy - mc) * (gy - mc) : (T)0);
+                if (gyz2 * h * h > vis.bound()) continue;
+                const int step = yface ? 1 : 2 * s;
+                for (int x = yface ? x0 : cx - s; x <= x1; x += (step > 0 ? step : 1)) {
+                    if (x < x0) continue;
+                    const T gx = x < cx ? (lx + (T)(cx - x - 1)) : (x > cx ? ((T)1 - lx + (T)(x - cx - 1)) : (T)0);
+                    const T g2 = gyz2 + (gx > mc ? (gx - mc) * (gx - mc) : (T)0);
+                    if (g2 * h * h > vis.bound()) continue;
+                    uint32_t st, en;
+                    if (cell_range(g, x, y, z, st, en)) vis.visit(st, en);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace pcp

@@ -1,0 +1,280 @@
+"""Python host layer over the C-ABI (include/pcp.h) for device-resident clouds.
+
+torch is plumbing only: it owns device memory and the stream; every computation is a
+libpcp HIP kernel.  Clouds in the reference layout (PointXYZRGBA, point_type.h:9-82) are
+uint8 tensors of shape (n, 48); xyz clouds are float64/float32 tensors of shape (n, 3).
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+POINT48 = np.dtype(
+    [("x", "<f8"), ("y", "<f8"), ("z", "<f8"), ("w", "<f8"), ("rgba", "<u4"),
+     ("stamp_id", "<u4"), ("pad", "<u4", (2,))])
+PLANE = np.dtype([("normal_x", "<f4"), ("normal_y", "<f4"), ("normal_z", "<f4"),
+                  ("min_value", "<f4"), ("curvature", "<f4"), ("distance", "<f4")])
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Context:
+    """pcp_ctx bound to a device and to torch's current stream on that device."""
+
+    def __init__(self, device=0):
+        self.lib = _lib.load()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        idx = self.device.index or 0
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        h = C.c_void_p()
+        rc = self.lib.pcp_ctx_create(idx, C.c_void_p(stream), C.byref(h))
+        if rc != 0:
+            raise _lib.PcpError(rc, f"pcp_ctx_create(device={idx}) failed")
+        self.h = h
+
+    def check(self, rc):
+        return check(rc, self.h)
+
+    def sync(self):
+        self.check(self.lib.pcp_sync(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pcp_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def cloud_to_device(cloud_np, device):
+    """numpy POINT48 structured array -> (n, 48) uint8 device tensor."""
+    arr = np.ascontiguousarray(cloud_np)
+    assert arr.dtype.itemsize == 48
+    t = torch.from_numpy(arr.view(np.uint8).reshape(len(arr), 48))
+    return t.to(device)
+
+
+def cloud_to_host(t):
+    a = t.detach().cpu().contiguous().numpy().reshape(-1)
+    return a.view(POINT48)
+
+
+class GridIndex:
+    """pcp_index over a cloud.  fp64 (KdTreeFLANN contract) or fp32 (ICP target)."""
+
+    def __init__(self, ctx, xyz, cell_size=0.0, indices=None, stride_bytes=None):
+        self.ctx = ctx
+        lib = ctx.lib
+        self.src = xyz  # keep alive
+        h = C.c_void_p()
+        n = xyz.shape[0]
+        if xyz.dtype == torch.uint8:  # AoS48
+            stride = 48
+            self.f64 = True
+        else:
+            self.f64 = xyz.dtype == torch.float64
+            stride = stride_bytes or xyz.stride(0) * xyz.element_size()
+        if self.f64:
+            self.indices = None if indices is None else indices.to(ctx.device, torch.int32).contiguous()
+            ni = 0 if self.indices is None else self.indices.numel()
+            ctx.check(lib.pcp_index_build_f64(ctx.h, _ptr(xyz), stride, n, _ptr(self.indices), ni,
+                                              float(cell_size), C.byref(h)))
+        else:
+            if indices is not None:
+                raise ValueError("fp32 index does not take an indices subset")
+            ctx.check(lib.pcp_index_build_f32(ctx.h, _ptr(xyz), stride, n, float(cell_size), C.byref(h)))
+        self.h = h
+
+    @property
+    def size(self):
+        return self.ctx.lib.pcp_index_size(self.h)
+
+    @property
+    def cell_size(self):
+        return self.ctx.lib.pcp_index_cell_size(self.h)
+
+    @property
+    def identity_mapping(self):
+        return bool(self.ctx.lib.pcp_index_identity_mapping(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.pcp_index_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def _qstride(q):
+    if q.dtype == torch.uint8:
+        return 48
+    return q.stride(0) * q.element_size()
+
+
+def knn(index, q, k):
+    """Batch nearestKSearch: (nq, k) int32 indices and float64 sqr distances."""
+    ctx = index.ctx
+    nq = q.shape[0]
+    idx = torch.empty((nq, k), dtype=torch.int32, device=ctx.device)
+    d2 = torch.empty((nq, k), dtype=torch.float64, device=ctx.device)
+    ctx.check(ctx.lib.pcp_knn(ctx.h, index.h, _ptr(q), _qstride(q), nq, int(k), _ptr(idx), _ptr(d2)))
+    return idx, d2
+
+
+def radius(index, q, r, max_nn=0):
+    """Batch radiusSearch -> CSR (offsets int64 (nq+1), idx int32, d2 float64)."""
+    ctx = index.ctx
+    nq = q.shape[0]
+    cnt = torch.empty(nq, dtype=torch.int32, device=ctx.device)
+    ctx.check(ctx.lib.pcp_radius_count(ctx.h, index.h, _ptr(q), _qstride(q), nq, float(r), int(max_nn),
+                                       _ptr(cnt)))
+    offs = torch.empty(nq + 1, dtype=torch.int64, device=ctx.device)
+    total = C.c_int64()
+    ctx.check(ctx.lib.pcp_scan_counts(ctx.h, _ptr(cnt), nq, _ptr(offs), C.byref(total)))
+    idx = torch.empty(max(total.value, 1), dtype=torch.int32, device=ctx.device)
+    d2 = torch.empty(max(total.value, 1), dtype=torch.float64, device=ctx.device)
+    ctx.check(ctx.lib.pcp_radius_fill(ctx.h, index.h, _ptr(q), _qstride(q), nq, float(r), int(max_nn),
+                                      _ptr(offs), _ptr(idx), _ptr(d2)))
+    return offs, idx[:total.value], d2[:total.value]
+
+
+def knn_bruteforce(ctx, target, q, k):
+    nt, nq = target.shape[0], q.shape[0]
+    idx = torch.empty((nq, k), dtype=torch.int32, device=ctx.device)
+    d2 = torch.empty((nq, k), dtype=torch.float64, device=ctx.device)
+    ctx.check(ctx.lib.pcp_knn_bruteforce(ctx.h, _ptr(target), _qstride(target), nt, _ptr(q), _qstride(q),
+                                         nq, int(k), _ptr(idx), _ptr(d2)))
+    return idx, d2
+
+
+def knn_lod(ctx, cloud, q, k):
+    nq = q.shape[0]
+    idx = torch.empty((nq, k), dtype=torch.int32, device=ctx.device)
+    d2 = torch.empty((nq, k), dtype=torch.float64, device=ctx.device)
+    ctx.check(ctx.lib.pcp_knn_lod(ctx.h, _ptr(cloud), cloud.shape[0], _ptr(q), nq, int(k), _ptr(idx),
+                                  _ptr(d2)))
+    return idx, d2
+
+
+def minmax(ctx, cloud, is_dense=True):
+    mn, mx = (C.c_double * 4)(), (C.c_double * 4)()
+    ctx.check(ctx.lib.pcp_minmax_aos48(ctx.h, _ptr(cloud), cloud.shape[0], int(is_dense), mn, mx))
+    return np.array(mn[:]), np.array(mx[:])
+
+
+def centroid(ctx, cloud, is_dense=True):
+    c = (C.c_double * 4)()
+    cnt = C.c_uint32()
+    ctx.check(ctx.lib.pcp_centroid_aos48(ctx.h, _ptr(cloud), cloud.shape[0], int(is_dense), c,
+                                         C.byref(cnt)))
+    return np.array(c[:]), cnt.value
+
+
+def transform(ctx, cloud, T, is_dense=True, out=None):
+    out = torch.empty_like(cloud) if out is None else out
+    Tm = _lib.f64arr(np.asarray(T, dtype=np.float64).reshape(16))
+    ctx.check(ctx.lib.pcp_transform_aos48(ctx.h, _ptr(cloud), _ptr(out), cloud.shape[0], int(is_dense), Tm))
+    return out
+
+
+def voxel_filter(ctx, cloud, leaf, is_dense=True, downsample_all=True, with_voxel_idx=False):
+    n = cloud.shape[0]
+    out = torch.empty((max(n, 1), 48), dtype=torch.uint8, device=ctx.device)
+    vidx = torch.empty(max(n, 1), dtype=torch.int32, device=ctx.device) if with_voxel_idx else None
+    lf = (leaf, leaf, leaf) if np.isscalar(leaf) else tuple(leaf)
+    nout = C.c_int64()
+    ctx.check(ctx.lib.pcp_voxel_filter(ctx.h, _ptr(cloud), n, int(is_dense), _lib.f64arr(lf),
+                                       int(downsample_all), _ptr(out), C.byref(nout), _ptr(vidx)))
+    m = nout.value
+    if with_voxel_idx:
+        return out[:m], vidx[:m].view(torch.int32)
+    return out[:m]
+
+
+def remove_duplicate(ctx, cloud, leaf, is_dense=True):
+    n = cloud.shape[0]
+    out = torch.empty((max(n, 1), 48), dtype=torch.uint8, device=ctx.device)
+    nout = C.c_int64()
+    ctx.check(ctx.lib.pcp_remove_duplicate(ctx.h, _ptr(cloud), n, int(is_dense), float(leaf), _ptr(out),
+                                           C.byref(nout)))
+    return out[:nout.value]
+
+
+def normals_knn(index, k):
+    ctx = index.ctx
+    n = ctx.lib.pcp_index_size(index.h)
+    n_out = index.src.shape[0] if index.indices is None else index.indices.numel()
+    out = torch.empty((max(n_out, 1), 6), dtype=torch.float32, device=ctx.device)
+    ctx.check(ctx.lib.pcp_normals_knn(ctx.h, index.h, int(k), _ptr(out), n_out))
+    return out[:n_out]
+
+
+class ICP:
+    """Device-resident ICP of a query set against an fp32 grid index (the target)."""
+
+    def __init__(self, target_index, q):
+        self.index = target_index
+        self.ctx = ctx = target_index.ctx
+        self.q = q
+        h = C.c_void_p()
+        ctx.check(ctx.lib.pcp_icp_create(ctx.h, target_index.h, _ptr(q), q.stride(0) * q.element_size(),
+                                         q.shape[0], C.byref(h)))
+        self.h = h
+        self.acc = torch.zeros(24, dtype=torch.float64, device=ctx.device)
+
+    def step(self, T, rmax, corr=False):
+        """One iteration at pose T; returns the (device) accumulators (+ correspondences)."""
+        ctx = self.ctx
+        Tm = _lib.f64arr(np.asarray(T, dtype=np.float64).reshape(16))
+        ci = cd = None
+        if corr:
+            ci = torch.empty(self.q.shape[0], dtype=torch.int32, device=ctx.device)
+            cd = torch.empty(self.q.shape[0], dtype=torch.float32, device=ctx.device)
+        ctx.check(ctx.lib.pcp_icp_step(ctx.h, self.h, Tm, float(rmax), _ptr(self.acc), _ptr(ci), _ptr(cd)))
+        return (self.acc, ci, cd) if corr else self.acc
+
+    def run(self, T0, rmax, iters, do_scale=False, eps=0.0):
+        ctx = self.ctx
+        T = _lib.f64arr(np.asarray(T0, dtype=np.float64).reshape(16))
+        err = C.c_float()
+        rc = ctx.lib.pcp_icp_run(ctx.h, self.h, T, float(rmax), int(iters), int(do_scale), float(eps),
+                                 C.byref(err))
+        if rc not in (0, -6):
+            ctx.check(rc)
+        return float(err.value), np.array(T[:]).reshape(4, 4)
+
+    def last_kernel_ms(self):
+        ms, n = C.c_double(), C.c_int()
+        self.ctx.check(self.ctx.lib.pcp_icp_last_kernel_ms(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.pcp_icp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def icp_solve(acc, do_scale=False):
+    a = np.asarray(acc, dtype=np.float64).reshape(24)
+    dT = (C.c_double * 16)()
+    rc = _lib.load().pcp_icp_solve(_lib.f64arr(a), int(do_scale), dT)
+    return rc, np.array(dT[:]).reshape(4, 4)
+
+
+def get_rot_icp(ctx, src, temp, rmax, iters=20, do_scale=False, cell_size=0.0):
+    M = (C.c_double * 16)()
+    err = C.c_float()
+    ctx.check(ctx.lib.pcp_get_rot_icp(ctx.h, _ptr(src), src.shape[0], _ptr(temp), temp.shape[0], M,
+                                      float(rmax), int(iters), int(do_scale), float(cell_size),
+                                      C.byref(err)))
+    return float(err.value), np.array(M[:]).reshape(4, 4)
