@@ -108,6 +108,7 @@ def main():
             if timed:
                 kernel["ms"] += ms
                 kernel["launches"] += nl
+                kernel["fallback"] = kernel.get("fallback", 0) + icp.last_fallback()
             if world > 1:
                 acc_buf.copy_(acc)
                 dist.all_reduce(acc_buf)
@@ -180,6 +181,8 @@ def main():
                 "kernel_avg_ms": round(k_avg_ms, 4),
                 "bytes_per_unit": BYTES_PER_CORR,
                 "units_per_launch": n,
+                "launch_includes": "k_icp_octant + k_icp_ring (fallback) per iteration",
+                "fallback_frac": round(kernel.get("fallback", 0) / max(1, n * kernel["launches"]), 5),
             },
             "cpu_baseline": None if args.no_cpu else cpu_baseline(args, T_true),
         }

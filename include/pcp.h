@@ -164,7 +164,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q_dev,
                    size_t q_stride_bytes, int64_t nq, pcp_icp** out);
 int pcp_icp_destroy(pcp_icp* icp);
 /* One iteration at pose T (row-major 4x4 double, cast to fp32 for the kernel):
- * correspondences within rmax + the 24 accumulators written to acc_dev
+ * correspondences within rmax + the 24 accumulators ([23] = queries that
+ * needed the exact fallback search, a diagnostic) written to acc_dev
  * (device, 24 doubles).  corr_idx_dev / corr_d2_dev (optional, nq each) receive the
  * winner per query in the ORIGINAL query order (-1 / +inf when rejected). */
 int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T_host[16], float rmax,
@@ -179,6 +180,9 @@ int pcp_icp_run(pcp_ctx* ctx, pcp_icp* icp, double T_inout[16], float rmax, int 
 /* Device time (ms) of the last pcp_icp_step/pcp_icp_run correspondence kernels
  * (sum over iterations) and the number of launches it covers, from hipEvents. */
 int pcp_icp_last_kernel_ms(const pcp_icp* icp, double* ms, int* launches);
+/* Queries of the last pcp_icp_step that needed the exact ring-search fallback (the fast
+ * octant pass could not certify their nearest neighbour). */
+int pcp_icp_last_fallback(const pcp_icp* icp, int64_t* n);
 
 /* PointCloudHelper::get_rot_icp (point_cloud_helper.cpp:75-166) on AoS48 clouds:
  * joint centroid, float cast, ICP(query = temp -> target = src), un-centring

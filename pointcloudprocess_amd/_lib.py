@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpcp.so")
+LIB_PATH = os.environ.get("PCP_LIB") or os.path.join(HERE, "libpcp.so")  # PCP_LIB: A/B builds
 
 PCP_OK = 0
 _STATUS = {
@@ -58,6 +58,7 @@ SIGNATURES = [
     ("pcp_icp_solve", _i32, [_P(_f64), _i32, _P(_f64)]),
     ("pcp_icp_run", _i32, [_vp, _vp, _P(_f64), _f32, _i32, _i32, _f64, _P(_f32)]),
     ("pcp_icp_last_kernel_ms", _i32, [_vp, _P(_f64), _P(_i32)]),
+    ("pcp_icp_last_fallback", _i32, [_vp, _P(_i64)]),
     ("pcp_get_rot_icp", _i32, [_vp, _vp, _i64, _vp, _i64, _P(_f64), _f32, _i32, _i32, _f64,
                                _P(_f32)]),
 ]

@@ -71,9 +71,11 @@ int scan_u32_inplace(pcp_ctx* ctx, uint32_t* data, int64_t n, uint32_t* total_ho
 int scan_i32_to_i64(pcp_ctx* ctx, const int32_t* in, int64_t n, int64_t* out, int64_t* total_host);
 
 // ---------------------------------------------------------------- grid description
-// Uniform grid of cubic cells, grouped into 4x4x4 bricks.  A dense brick table maps a
-// brick to a slot (or -1); each slot owns 64 consecutive entries of cell_start, so the
-// points of cell (slot, local) are sorted[cell_start[64*slot+local] .. cell_start[.. +1]).
+// Uniform grid of cubic cells.  Dense mode (the MI355X default whenever the table fits the
+// HBM budget): cstart has one entry per cell of the bounding grid, linear id
+// (z*ny + y)*nx + x, so a row of cells along x is one contiguous point range.  Sparse
+// mode (huge sparse bounding boxes): 4x4x4 bricks, a dense brick table maps a brick to a
+// slot (or -1) and each slot owns 64 consecutive cstart entries.
 struct GridDesc {
     double o[3];      // origin (bbox min)
     double h, inv_h;  // cell size
@@ -83,9 +85,14 @@ struct GridDesc {
     int nb[3];        // bricks per axis
     int64_t nbricks;
     int64_t nslots;
-    const int32_t* brick;     // nbricks
-    const uint32_t* cstart;   // 64*nslots + 1
+    int dense;                // 1: cstart is indexed by the linear cell id (x fastest)
+    int64_t ncells;           // dense: n[0]*n[1]*n[2]
+    const int32_t* brick;     // nbricks (sparse mode only)
+    const uint32_t* cstart;   // dense: ncells + 1 ; sparse: 64*nslots + 1
 };
+
+int index_build_f32_bricks(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size,
+                           pcp_index** out);
 
 }  // namespace pcp
 

@@ -129,8 +129,34 @@ __global__ void k_count(GridDesc g, const T* cxyz, int64_t n, uint32_t* count, u
          i += (int64_t)gridDim.x * blockDim.x) {
         int cx, cy, cz;
         cell_of_point<T>(g, cxyz + 3 * i, cx, cy, cz);
-        int64_t c = (int64_t)g.brick[brick_of(g, cx, cy, cz)] * 64 + local_of(cx, cy, cz);
-        rank[i] = atomicAdd(&count[c], 1u);
+        rank[i] = atomicAdd(&count[cell_id(g, cx, cy, cz)], 1u);
+    }
+}
+
+// (x, tie) key of a sorted point: tie = caller index bits (fp32) or internal j (fp64)
+__device__ __forceinline__ bool key_less(const float4& a, const float4& b) {
+    return a.x < b.x || (a.x == b.x && __float_as_int(a.w) < __float_as_int(b.w));
+}
+__device__ __forceinline__ bool key_less(const double4& a, const double4& b) {
+    return a.x < b.x || (a.x == b.x && a.w < b.w);
+}
+
+// rank sort inside each cell: position = cell start + #(points of the cell with a smaller key)
+template <typename T>
+__global__ void k_cell_sort(GridDesc g, const typename Real<T>::V4* pts, const int32_t* sj, int64_t n,
+                            typename Real<T>::V4* out, int32_t* sj_out) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const typename Real<T>::V4 p = pts[k];
+        const T c3[3] = {p.x, p.y, p.z};
+        int cx, cy, cz;
+        cell_of_point<T>(g, c3, cx, cy, cz);
+        const int64_t c = cell_id(g, cx, cy, cz);
+        const uint32_t s = g.cstart[c], e = g.cstart[c + 1];
+        uint32_t r = 0;
+        for (uint32_t j = s; j < e; j++) r += key_less(pts[j], p) ? 1u : 0u;
+        out[s + r] = p;
+        sj_out[s + r] = sj[k];
     }
 }
 
@@ -152,8 +178,7 @@ __global__ void k_scatter(GridDesc g, const T* cxyz, int64_t n, const uint32_t* 
         int cx, cy, cz;
         const T* p = cxyz + 3 * i;
         cell_of_point<T>(g, p, cx, cy, cz);
-        int64_t c = (int64_t)g.brick[brick_of(g, cx, cy, cz)] * 64 + local_of(cx, cy, cz);
-        uint32_t dst = g.cstart[c] + rank[i];
+        uint32_t dst = g.cstart[cell_id(g, cx, cy, cz)] + rank[i];
         typename Real<T>::V4 v;
         v.x = p[0]; v.y = p[1]; v.z = p[2];
         if (is_f64) v.w = (T)(double)i;                     // internal j (FLANN tie order)
@@ -187,7 +212,7 @@ bool make_geometry(GridDesc& g, const double mn[3], const double mx[3], double h
 
 template <typename T>
 int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const int32_t* indices,
-               double cell_size, int is_f64, pcp_index** out) {
+               double cell_size, int is_f64, pcp_index** out, bool force_sparse = false) {
     if (!ctx || !out || n_in < 0 || (n_in > 0 && !xyz)) return PCP_ERR_ARG;
     if (n_in >= (int64_t)1 << 31) return set_error(ctx, PCP_ERR_ARG, "index supports < 2^31 points");
     PCP_HIP(ctx, hipSetDevice(ctx->device));
@@ -250,6 +275,8 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
 
     // ---- cell size: given, or a density estimate refined once from the measured occupancy
     const int64_t cap = std::max<int64_t>((int64_t)1 << 24, 8 * n);
+    // dense cell table budget: up to 16 cells per point (<= 6.4 GB for 100M points), < 2^31
+    const int64_t dense_cap = std::min<int64_t>(((int64_t)1 << 31) - 2, std::max<int64_t>((int64_t)1 << 26, 16 * n));
     double ext[3];
     for (int a = 0; a < 3; a++) ext[a] = std::max(mx[a] - mn[a], 1e-9);
     const bool auto_h = !(cell_size > 0);
@@ -269,21 +296,31 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         while (!make_geometry(g, mn, mx, h, cap)) h *= 2.0;
         hipFree(ix->brick); ix->brick = nullptr;
         hipFree(count); count = nullptr;
-        if ((rc = dmalloc(ctx, &ix->brick, g.nbricks))) break;
-        PCP_HIP(ctx, hipMemsetAsync(ix->brick, 0, (size_t)g.nbricks * sizeof(int32_t), st));
-        if (n > 0) hipLaunchKernelGGL(k_mark<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, ix->brick);
-        const int64_t nbw = (g.nbricks + 31) / 32;
-        uint32_t* bbits;
-        if ((rc = dmalloc(ctx, &bbits, nbw + 1))) break;
-        hipLaunchKernelGGL(k_brick_bits, dim3(grid_for(nbw, kB)), dim3(kB), 0, st, ix->brick, g.nbricks, bbits);
-        uint32_t nslots = 0;
-        rc = scan_u32_inplace(ctx, (uint32_t*)ix->brick, g.nbricks, &nslots);
-        if (rc) { hipFree(bbits); break; }
-        hipLaunchKernelGGL(k_brick_final, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks, bbits);
-        hipFree(bbits);
-        g.nslots = nslots;
-        g.brick = ix->brick;
-        const int64_t ncells = (int64_t)nslots * 64;
+        const int64_t ncells_dense = (int64_t)g.n[0] * g.n[1] * g.n[2];
+        g.dense = (!force_sparse && ncells_dense <= dense_cap) ? 1 : 0;
+        g.ncells = ncells_dense;
+        int64_t ncells;
+        if (g.dense) {
+            ncells = ncells_dense;
+            g.nslots = 0;
+            g.brick = nullptr;
+        } else {
+            if ((rc = dmalloc(ctx, &ix->brick, g.nbricks))) break;
+            PCP_HIP(ctx, hipMemsetAsync(ix->brick, 0, (size_t)g.nbricks * sizeof(int32_t), st));
+            if (n > 0) hipLaunchKernelGGL(k_mark<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, ix->brick);
+            const int64_t nbw = (g.nbricks + 31) / 32;
+            uint32_t* bbits;
+            if ((rc = dmalloc(ctx, &bbits, nbw + 1))) break;
+            hipLaunchKernelGGL(k_brick_bits, dim3(grid_for(nbw, kB)), dim3(kB), 0, st, ix->brick, g.nbricks, bbits);
+            uint32_t nslots = 0;
+            rc = scan_u32_inplace(ctx, (uint32_t*)ix->brick, g.nbricks, &nslots);
+            if (rc) { hipFree(bbits); break; }
+            hipLaunchKernelGGL(k_brick_final, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks, bbits);
+            hipFree(bbits);
+            g.nslots = nslots;
+            g.brick = ix->brick;
+            ncells = (int64_t)nslots * 64;
+        }
         if ((rc = dmalloc(ctx, &count, ncells + 1))) break;
         PCP_HIP(ctx, hipMemsetAsync(count, 0, (size_t)(ncells + 1) * sizeof(uint32_t), st));
         if (n > 0) hipLaunchKernelGGL(k_count<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, count, rank);
@@ -309,9 +346,22 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         count = nullptr;
         using V4 = typename Real<T>::V4;
         if ((rc = dmalloc(ctx, (V4**)&ix->pts, n + 1)) || (rc = dmalloc(ctx, &ix->sorted_j, n + 1))) break;
-        if (n > 0)
+        if (n > 0) {
             hipLaunchKernelGGL(k_scatter<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, rank,
                                ix->mapping, (V4*)ix->pts, ix->sorted_j, is_f64);
+            // order each cell by (x, index): a dense-grid row of cells is then one x-sorted run
+            V4* pts2;
+            int32_t* sj2;
+            if ((rc = dmalloc(ctx, &pts2, n + 1))) break;
+            if ((rc = dmalloc(ctx, &sj2, n + 1))) { hipFree(pts2); break; }
+            hipLaunchKernelGGL(k_cell_sort<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const V4*)ix->pts,
+                               (const int32_t*)ix->sorted_j, n, pts2, sj2);
+            PCP_HIP(ctx, hipStreamSynchronize(st));
+            hipFree(ix->pts);
+            hipFree(ix->sorted_j);
+            ix->pts = pts2;
+            ix->sorted_j = sj2;
+        }
         break;
     }
     hipFree(count);
@@ -325,6 +375,15 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
 }
 
 }  // namespace
+
+// Brick-ordered (4x4x4-cell bricks, x-fastest brick order) index: used to give ICP query
+// sets a spatially compact order (a chunk of consecutive queries spans a few bricks).
+int index_build_f32_bricks(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size,
+                           pcp_index** out) {
+    if (stride == 0) stride = 3 * sizeof(float);
+    return build_impl<float>(ctx, xyz, stride, n, nullptr, cell_size, 0, out, true);
+}
+
 }  // namespace pcp
 
 extern "C" {
@@ -356,7 +415,7 @@ int pcp_index_destroy(pcp_index* ix) {
 int64_t pcp_index_size(const pcp_index* ix) { return ix ? ix->n : -1; }
 int pcp_index_identity_mapping(const pcp_index* ix) { return ix ? ix->identity : 0; }
 double pcp_index_cell_size(const pcp_index* ix) { return ix ? ix->g.h : 0.0; }
-int64_t pcp_index_cells(const pcp_index* ix) { return ix ? ix->g.nslots * 64 : 0; }
+int64_t pcp_index_cells(const pcp_index* ix) { return ix ? (ix->g.dense ? ix->g.ncells : ix->g.nslots * 64) : 0; }
 const void* pcp_index_sorted_points(const pcp_index* ix) { return ix ? ix->pts : nullptr; }
 
 }  // extern "C"

@@ -50,12 +50,22 @@ __device__ __forceinline__ int local_of(int cx, int cy, int cz) {
     return (cx & 3) | ((cy & 3) << 2) | ((cz & 3) << 4);
 }
 
+__device__ __forceinline__ int64_t dense_id(const GridDesc& g, int cx, int cy, int cz) {
+    return ((int64_t)cz * g.n[1] + cy) * g.n[0] + cx;
+}
+
+// cstart index of an in-range cell, or -1 when its brick is empty (sparse mode)
+__device__ __forceinline__ int64_t cell_id(const GridDesc& g, int cx, int cy, int cz) {
+    if (g.dense) return dense_id(g, cx, cy, cz);
+    const int32_t slot = g.brick[brick_of(g, cx, cy, cz)];
+    return slot < 0 ? -1 : (int64_t)slot * 64 + local_of(cx, cy, cz);
+}
+
 // point range of an in-range cell; returns false when the cell is empty
 __device__ __forceinline__ bool cell_range(const GridDesc& g, int cx, int cy, int cz,
                                            uint32_t& s, uint32_t& e) {
-    const int32_t slot = g.brick[brick_of(g, cx, cy, cz)];
-    if (slot < 0) return false;
-    const int64_t c = (int64_t)slot * 64 + local_of(cx, cy, cz);
+    const int64_t c = cell_id(g, cx, cy, cz);
+    if (c < 0) return false;
     s = g.cstart[c];
     e = g.cstart[c + 1];
     return e > s;

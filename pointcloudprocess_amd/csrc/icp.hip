@@ -9,6 +9,7 @@
 // fixed-order pass over the workgroup partials.  The host solves the 3x3 Kabsch/Umeyama
 // problem (pcp_icp_solve) and composes the pose.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -17,20 +18,33 @@
 struct pcp_icp {
     pcp_ctx* ctx = nullptr;
     const pcp_index* target = nullptr;
-    int64_t nq = 0;
+    int64_t nq = 0;               // finite queries
+    int64_t nq_in = 0;            // queries passed to pcp_icp_create
     float4* q = nullptr;          // sorted queries {x,y,z,bits(original index)}
-    double* partials = nullptr;   // nblocks * 24
+    int32_t* win = nullptr;       // per sorted query: winning target index (-1 = rejected)
+    float* wd2 = nullptr;         // per sorted query: winning d2 (+inf = rejected)
+    int32_t* fb = nullptr;        // fallback lists: one segment of fb_seg entries per octant WG
+    uint32_t* fb_count = nullptr; // per octant wave: entries in its segment
+    uint32_t* fb_off = nullptr;   // exclusive scan of fb_count (+ total)
+    int32_t* fbc = nullptr;       // compacted fallback list
+    int64_t fb_seg = 0;
+    double* partials = nullptr;   // (nb_fast + nb_ring) * 24
     double* acc = nullptr;        // 24 (scratch for pcp_icp_run)
-    int nblocks = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int nb_fast = 0, nb_ring = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
+    int dbg = 0;                  // PCP_ICP_ABLATE flags (profiling only)
     double last_ms = 0.0;
     int last_launches = 0;
+    uint32_t last_fallback = 0;
 };
 
 namespace pcp {
 namespace {
 
 constexpr int kIcpBlock = 256;
+#ifndef PCP_OCT_WAVES
+#define PCP_OCT_WAVES 8
+#endif
 constexpr int kAcc = 24;
 
 struct IcpArgs {
@@ -38,33 +52,137 @@ struct IcpArgs {
     const float4* tp;   // sorted target points
     const float4* q;    // sorted queries
     int64_t nq;
+    int64_t nchunks;
     float R[9], t[3];
     float r2;
+    float cert2;        // certified radius^2 of the 2x2x2 octant search
+    float rho;          // octant half-width in cell units (0.5 - margin)
     float mc;           // cell-unit margin for pruning
     double* partials;
-    int32_t* corr_idx;  // optional, original query order
-    float* corr_d2;
+    int32_t* win;
+    float* wd2;
+    int32_t* fb;
+    uint32_t* fb_count;
+    int64_t fb_seg;
+    int nb_fast;
+    int64_t nseg;       // fallback segments (= waves of the octant kernel)
+    int ring_all;       // ring kernel: process every query (sparse grid) instead of the list
+    int dbg;            // ablation flags (PCP_ICP_ABLATE, profiling builds of the bench only)
 };
 
-struct NN1 {
-    const float4* pts;
-    float qx, qy, qz;
+// Ablation switches for profiling (env PCP_ICP_ABLATE); results are wrong when any is set.
+constexpr int kDbgNoScan = 1, kDbgNoAccum = 4, kDbgNoFallback = 8;
+
+__device__ __forceinline__ void xform(const IcpArgs& a, const float4 q, float& x, float& y, float& z) {
+    // q' = R q + t: x' = fmaf(R02,z,fmaf(R01,y,fmaf(R00,x,t0)))
+    x = __fmaf_rn(a.R[2], q.z, __fmaf_rn(a.R[1], q.y, __fmaf_rn(a.R[0], q.x, a.t[0])));
+    y = __fmaf_rn(a.R[5], q.z, __fmaf_rn(a.R[4], q.y, __fmaf_rn(a.R[3], q.x, a.t[1])));
+    z = __fmaf_rn(a.R[8], q.z, __fmaf_rn(a.R[7], q.y, __fmaf_rn(a.R[6], q.x, a.t[2])));
+}
+
+// running 1-NN: best d2, its target index (tie order) and its position in the scanned array
+struct Best {
     float bd;
     int bj;
-    float px, py, pz;
-    __device__ __forceinline__ float bound() const { return bd * 1.00002f + 1e-30f; }
-    __device__ __forceinline__ void visit(uint32_t s, uint32_t e) {
-        for (uint32_t k = s; k < e; k++) {
+    uint32_t bk;
+    float px, py, pz;  // filled by fetch() once the scan is over
+    __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t k) {
+        const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+        const float d2 = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx));
+        const int id = __float_as_int(p.w);
+        // "<=" on the index: re-visiting the current winner (a provisional bound) refreshes bk
+        const bool take = d2 < bd || (d2 == bd && id <= bj);
+        bd = take ? d2 : bd;
+        bj = take ? id : bj;
+        bk = take ? k : bk;
+    }
+    // candidates [s, e) of `pts` (LDS or global); loads issued 4 at a time so the memory
+    // latency of a candidate is not serialised behind the previous update
+    template <typename P>
+    __device__ __forceinline__ void scan(const P* pts, uint32_t s, uint32_t e, float qx, float qy, float qz) {
+        uint32_t k = s;
+        for (; k + 4 <= e; k += 4) {
+            const float4 p0 = pts[k], p1 = pts[k + 1], p2 = pts[k + 2], p3 = pts[k + 3];
+            consider(qx, qy, qz, p0, k);
+            consider(qx, qy, qz, p1, k + 1);
+            consider(qx, qy, qz, p2, k + 2);
+            consider(qx, qy, qz, p3, k + 3);
+        }
+        for (; k < e; k++) consider(qx, qy, qz, pts[k], k);
+    }
+    // [s, e) sorted by x: binary search of q.x, then sweep outward while dx^2 <= bd.  A point
+    // beyond the stop has a larger |dx| and fp32 d2 >= dx*dx (monotone rounding), so it can
+    // neither beat nor tie the current best: the result equals a full scan of [s, e).
+    template <typename P>
+    __device__ __forceinline__ void sweep(const P* pts, uint32_t s, uint32_t e, float qx, float qy, float qz) {
+        uint32_t lo = s, hi = e;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pts[mid].x < qx) lo = mid + 1;
+            else hi = mid;
+        }
+        for (uint32_t k = lo; k < e; k++) {
             const float4 p = pts[k];
-            const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
-            const float d2 = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx));
-            const int id = __float_as_int(p.w);
-            if (d2 < bd || (d2 == bd && id < bj)) {
-                bd = d2; bj = id; px = p.x; py = p.y; pz = p.z;
+            const float dx = p.x - qx;
+            if (dx * dx > bd) break;
+            consider(qx, qy, qz, p, k);
+        }
+        for (uint32_t k = lo; k > s; k--) {
+            const float4 p = pts[k - 1];
+            const float dx = qx - p.x;
+            if (dx * dx > bd) break;
+            consider(qx, qy, qz, p, k - 1);
+        }
+    }
+    template <typename P>
+    __device__ __forceinline__ void fetch(const P* pts) {
+        const float4 p = pts[bk];
+        px = p.x; py = p.y; pz = p.z;
+    }
+};
+
+// Exact 1-NN within sqrt(b.bd) by rows of cells: the rows (y,z) that intersect the sphere's
+// bounding box are visited nearest-first, and each row is scanned over the x-range of cells
+// still within the (shrinking) bound -- one contiguous point range per row on a dense grid.
+// Rows and cells are pruned conservatively (margin mc cells, 2e-5 relative on d2), so the
+// winner equals an exhaustive lexicographic (d2, index) search.
+__device__ __forceinline__ void box_search(const GridDesc& g, const float4* tp, float qx, float qy,
+                                           float qz, float mc, Best& b) {
+    const float fx = cell_f<float>(g, qx, 0), fy = cell_f<float>(g, qy, 1), fz = cell_f<float>(g, qz, 2);
+    const int cy = (int)floorf(fy), cz = (int)floorf(fz);
+    const float ly = fy - (float)cy, lz = fz - (float)cz;
+    const float inv_h2 = g.inv_hf * g.inv_hf;
+    const float rc = sqrtf(b.bd * 1.00002f * inv_h2) + mc;  // initial radius in cells
+    const int ry = (int)ceilf(rc) + 1, rz = ry;
+    for (int oz = 0; oz <= 2 * rz; oz++) {
+        const int dz = (oz & 1) ? -((oz + 1) >> 1) : (oz >> 1);  // 0, -1, +1, -2, +2, ...
+        const int z = cz + dz;
+        if (z < 0 || z >= g.n[2]) continue;
+        const float gz = dz < 0 ? (lz + (float)(-dz - 1)) : (dz > 0 ? (1.f - lz + (float)(dz - 1)) : 0.f);
+        const float gz2 = gz > mc ? (gz - mc) * (gz - mc) : 0.f;
+        for (int oy = 0; oy <= 2 * ry; oy++) {
+            const int dy = (oy & 1) ? -((oy + 1) >> 1) : (oy >> 1);
+            const int y = cy + dy;
+            if (y < 0 || y >= g.n[1]) continue;
+            const float gy = dy < 0 ? (ly + (float)(-dy - 1)) : (dy > 0 ? (1.f - ly + (float)(dy - 1)) : 0.f);
+            const float gyz2 = gz2 + (gy > mc ? (gy - mc) * (gy - mc) : 0.f);
+            const float lim = b.bd * 1.00002f * inv_h2 - gyz2;  // remaining x extent^2 (cells)
+            if (lim < 0.f) continue;
+            const float rx = sqrtf(lim) + mc;
+            const int xa = max((int)floorf(fx - rx), 0), xb = min((int)floorf(fx + rx), g.n[0] - 1);
+            if (xa > xb) continue;
+            if (g.dense) {
+                const int64_t c = dense_id(g, xa, y, z);
+                b.sweep(tp, g.cstart[c], g.cstart[c + (xb - xa + 1)], qx, qy, qz);
+            } else {
+                for (int x = xa; x <= xb; x++) {
+                    uint32_t s, e;
+                    if (cell_range(g, x, y, z, s, e)) b.sweep(tp, s, e, qx, qy, qz);
+                }
             }
         }
     }
-};
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -72,56 +190,198 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-__global__ void __launch_bounds__(kIcpBlock) k_icp_step(IcpArgs a) {
-    double acc[kAcc - 1];
-#pragma unroll
-    for (int k = 0; k < kAcc - 1; k++) acc[k] = 0.0;
-    const int64_t stride = (int64_t)gridDim.x * kIcpBlock;
-    for (int64_t i = blockIdx.x * (int64_t)kIcpBlock + threadIdx.x; i < a.nq; i += stride) {
-        const float4 q = a.q[i];
-        // q' = R q + t: x' = fmaf(R02,z,fmaf(R01,y,fmaf(R00,x,t0)))
-        const float qx = __fmaf_rn(a.R[2], q.z, __fmaf_rn(a.R[1], q.y, __fmaf_rn(a.R[0], q.x, a.t[0])));
-        const float qy = __fmaf_rn(a.R[5], q.z, __fmaf_rn(a.R[4], q.y, __fmaf_rn(a.R[3], q.x, a.t[1])));
-        const float qz = __fmaf_rn(a.R[8], q.z, __fmaf_rn(a.R[7], q.y, __fmaf_rn(a.R[6], q.x, a.t[2])));
-        NN1 v{a.tp, qx, qy, qz, a.r2, 0x7fffffff, 0.f, 0.f, 0.f};
-        ring_search<float>(a.g, qx, qy, qz, a.mc, v);
-        const bool ok = v.bj != 0x7fffffff;
-        if (a.corr_idx) {
-            const int oq = __float_as_int(q.w);
-            a.corr_idx[oq] = ok ? v.bj : -1;
-            a.corr_d2[oq] = ok ? v.bd : INFINITY;
-        }
-        if (ok) {
-            const double x0 = qx, x1 = qy, x2 = qz, p0 = v.px, p1 = v.py, p2 = v.pz;
-            acc[0] += 1.0;
-            acc[1] += x0; acc[2] += x1; acc[3] += x2;
-            acc[4] += p0; acc[5] += p1; acc[6] += p2;
-            acc[7] += x0 * p0; acc[8] += x0 * p1; acc[9] += x0 * p2;
-            acc[10] += x1 * p0; acc[11] += x1 * p1; acc[12] += x1 * p2;
-            acc[13] += x2 * p0; acc[14] += x2 * p1; acc[15] += x2 * p2;
-            acc[16] += x0 * x0; acc[17] += x0 * x1; acc[18] += x0 * x2;
-            acc[19] += x1 * x1; acc[20] += x1 * x2; acc[21] += x2 * x2;
-            acc[22] += (double)v.bd;
-        }
+__device__ __forceinline__ int wave_min_i(int v) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// Main pass (dense grid).  Wave-autonomous, one query per lane: waves take 64-query chunks
+// of the spatially sorted query set (grid-stride, so the 4 waves of a workgroup work on
+// adjacent chunks and share L1), transform each query, and scan its 2x2x2 "octant" block
+// of cells straight from the x-rows of the dense table.  The octant holds every target
+// within (0.5 - mc) cells of the query: a winner with d2 <= cert2 is the exact 1-NN, and
+// "nothing within rmax" is certified when rmax^2 <= cert2.  Other queries keep their
+// provisional octant winner (a valid upper bound for the exact fallback search) and go to
+// the wave's fallback segment (ballot + mbcnt, no atomics).
+// Accumulators: per chunk, fp32 products centred on the chunk's first query are summed
+// across the wave with DPP adds (no LDS permutes), un-centred in fp64 by one lane and kept
+// in LDS -- no accumulator registers, so the kernel fits 8 waves per SIMD.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_add(float v) {
+    const int t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xf, false);
+    return v + __int_as_float(t);
+}
+// full-wave fp32 sum (every lane must be active); the total ends in lane 63
+__device__ __forceinline__ float wave_sum_f32(float v) {
+    v = dpp_add<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x141, 0xf>(v);  // row_half_mirror
+    v = dpp_add<0x140, 0xf>(v);  // row_mirror
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// Add one chunk's accepted pairs (lanes with ok) to the wave's fp64 accumulators S (LDS):
+// fp32 products centred on lane 0's query, summed across the wave with DPP adds, then
+// un-centred in fp64 by lane 0.  Every lane of the wave must call it (full EXEC).
+__device__ __forceinline__ void chunk_accumulate(bool ok, float qx, float qy, float qz, const Best& b,
+                                                 double* S, int lane) {
+    if (!__ballot(ok)) return;
+    const float ccx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), 0));
+    const float ccy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qy), 0));
+    const float ccz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qz), 0));
+    const float x0 = ok ? qx - ccx : 0.f, x1 = ok ? qy - ccy : 0.f, x2 = ok ? qz - ccz : 0.f;
+    const float p0 = ok ? b.px - ccx : 0.f, p1 = ok ? b.py - ccy : 0.f, p2 = ok ? b.pz - ccz : 0.f;
+    const float nn = wave_sum_f32(ok ? 1.f : 0.f);
+    const float A0 = wave_sum_f32(x0), A1 = wave_sum_f32(x1), A2 = wave_sum_f32(x2);
+    const float B0 = wave_sum_f32(p0), B1 = wave_sum_f32(p1), B2 = wave_sum_f32(p2);
+    const float AB[9] = {wave_sum_f32(x0 * p0), wave_sum_f32(x0 * p1), wave_sum_f32(x0 * p2),
+                         wave_sum_f32(x1 * p0), wave_sum_f32(x1 * p1), wave_sum_f32(x1 * p2),
+                         wave_sum_f32(x2 * p0), wave_sum_f32(x2 * p1), wave_sum_f32(x2 * p2)};
+    const float AA[6] = {wave_sum_f32(x0 * x0), wave_sum_f32(x0 * x1), wave_sum_f32(x0 * x2),
+                         wave_sum_f32(x1 * x1), wave_sum_f32(x1 * x2), wave_sum_f32(x2 * x2)};
+    const float DD = wave_sum_f32(ok ? b.bd : 0.f);
+    if (lane == 0) {  // un-centre in fp64: q = a + c, p = b + c
+        const double n = nn, C[3] = {ccx, ccy, ccz}, A[3] = {A0, A1, A2}, B[3] = {B0, B1, B2};
+        S[0] += n;
+        for (int k = 0; k < 3; k++) { S[1 + k] += A[k] + n * C[k]; S[4 + k] += B[k] + n * C[k]; }
+        for (int r = 0; r < 3; r++)
+            for (int k = 0; k < 3; k++)
+                S[7 + 3 * r + k] += (double)AB[3 * r + k] + A[r] * C[k] + C[r] * B[k] + n * C[r] * C[k];
+        const int ir[6] = {0, 0, 0, 1, 1, 2}, ik[6] = {0, 1, 2, 1, 2, 2};
+        for (int m = 0; m < 6; m++)
+            S[16 + m] += (double)AA[m] + A[ir[m]] * C[ik[m]] + C[ir[m]] * A[ik[m]] + n * C[ir[m]] * C[ik[m]];
+        S[22] += DD;
     }
-    __shared__ double red[kIcpBlock / 64][kAcc];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < kAcc - 1; k++) {
-        double s = wave_sum(acc[k]);
-        if (lane == 0) red[wid][k] = s;
-    }
+}
+
+__device__ __forceinline__ void write_wave_partials(double (*s_acc)[kAcc], double* out) {
     __syncthreads();
     if (threadIdx.x < kAcc) {
         double s = 0.0;
         if (threadIdx.x < kAcc - 1)
-            for (int w = 0; w < kIcpBlock / 64; w++) s += red[w][threadIdx.x];
-        a.partials[(int64_t)blockIdx.x * kAcc + threadIdx.x] = s;
+            for (int w = 0; w < kIcpBlock / 64; w++) s += s_acc[w][threadIdx.x];
+        out[threadIdx.x] = s;
     }
 }
 
+__global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a) {
+    constexpr int kW = kIcpBlock / 64;
+    __shared__ double s_acc[kW][kAcc];
+    const GridDesc& g = a.g;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * kW + wid;  // global wave id = fallback segment
+    const int64_t nwaves = (int64_t)gridDim.x * kW;
+    const int64_t nch = (a.nq + 63) / 64;
+    const bool reject_certified = a.r2 <= a.cert2;
+    if (lane < kAcc) s_acc[wid][lane] = 0.0;
+    uint32_t fbn = 0;  // wave-uniform count of this wave's fallback entries
+
+    float4 qn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gw < nch && gw * 64 + lane < a.nq) qn = a.q[gw * 64 + lane];
+    for (int64_t c = gw; c < nch; c += nwaves) {
+        const int64_t i = c * 64 + lane;
+        const bool valid = i < a.nq;
+        const float4 qraw = qn;
+        if (c + nwaves < nch && i + 64 * nwaves < a.nq) qn = a.q[i + 64 * nwaves];  // prefetch
+        Best b{a.r2, 0x7fffffff, ~0u, 0.f, 0.f, 0.f};
+        float qx = 0.f, qy = 0.f, qz = 0.f;
+        int bx = 0, by = 0, bz = 0;
+        if (valid) {
+            xform(a, qraw, qx, qy, qz);
+            bx = (int)floorf(cell_f<float>(g, qx, 0) - a.rho);
+            by = (int)floorf(cell_f<float>(g, qy, 1) - a.rho);
+            bz = (int)floorf(cell_f<float>(g, qz, 2) - a.rho);
+        }
+        if (valid && !(a.dbg & kDbgNoScan)) {
+            const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
+            if (xa <= xb) {
+                for (int r = 0; r < 4; r++) {
+                    const int y = by + (r & 1), z = bz + (r >> 1);
+                    if (y < 0 || y >= g.n[1] || z < 0 || z >= g.n[2]) continue;
+                    const int64_t cc = dense_id(g, xa, y, z);
+                    b.scan(a.tp, g.cstart[cc], g.cstart[cc + (xb - xa + 1)], qx, qy, qz);
+                }
+            }
+        }
+        // ---- epilogue: results, fallback list, accumulators
+        const bool found = b.bj != 0x7fffffff;
+        const bool done = valid && ((found && b.bd <= a.cert2) || (!found && reject_certified) ||
+                                    (a.dbg & kDbgNoFallback));
+        if (valid) {  // provisional for fallback queries (an upper bound), final otherwise
+            a.win[i] = found ? b.bj : -1;
+            a.wd2[i] = found ? b.bd : INFINITY;
+        }
+        const bool fb = valid && !done;
+        const uint64_t fbm = __ballot(fb);
+        if (fb) {
+            const uint32_t pos = fbn + __builtin_amdgcn_mbcnt_hi((uint32_t)(fbm >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)fbm, 0u));
+            a.fb[gw * a.fb_seg + pos] = (int32_t)i;
+        }
+        fbn += (uint32_t)__popcll(fbm);
+        const bool acc_ok = done && found && !(a.dbg & kDbgNoAccum);
+        if (acc_ok) b.fetch(a.tp);
+        chunk_accumulate(acc_ok, qx, qy, qz, b, s_acc[wid], lane);
+    }
+    if (lane == 0) a.fb_count[gw] = fbn;
+    write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
+}
+
+// Fallback / general pass: exact box search (dense or sparse grid), starting from the
+// octant pass's provisional winner when it has one.  Queries come from the compacted
+// fallback list (or are all queries when ring_all is set, i.e. on a sparse grid); waves
+// take 64-entry chunks grid-stride and accumulate like the octant pass.
+__global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_ring(IcpArgs a, double* partials,
+                                                                        const int32_t* list, const uint32_t* list_n) {
+    constexpr int kW = kIcpBlock / 64;
+    __shared__ double s_acc[kW][kAcc];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane < kAcc) s_acc[wid][lane] = 0.0;
+    const int64_t n = a.ring_all ? a.nq : (int64_t)*list_n;
+    const int64_t gw = (int64_t)blockIdx.x * kW + wid, nwaves = (int64_t)gridDim.x * kW;
+    for (int64_t c = gw; c * 64 < n; c += nwaves) {
+        const int64_t j = c * 64 + lane;
+        const bool valid = j < n;
+        Best b{a.r2, 0x7fffffff, 0u, 0.f, 0.f, 0.f};
+        float qx = 0.f, qy = 0.f, qz = 0.f;
+        int64_t i = 0;
+        if (valid) {
+            i = a.ring_all ? j : list[j];
+            xform(a, a.q[i], qx, qy, qz);
+            if (!a.ring_all && a.win[i] >= 0) {  // provisional octant winner: a valid upper bound
+                b.bd = a.wd2[i];
+                b.bj = a.win[i];
+            }
+            box_search(a.g, a.tp, qx, qy, qz, a.mc, b);
+            const bool ok = b.bj != 0x7fffffff;
+            a.win[i] = ok ? b.bj : -1;
+            a.wd2[i] = ok ? b.bd : INFINITY;
+        }
+        const bool acc_ok = valid && b.bj != 0x7fffffff && !(a.dbg & kDbgNoAccum);
+        if (acc_ok) b.fetch(a.tp);
+        chunk_accumulate(acc_ok, qx, qy, qz, b, s_acc[wid], lane);
+    }
+    write_wave_partials(s_acc, partials + (int64_t)blockIdx.x * kAcc);
+}
+
+// concatenate the per-wave fallback segments (one wave per segment)
+__global__ void k_fb_compact(const int32_t* fb, const uint32_t* cnt, const uint32_t* off, int64_t nseg,
+                             int64_t seg_cap, int32_t* out) {
+    const int64_t seg = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (seg >= nseg) return;
+    const uint32_t n = cnt[seg], o = off[seg];
+    for (uint32_t k = threadIdx.x & 63; k < n; k += 64) out[o + k] = fb[seg * seg_cap + k];
+}
+
 // fixed-order reduction of nb partial rows of 24 doubles -> out[24]
-__global__ void __launch_bounds__(256) k_reduce_partials(const double* part, int nb, double* out) {
+__global__ void __launch_bounds__(256) k_reduce_partials(const double* part, int nb, double* out,
+                                                         const uint32_t* fbc, int nfb) {
     __shared__ double s[256];
     for (int k = 0; k < kAcc; k++) {
         double v = 0.0;
@@ -134,6 +394,27 @@ __global__ void __launch_bounds__(256) k_reduce_partials(const double* part, int
         }
         if (threadIdx.x == 0) out[k] = s[0];
         __syncthreads();
+    }
+    // slot 23 (unused by the solve): fallback queries of this iteration
+    double f = 0.0;
+    for (int b = threadIdx.x; b < nfb; b += 256) f += (double)fbc[b];
+    s[threadIdx.x] = f;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[kAcc - 1] = s[0];
+}
+
+// sorted-order winners -> caller (original query) order
+__global__ void k_scatter_corr(const float4* q, const int32_t* win, const float* wd2, int64_t n,
+                               int32_t* idx, float* d2) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int oq = __float_as_int(q[i].w);
+        idx[oq] = win[i];
+        d2[oq] = wd2[i];
     }
 }
 
@@ -230,6 +511,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.tp = (const float4*)tg->pts;
     a.q = icp->q;
     a.nq = icp->nq;
+    a.nchunks = (icp->nq + kIcpBlock - 1) / kIcpBlock;
     for (int r = 0; r < 3; r++) {
         for (int c = 0; c < 3; c++) a.R[3 * r + c] = (float)T[4 * r + c];
         a.t[r] = (float)T[4 * r + 3];
@@ -237,17 +519,51 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.r2 = rmax * rmax;
     const int nmax = std::max(a.g.n[0], std::max(a.g.n[1], a.g.n[2]));
     a.mc = 1e-5f + 8e-7f * (float)nmax;  // >> fp32 rounding of the cell coordinates
+    a.rho = 0.5f;
+    // exact radius of the octant block: (0.5 - mc) cells, shrunk for fp32 d2 rounding
+    const double rr = (0.5 - (double)a.mc) * a.g.h;
+    a.cert2 = (float)(rr * rr * (1.0 - 1e-5));
     a.partials = icp->partials;
-    a.corr_idx = corr_idx;
-    a.corr_d2 = corr_d2;
-    if (corr_idx && icp->nq > 0)
-        hipLaunchKernelGGL(k_fill_corr, dim3(grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, corr_idx,
-                           corr_d2, icp->nq);
+    a.win = icp->win;
+    a.wd2 = icp->wd2;
+    a.fb = icp->fb;
+    a.fb_count = icp->fb_count;
+    a.fb_seg = icp->fb_seg;
+    a.nb_fast = icp->nb_fast;
+    a.nseg = (int64_t)icp->nb_fast * (kIcpBlock / 64);
+    a.ring_all = a.g.dense ? 0 : 1;
+    a.dbg = icp->dbg;
+    PCP_HIP(ctx, hipMemsetAsync(icp->fb_count, 0, (size_t)a.nseg * sizeof(uint32_t), ctx->stream));
     PCP_HIP(ctx, hipEventRecord(icp->ev0, ctx->stream));
-    hipLaunchKernelGGL(k_icp_step, dim3(icp->nblocks), dim3(kIcpBlock), 0, ctx->stream, a);
+    if (a.g.dense) {
+        hipLaunchKernelGGL(k_icp_octant, dim3(icp->nb_fast), dim3(kIcpBlock), 0, ctx->stream, a);
+    } else {
+        PCP_HIP(ctx, hipMemsetAsync(icp->partials, 0, (size_t)icp->nb_fast * kAcc * sizeof(double), ctx->stream));
+    }
+    if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_mid, ctx->stream));
+    if (a.g.dense) {  // compact the per-wave fallback segments into one list
+        PCP_HIP(ctx, hipMemcpyAsync(icp->fb_off, icp->fb_count, (size_t)a.nseg * sizeof(uint32_t),
+                                    hipMemcpyDeviceToDevice, ctx->stream));
+        PCP_HIP(ctx, hipMemsetAsync(icp->fb_off + a.nseg, 0, sizeof(uint32_t), ctx->stream));
+        PCP_TRY(scan_u32_inplace(ctx, icp->fb_off, a.nseg + 1, nullptr));
+        hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)((a.nseg + 3) / 4)), dim3(256), 0, ctx->stream, icp->fb,
+                           (const uint32_t*)icp->fb_count, (const uint32_t*)icp->fb_off, a.nseg, a.fb_seg, icp->fbc);
+    }
+    hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, ctx->stream, a,
+                       icp->partials + (int64_t)icp->nb_fast * kAcc, (const int32_t*)icp->fbc,
+                       (const uint32_t*)(icp->fb_off + a.nseg));
     PCP_HIP(ctx, hipEventRecord(icp->ev1, ctx->stream));
-    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(256), 0, ctx->stream, icp->partials, icp->nblocks,
-                       acc_dev);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(256), 0, ctx->stream, icp->partials,
+                       icp->nb_fast + icp->nb_ring, acc_dev, (const uint32_t*)icp->fb_count,
+                       a.g.dense ? (int)a.nseg : 0);
+    if (corr_idx) {
+        if (icp->nq_in > icp->nq)  // non-finite queries were dropped at create time
+            hipLaunchKernelGGL(k_fill_corr, dim3(grid_for(icp->nq_in, 256)), dim3(256), 0, ctx->stream, corr_idx,
+                               corr_d2, icp->nq_in);
+        if (icp->nq > 0)
+            hipLaunchKernelGGL(k_scatter_corr, dim3(grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, icp->q,
+                               icp->win, icp->wd2, icp->nq, corr_idx, corr_d2);
+    }
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }
@@ -304,11 +620,12 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     *out = nullptr;
     // spatially sort the query set once (same grid machinery), keep its sorted points
     pcp_index* qi = nullptr;
-    PCP_TRY(pcp_index_build_f32(ctx, q, q_stride, nq, target->g.h, &qi));
+    PCP_TRY(pcp::index_build_f32_bricks(ctx, q, q_stride, nq, target->g.h, &qi));
     pcp_icp* icp = new pcp_icp();
     icp->ctx = ctx;
     icp->target = target;
     icp->nq = qi->n;
+    icp->nq_in = nq;
     icp->q = (float4*)qi->pts;
     qi->pts = nullptr;
     pcp_index_destroy(qi);
@@ -317,11 +634,23 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
         dev_cus = prop.multiProcessorCount;
     const int64_t want = (icp->nq + pcp::kIcpBlock - 1) / pcp::kIcpBlock;
-    icp->nblocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * 8));
-    int rc = pcp::dmalloc(ctx, &icp->partials, (size_t)icp->nblocks * pcp::kAcc);
+    icp->nb_fast = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * 8));
+    icp->nb_ring = icp->nb_fast;
+    const int64_t nwaves = (int64_t)icp->nb_fast * (pcp::kIcpBlock / 64);
+    const int64_t nchunks64 = (icp->nq + 63) / 64;
+    icp->fb_seg = ((nchunks64 + nwaves - 1) / nwaves) * 64;
+    int rc = pcp::dmalloc(ctx, &icp->partials, (size_t)(icp->nb_fast + icp->nb_ring) * pcp::kAcc);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->acc, pcp::kAcc);
-    if (!rc && (hipEventCreate(&icp->ev0) != hipSuccess || hipEventCreate(&icp->ev1) != hipSuccess))
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->win, icp->nq + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->wd2, icp->nq + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb, (size_t)nwaves * icp->fb_seg + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_count, (size_t)nwaves);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_off, (size_t)nwaves + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->fbc, icp->nq + 1);
+    if (!rc && (hipEventCreate(&icp->ev0) != hipSuccess || hipEventCreate(&icp->ev1) != hipSuccess ||
+                hipEventCreate(&icp->ev_mid) != hipSuccess))
         rc = pcp::set_error(ctx, PCP_ERR_HIP, "hipEventCreate failed");
+    if (const char* ab = std::getenv("PCP_ICP_ABLATE")) icp->dbg = std::atoi(ab);
     if (rc) {
         pcp_icp_destroy(icp);
         return rc;
@@ -336,8 +665,15 @@ int pcp_icp_destroy(pcp_icp* icp) {
     hipFree(icp->q);
     hipFree(icp->partials);
     hipFree(icp->acc);
+    hipFree(icp->win);
+    hipFree(icp->wd2);
+    hipFree(icp->fb);
+    hipFree(icp->fb_count);
+    hipFree(icp->fb_off);
+    hipFree(icp->fbc);
     if (icp->ev0) hipEventDestroy(icp->ev0);
     if (icp->ev1) hipEventDestroy(icp->ev1);
+    if (icp->ev_mid) hipEventDestroy(icp->ev_mid);
     delete icp;
     return PCP_OK;
 }
@@ -348,11 +684,20 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     icp->ctx = ctx;
     PCP_TRY(pcp::icp_launch(icp, T, rmax, acc_dev, corr_idx, corr_d2));
-    PCP_HIP(ctx, hipEventSynchronize(icp->ev1));
+    double fbn = 0.0;
+    PCP_HIP(ctx, hipMemcpyAsync(&fbn, acc_dev + 23, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    icp->last_fallback = (uint32_t)fbn;
     float ms = 0.f;
     PCP_HIP(ctx, hipEventElapsedTime(&ms, icp->ev0, icp->ev1));
     icp->last_ms = ms;
     icp->last_launches = 1;
+    if (icp->dbg) {
+        float m1 = 0.f;
+        (void)hipEventElapsedTime(&m1, icp->ev0, icp->ev_mid);
+        std::fprintf(stderr, "[pcp icp dbg=%d] octant %.4f ms  fallback %.4f ms  n_fallback %u\n", icp->dbg, m1,
+                     ms - m1, icp->last_fallback);
+    }
     return PCP_OK;
 }
 
@@ -402,6 +747,12 @@ int pcp_icp_run(pcp_ctx* ctx, pcp_icp* icp, double T[16], float rmax, int iters,
     icp->last_launches = launches;
     if (err) *err = (float)e;
     return e < 0 ? PCP_ERR_ICP : PCP_OK;
+}
+
+int pcp_icp_last_fallback(const pcp_icp* icp, int64_t* n) {
+    if (!icp || !n) return PCP_ERR_ARG;
+    *n = icp->last_fallback;
+    return PCP_OK;
 }
 
 int pcp_icp_last_kernel_ms(const pcp_icp* icp, double* ms, int* launches) {

@@ -255,6 +255,11 @@ class ICP:
         self.ctx.check(self.ctx.lib.pcp_icp_last_kernel_ms(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def last_fallback(self):
+        n = C.c_int64()
+        self.ctx.check(self.ctx.lib.pcp_icp_last_fallback(self.h, C.byref(n)))
+        return n.value
+
     def close(self):
         if getattr(self, "h", None):
             self.ctx.lib.pcp_icp_destroy(self.h)

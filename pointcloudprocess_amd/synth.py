@@ -17,14 +17,23 @@ def _u(g, n, lo, hi, device):
 def street_scene(n, seed, extent=(200.0, 200.0), noise=0.01, device="cpu", dtype=torch.float32):
     """Street scene: undulating ground + building facades + poles (C3/C4/C5 generator).
 
-    Returns an (n, 3) tensor centred near the origin.  Point density is
-    n / (extent_x * extent_y) per ground m^2 (times 0.55).
+    Returns an (n, 3) tensor centred near the origin.  Points are allocated to the three
+    surface kinds in proportion to their area, so the surface density is about uniform
+    (as in the reference's inputs, which remove_duplicate(0.04) caps at ~625 pts/m^2;
+    point_cloud_helper.cpp:42-63, main_blend.cpp:276,462).
     """
     g = torch.Generator(device=device)
     g.manual_seed(int(seed))
     X, Y = float(extent[0]), float(extent[1])
-    n_ground = int(0.55 * n)
-    n_fac = int(0.40 * n)
+    n_sx = len(np.arange(-X / 2 + 25, X / 2, 50.0))
+    n_sy = len(np.arange(-Y / 2 + 25, Y / 2, 50.0))
+    n_poles = 2 * n_sy * len(np.arange(-X / 2 + 7.5, X / 2, 15.0))
+    a_ground = X * Y
+    a_fac = 11.5 * (2 * n_sx * Y + 2 * n_sy * X)     # mean facade height 11.5 m
+    a_pole = n_poles * 2 * math.pi * 0.15 * 6.0
+    a_tot = a_ground + a_fac + a_pole
+    n_ground = int(n * a_ground / a_tot)
+    n_fac = int(n * a_fac / a_tot)
     n_pole = n - n_ground - n_fac
 
     def gnoise(m):
@@ -68,7 +77,7 @@ def street_scene(n, seed, extent=(200.0, 200.0), noise=0.01, device="cpu", dtype
     ppy = torch.tensor(py_list, dtype=torch.float64, device=device)
     j = torch.randint(0, ppx.numel(), (n_pole,), generator=g, device=device)
     th = _u(g, n_pole, 0.0, 2 * math.pi, device)
-    rr = 0.1 + gnoise(n_pole)
+    rr = 0.15 + gnoise(n_pole)
     qx = ppx[j] + rr * torch.cos(th)
     qy = ppy[j] + rr * torch.sin(th)
     qz = ground_z(qx, qy) + _u(g, n_pole, 0.0, 6.0, device)

@@ -3,7 +3,7 @@
 Contract (oracle/pcp_oracle.h): per query q' = R q + t (fp32 fmaf chain),
 exact 1-NN within rmax by fp32 d2 = fmaf(dz,dz,fmaf(dy,dy,dx*dx)), ties by target index.
 Correspondence indices and d2 are compared BIT-EXACT with the oracle at the same pose;
-accumulators to 1e-12 relative (different summation order); full ICP poses to 1e-5
+accumulators to 1e-7 relative (fp32 centred partial sums); full ICP poses to 1e-5
 (north_star tolerance).  ICP itself is "parity unpinned" against the reference
 (trimesh2 ICP() is absent).
 """
@@ -48,7 +48,10 @@ def test_correspondence_bit_exact(ctx, cell):
         eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
         gacc = acc.cpu().numpy()
         assert gacc[0] == eacc[0]
-        assert np.allclose(gacc, eacc, rtol=1e-12, atol=1e-9)
+        # GPU: per-lane fp32 sums of products centred on a per-wave point, then fp64;
+        # oracle: sequential fp64.  [23] is the fallback count (diagnostic).
+        scale = np.abs(eacc[:23]).max()
+        assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-9 * scale)
 
 
 def test_ties_lattice(ctx):
@@ -96,3 +99,20 @@ def test_icp_run_matches_oracle(ctx):
     eerr, eT = ora.icp(tgt.numpy(), q.numpy(), np.eye(4), 0.25, 20)
     assert err > 0 and abs(err - eerr) < 1e-5
     assert np.abs(T - eT).max() < 1e-5
+
+
+def test_sparse_grid_matches_oracle(ctx):
+    # two clusters 5 km apart with 5 cm cells: the dense cell table would exceed its budget,
+    # so the index uses 4x4x4 bricks and the ICP runs the general box search for every query
+    from pointcloudprocess_amd import ops, synth
+    rng = np.random.default_rng(4)
+    a = rng.uniform(0, 2, size=(20000, 3)).astype(np.float32)
+    tgt = np.concatenate([a, a[:5000] + np.float32(5000.0)])
+    q = (tgt + rng.normal(scale=0.01, size=tgt.shape)).astype(np.float32)
+    index = ops.GridIndex(ctx, torch.from_numpy(tgt).to(ctx.device), cell_size=0.05)
+    assert ctx.lib.pcp_index_cells(index.h) < 1e9  # sparse (brick) mode
+    icp = ops.ICP(index, torch.from_numpy(q).to(ctx.device))
+    T = synth.rigid(0.1, 0.0, 0.0, (0.01, 0.0, 0.0))
+    acc, ci, cd = icp.step(T, 0.1, corr=True)
+    ei, ed = ora.F32Index(tgt).correspond(q, T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32), 0.1)
+    assert np.array_equal(ci.cpu().numpy(), ei)
