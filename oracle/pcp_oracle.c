@@ -386,6 +386,13 @@ int ora_remove_duplicate(const ora_point48* in, int n, int is_dense, float leaf,
     if (n <= 0) return 0;
     double c[4] = {0, 0, 0, 0};
     ora_centroid(in, n, is_dense, c);                       /* point_cloud_helper.cpp:45 */
+    return ora_remove_duplicate_c(in, n, is_dense, leaf, c, out);
+}
+
+int ora_remove_duplicate_c(const ora_point48* in, int n, int is_dense, float leaf,
+                           const double cin[3], ora_point48* out) {
+    if (n <= 0) return 0;
+    const double c[3] = {cin[0], cin[1], cin[2]};
     double T[16] = {1, 0, 0, -c[0], 0, 1, 0, -c[1], 0, 0, 1, -c[2], 0, 0, 0, 1};
     ora_point48* tmp = (ora_point48*)malloc((size_t)n * sizeof(ora_point48));
     for (int i = 0; i < n; i++) {                           /* copyPointCloud: registered fields */

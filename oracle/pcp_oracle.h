@@ -90,6 +90,10 @@ int ora_voxel_filter(const ora_point48* in, int n, int is_dense, double lx, doub
  * Returns number of output points written to `out` (capacity n). */
 int ora_remove_duplicate(const ora_point48* in, int n, int is_dense, float leaf,
                          ora_point48* out);
+/* Same with the centroid supplied (the GPU's centroid is a fixed-order tree sum, not the
+ * sequential fold: this variant checks every step after the centroid bit-exactly). */
+int ora_remove_duplicate_c(const ora_point48* in, int n, int is_dense, float leaf,
+                           const double c[3], ora_point48* out);
 
 /* ---------------------------------------------------------------- F: calculate_feature */
 /* PlanSegment fields of calculate_plan_parameter_h_points (calculate_feature.cpp:119-206),

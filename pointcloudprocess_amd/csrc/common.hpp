@@ -107,5 +107,6 @@ struct pcp_index {
     void* pts = nullptr;        // float4[n] or double4[n], sorted by (slot, local cell)
     int32_t* mapping = nullptr; // internal j -> caller index (n)
     int32_t* sorted_j = nullptr; // sorted position -> internal j (n)
+    int32_t* pos_of_j = nullptr; // internal j -> sorted position (n, fp64 index only)
     pcp_ctx* owner = nullptr;
 };

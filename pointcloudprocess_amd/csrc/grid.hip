@@ -188,6 +188,12 @@ __global__ void k_scatter(GridDesc g, const T* cxyz, int64_t n, const uint32_t* 
     }
 }
 
+__global__ void k_inverse(const int32_t* sorted_j, int64_t n, int32_t* pos_of_j) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x)
+        pos_of_j[sorted_j[k]] = (int32_t)k;
+}
+
 // Grid geometry for a cell size.  Returns false when the brick table would exceed the cap.
 bool make_geometry(GridDesc& g, const double mn[3], const double mx[3], double h, int64_t cap) {
     g.h = h;
@@ -362,6 +368,12 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             ix->pts = pts2;
             ix->sorted_j = sj2;
         }
+        if (is_f64) {
+            if ((rc = dmalloc(ctx, &ix->pos_of_j, n + 1))) break;
+            if (n > 0)
+                hipLaunchKernelGGL(k_inverse, dim3(grid_for(n, kB)), dim3(kB), 0, st,
+                                   (const int32_t*)ix->sorted_j, n, ix->pos_of_j);
+        }
         break;
     }
     hipFree(count);
@@ -408,6 +420,7 @@ int pcp_index_destroy(pcp_index* ix) {
     hipFree(ix->pts);
     hipFree(ix->mapping);
     hipFree(ix->sorted_j);
+    hipFree(ix->pos_of_j);
     delete ix;
     return PCP_OK;
 }

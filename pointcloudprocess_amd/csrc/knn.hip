@@ -1,0 +1,623 @@
+// Exact fp64 neighbour queries over the uniform-grid index: the FLANN contract of
+// KdTreeFLANN::nearestKSearch / radiusSearch (kd_tree.h:814-845, 863-903), the per-point
+// PCA normals of calculate_feature.cpp:119-206 over kNN neighbourhoods, and the
+// kd_tree_lod KdTree (kd_tree_lod/kd_tree.cpp:29-117).
+//
+// One lane per query.  The k best (d2, internal j) pairs live in registers (compile-time
+// K, unrolled branch-free insertion) and the ring search (grid.hpp) visits cells nearest
+// first, pruning with the current k-th distance.  d2 is FLANN L2_Simple<double>
+// ((0 + d0^2) + d1^2) + d2^2 with contraction off (the build compiles -ffp-contract=off),
+// so distances are bit-identical to the reference's and ties break on internal j exactly
+// like FLANN's "first found in index order" result set after sorting.
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <vector>
+
+#include "grid.hpp"
+
+namespace pcp {
+namespace {
+
+constexpr int kB = 256;
+
+__device__ __forceinline__ bool lex_less(double da, int ja, double db, int jb) {
+    return da < db || (da == db && ja < jb);
+}
+
+// FLANN L2_Simple<double> (external): r = 0; r += d0*d0; ...
+__device__ __forceinline__ double l2_simple(double qx, double qy, double qz, const double4& p) {
+    const double d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
+    double r = d0 * d0;
+    r = r + d1 * d1;
+    r = r + d2 * d2;
+    return r;
+}
+
+// pruning margin in cell units: floor() rounding of query and point cell coordinates
+__host__ __device__ inline double cell_margin64(const GridDesc& g) {
+    const int nmax = g.n[0] > g.n[1] ? (g.n[0] > g.n[2] ? g.n[0] : g.n[2]) : (g.n[1] > g.n[2] ? g.n[1] : g.n[2]);
+    return 1e-9 + 8e-16 * (double)nmax;
+}
+
+// k best (d2, j) in registers; only the first `k` (runtime, <= K) entries are maintained.
+template <int K>
+struct TopK {
+    double d[K];
+    int j[K];
+    double kth;
+    int kthj;
+    int k;
+    __device__ void init(int k_) {
+        k = k_;
+#pragma unroll
+        for (int i = 0; i < K; i++) { d[i] = INFINITY; j[i] = INT_MAX; }
+        kth = INFINITY;
+        kthj = INT_MAX;
+    }
+    // pruning radius^2: a cell whose box lower bound exceeds it holds no point that could
+    // enter (1e-12 covers the rounding of the box bound and of d2 itself)
+    __device__ double bound() const { return kth * (1.0 + 1e-12); }
+    __device__ __forceinline__ void push(double x, int jx) {
+        if (!lex_less(x, jx, kth, kthj)) return;
+        bool c[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) c[i] = lex_less(x, jx, d[i], j[i]);
+#pragma unroll
+        for (int i = K - 1; i >= 1; i--) {
+            if (c[i - 1]) { d[i] = d[i - 1]; j[i] = j[i - 1]; }
+            else if (c[i]) { d[i] = x; j[i] = jx; }
+        }
+        if (c[0]) { d[0] = x; j[0] = jx; }
+#pragma unroll
+        for (int i = 0; i < K; i++)
+            if (i == k - 1) { kth = d[i]; kthj = j[i]; }
+    }
+};
+
+template <int K>
+struct KnnVisitor {
+    const double4* pts;
+    double qx, qy, qz;
+    TopK<K> top;
+    __device__ double bound() const { return top.bound(); }
+    __device__ void visit(uint32_t s, uint32_t e) {
+        for (uint32_t t = s; t < e; t++) {
+            const double4 p = pts[t];
+            top.push(l2_simple(qx, qy, qz, p), (int)p.w);
+        }
+    }
+};
+
+__device__ __forceinline__ const double* qptr(const double* q, size_t stride, int64_t i) {
+    return (const double*)((const char*)q + (size_t)i * stride);
+}
+
+// K3: batch nearestKSearch.  Rows ascending by (d2, internal j), indices mapped through
+// index_mapping_ (kd_tree.h:837-842); entries past min(k, size) are -1 / +inf.
+template <int K>
+__global__ __launch_bounds__(kB) void k_knn(GridDesc g, const double4* pts, const int32_t* mapping, int identity,
+                                            const double* q, size_t qstride, int64_t nq, int k, int kk,
+                                            double mc, int32_t* oidx, double* od2) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+        const double* qp = qptr(q, qstride, i);
+        KnnVisitor<K> v;
+        v.pts = pts;
+        v.qx = qp[0]; v.qy = qp[1]; v.qz = qp[2];
+        v.top.init(kk);
+        if (kk > 0 && finite3(v.qx, v.qy, v.qz)) ring_search<double>(g, v.qx, v.qy, v.qz, mc, v);
+        int32_t* ri = oidx + i * k;
+        double* rd = od2 + i * k;
+#pragma unroll
+        for (int r = 0; r < K; r++) {
+            if (r < kk) {
+                const int j = v.top.j[r];
+                const bool ok = j != INT_MAX;
+                ri[r] = ok ? (identity ? j : mapping[j]) : -1;
+                if (od2) rd[r] = ok ? v.top.d[r] : INFINITY;
+            }
+        }
+        for (int r = kk; r < k; r++) {
+            ri[r] = -1;
+            if (od2) rd[r] = INFINITY;
+        }
+    }
+}
+
+// K4 count pass: #points with d2 < r2 (strict, FLANN RadiusResultSet), truncated to max_nn
+struct CountVisitor {
+    const double4* pts;
+    double qx, qy, qz, r2, b;
+    uint32_t cnt;
+    __device__ double bound() const { return b; }
+    __device__ void visit(uint32_t s, uint32_t e) {
+        for (uint32_t t = s; t < e; t++) cnt += l2_simple(qx, qy, qz, pts[t]) < r2 ? 1u : 0u;
+    }
+};
+
+__global__ __launch_bounds__(kB) void k_radius_count(GridDesc g, const double4* pts, const double* q, size_t qstride,
+                                                     int64_t nq, double r2, uint32_t cap, double mc, int32_t* ocnt) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+        const double* qp = qptr(q, qstride, i);
+        CountVisitor v{pts, qp[0], qp[1], qp[2], r2, r2 * (1.0 + 1e-12), 0u};
+        if (finite3(v.qx, v.qy, v.qz)) ring_search<double>(g, v.qx, v.qy, v.qz, mc, v);
+        ocnt[i] = (int32_t)(v.cnt < cap ? v.cnt : cap);
+    }
+}
+
+// K4 fill pass: the query's CSR row is kept sorted by (d2, j) by insertion (it holds the
+// m = min(count, max_nn) best found so far; m was fixed by the count pass).
+struct FillVisitor {
+    const double4* pts;
+    double qx, qy, qz, r2, b;
+    int32_t* ri;
+    double* rd;
+    int64_t m, filled;
+    __device__ double bound() const { return b; }
+    __device__ void visit(uint32_t s, uint32_t e) {
+        for (uint32_t t = s; t < e; t++) {
+            const double4 p = pts[t];
+            const double d = l2_simple(qx, qy, qz, p);
+            if (!(d < r2)) continue;
+            const int j = (int)p.w;
+            int64_t pos;
+            if (filled < m) pos = filled++;
+            else if (lex_less(d, j, rd[m - 1], ri[m - 1])) pos = m - 1;
+            else continue;
+            while (pos > 0 && lex_less(d, j, rd[pos - 1], ri[pos - 1])) {
+                rd[pos] = rd[pos - 1];
+                ri[pos] = ri[pos - 1];
+                pos--;
+            }
+            rd[pos] = d;
+            ri[pos] = j;
+        }
+    }
+};
+
+__global__ __launch_bounds__(kB) void k_radius_fill(GridDesc g, const double4* pts, const int32_t* mapping,
+                                                    int identity, const double* q, size_t qstride, int64_t nq,
+                                                    double r2, double mc, const int64_t* off, int32_t* oidx,
+                                                    double* od2) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = off[i], m = off[i + 1] - o;
+        if (m <= 0) continue;
+        const double* qp = qptr(q, qstride, i);
+        FillVisitor v{pts, qp[0], qp[1], qp[2], r2, r2 * (1.0 + 1e-12), oidx + o, od2 + o, m, 0};
+        ring_search<double>(g, v.qx, v.qy, v.qz, mc, v);
+        if (!identity)
+            for (int64_t r = 0; r < v.filled; r++) v.ri[r] = mapping[v.ri[r]];
+    }
+}
+
+// ------------------------------------------------------------------ F1: PCA normals
+// Device restatement of the deterministic core (calculate_feature.cpp:119-206): sequential
+// fp64 mean, centred X X^T, cyclic Jacobi eigen (eigenvalues descending, eigenvectors as
+// rows: the cvEigenVV convention, :165), normal = eigenvector of the smallest eigenvalue,
+// sign canonicalised (largest |component| positive; OpenCV's sign is unpinned).
+__device__ void eigen_sym3(const double Ain[9], double ev[3], double E[9]) {
+    double A[9], V[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+#pragma unroll
+    for (int i = 0; i < 9; i++) A[i] = Ain[i];
+    for (int sweep = 0; sweep < 64; sweep++) {
+        const double off = fabs(A[1]) + fabs(A[2]) + fabs(A[5]);
+        const double scale = fabs(A[0]) + fabs(A[4]) + fabs(A[8]);
+        if (off == 0.0 || off <= 1e-300 || off < 1e-18 * scale) break;
+#pragma unroll
+        for (int pq = 0; pq < 3; pq++) {
+            const int p = pq == 2 ? 1 : 0, qq = pq == 0 ? 1 : 2;
+            const double apq = A[3 * p + qq];
+            if (apq == 0.0) continue;
+            const double app = A[3 * p + p], aqq = A[3 * qq + qq];
+            const double theta = (aqq - app) / (2.0 * apq);
+            const double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+            const double cs = 1.0 / sqrt(tt * tt + 1.0), sn = tt * cs;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const double arp = A[3 * r + p], arq = A[3 * r + qq];
+                A[3 * r + p] = cs * arp - sn * arq;
+                A[3 * r + qq] = sn * arp + cs * arq;
+            }
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const double apr = A[3 * p + r], aqr = A[3 * qq + r];
+                A[3 * p + r] = cs * apr - sn * aqr;
+                A[3 * qq + r] = sn * apr + cs * aqr;
+            }
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const double vrp = V[3 * r + p], vrq = V[3 * r + qq];
+                V[3 * r + p] = cs * vrp - sn * vrq;
+                V[3 * r + qq] = sn * vrp + cs * vrq;
+            }
+        }
+    }
+    const double d[3] = {A[0], A[4], A[8]};
+    int ord[3] = {0, 1, 2};
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int jj = i + 1; jj < 3; jj++)
+            if (d[ord[jj]] > d[ord[i]]) { const int t = ord[i]; ord[i] = ord[jj]; ord[jj] = t; }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        ev[i] = d[ord[i]];
+#pragma unroll
+        for (int r = 0; r < 3; r++) E[3 * i + r] = V[3 * r + ord[i]];
+    }
+}
+
+__device__ void plane_from_cov(const double C[9], double xa, double ya, double za, pcp_plane& out) {
+    double ev[3], E[9];
+    eigen_sym3(C, ev, E);
+    int nummin = 0, nummax = 0;  // calculate_feature.cpp:168-179
+    double vmin = ev[0], vmax = ev[0];
+    for (int i = 0; i < 3; i++) {
+        if (vmin > ev[i]) { vmin = ev[i]; nummin = i; }
+        if (vmax < ev[i]) { vmax = ev[i]; nummax = i; }
+    }
+    double l1 = 0, l2 = 0, l3 = 0;  // :180-192
+    for (int i = 0; i < 3; i++) {
+        if (i == nummin) l3 = ev[nummin];
+        else if (i == nummax) l1 = ev[nummax];
+        else l2 = ev[i];
+    }
+    double n[3] = {E[3 * nummin], E[3 * nummin + 1], E[3 * nummin + 2]};
+    int big = 0;
+    for (int a = 1; a < 3; a++)
+        if (fabs(n[a]) > fabs(n[big])) big = a;
+    if (n[big] < 0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+    out.normal_x = (float)n[0];
+    out.normal_y = (float)n[1];
+    out.normal_z = (float)n[2];
+    // Distance uses the float normal (PlanSegment float fields, :197)
+    const double dist = -((double)out.normal_x * xa + (double)out.normal_y * ya + (double)out.normal_z * za);
+    out.distance = (float)dist;
+    out.min_value = (float)l3;                     // :198
+    out.curvature = (float)(l3 / (l1 + l2 + l3));  // :199
+}
+
+__global__ void k_plane_default(pcp_plane* out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = pcp_plane{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};  // rpca's N <= 3 branch (:353-361)
+}
+
+// queries = the indexed points themselves, walked in the index's spatial order
+template <int K>
+__global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, const int32_t* mapping, int identity,
+                                                const int32_t* pos_of_j, int64_t n, int kk, double mc,
+                                                pcp_plane* out, int64_t n_out) {
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+        const double4 qp = pts[s];
+        KnnVisitor<K> v;
+        v.pts = pts;
+        v.qx = qp.x; v.qy = qp.y; v.qz = qp.z;
+        v.top.init(kk);
+        ring_search<double>(g, v.qx, v.qy, v.qz, mc, v);
+        const int jq = (int)qp.w;
+        const int64_t oi = identity ? jq : mapping[jq];
+        if (oi >= n_out) continue;
+        // mean, sequential in kNN order (:131-142)
+        double xa = 0, ya = 0, za = 0;
+#pragma unroll
+        for (int r = 0; r < K; r++)
+            if (r < kk) {
+                const double4 p = pts[pos_of_j[v.top.j[r]]];
+                xa += p.x; ya += p.y; za += p.z;
+            }
+        xa /= kk; ya /= kk; za /= kk;
+        double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+#pragma unroll
+        for (int r = 0; r < K; r++)
+            if (r < kk) {
+                const double4 p = pts[pos_of_j[v.top.j[r]]];
+                const double x0 = p.x - xa, x1 = p.y - ya, x2 = p.z - za;
+                c00 += x0 * x0; c01 += x0 * x1; c02 += x0 * x2;
+                c11 += x1 * x1; c12 += x1 * x2; c22 += x2 * x2;
+            }
+        const double C[9] = {c00, c01, c02, c01, c11, c12, c02, c12, c22};
+        pcp_plane pl;
+        plane_from_cov(C, xa, ya, za, pl);
+        out[oi] = pl;
+    }
+}
+
+// ------------------------------------------------------------------ K6: kd_tree_lod
+// fp32 kNN over the float vertices float(p - c) (kd_tree_lod/kd_tree.cpp:39-43, 62-68;
+// the trimesh2 search is external: exact k nearest, ties by vertex index).
+template <int K>
+struct TopKf {
+    float d[K];
+    int j[K];
+    float kth;
+    int kthj;
+    int k;
+    __device__ void init(int k_) {
+        k = k_;
+#pragma unroll
+        for (int i = 0; i < K; i++) { d[i] = INFINITY; j[i] = INT_MAX; }
+        kth = INFINITY;
+        kthj = INT_MAX;
+    }
+    __device__ static bool less(float a, int ja, float b, int jb) { return a < b || (a == b && ja < jb); }
+    __device__ void push(float x, int jx) {
+        if (!less(x, jx, kth, kthj)) return;
+        bool c[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) c[i] = less(x, jx, d[i], j[i]);
+#pragma unroll
+        for (int i = K - 1; i >= 1; i--) {
+            if (c[i - 1]) { d[i] = d[i - 1]; j[i] = j[i - 1]; }
+            else if (c[i]) { d[i] = x; j[i] = jx; }
+        }
+        if (c[0]) { d[0] = x; j[0] = jx; }
+#pragma unroll
+        for (int i = 0; i < K; i++)
+            if (i == k - 1) { kth = d[i]; kthj = j[i]; }
+    }
+};
+
+template <int K>
+struct LodVisitor {
+    const float4* pts;
+    float qx, qy, qz;
+    TopKf<K> top;
+    __device__ float bound() const { return top.kth * (1.0f + 1e-5f); }
+    __device__ void visit(uint32_t s, uint32_t e) {
+        for (uint32_t t = s; t < e; t++) {
+            const float4 p = pts[t];
+            const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+            float d = dx * dx;
+            d = d + dy * dy;
+            d = d + dz * dz;
+            top.push(d, __float_as_int(p.w));
+        }
+    }
+};
+
+// first original j with point_dis2(k_point, cloud[j]) <= FLT_EPSILON (kd_tree.cpp:91-105)
+struct MatchVisitor {
+    const double4* pts;
+    const int32_t* mapping;
+    int identity;
+    double kx, ky, kz;
+    int best;
+    double bestd;
+    __device__ double bound() const { return (double)FLT_EPSILON * (1.0 + 1e-9); }
+    __device__ void visit(uint32_t s, uint32_t e) {
+        for (uint32_t t = s; t < e; t++) {
+            const double4 p = pts[t];
+            const double dx = kx - p.x, dy = ky - p.y, dz = kz - p.z;
+            double d = dx * dx + dy * dy;  // pow(.,2) + pow(.,2) + pow(.,2)
+            d = d + dz * dz;
+            if (d <= (double)FLT_EPSILON) {
+                const int jo = identity ? (int)p.w : mapping[(int)p.w];
+                if (jo < best) { best = jo; bestd = d; }
+            }
+        }
+    }
+};
+
+template <int K>
+__global__ __launch_bounds__(kB) void k_lod(GridDesc gf, const float4* fpts, GridDesc gd, const double4* dpts,
+                                            const int32_t* dmap, int didentity, const char* cloud, int64_t n,
+                                            const char* q, int64_t nq, int k, int kk, float mcf, double mcd,
+                                            int ci0, int ci1, int ci2, int32_t* oidx, double* od2) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+        const double* qp = (const double*)(q + i * PCP_AOS48_STRIDE);
+        LodVisitor<K> v;
+        v.pts = fpts;
+        v.qx = (float)(qp[0] - ci0); v.qy = (float)(qp[1] - ci1); v.qz = (float)(qp[2] - ci2);
+        v.top.init(kk);
+        ring_search<float>(gf, v.qx, v.qy, v.qz, mcf, v);
+        const double* last = (const double*)(cloud + (n - 1) * PCP_AOS48_STRIDE);
+#pragma unroll
+        for (int r = 0; r < K; r++) {
+            if (r >= kk) continue;
+            const int jv = v.top.j[r];
+            int index = -1;
+            double d2 = INFINITY;
+            if (jv != INT_MAX) {
+                const double* vp = (const double*)(cloud + (int64_t)jv * PCP_AOS48_STRIDE);
+                // vertex float(p - c), neighbour rebuilt as double(float + float(c)) (:71-73)
+                const float fx = (float)(vp[0] - ci0), fy = (float)(vp[1] - ci1), fz = (float)(vp[2] - ci2);
+                MatchVisitor m{dpts, dmap, didentity, (double)(float)(fx + (float)ci0),
+                               (double)(float)(fy + (float)ci1), (double)(float)(fz + (float)ci2), INT_MAX, 0.0};
+                ring_search<double>(gd, m.kx, m.ky, m.kz, mcd, m);
+                if (m.best != INT_MAX) {
+                    index = m.best;
+                    d2 = m.bestd;
+                } else {  // no match: k_dis2 = residual to the last scanned point (:100)
+                    const double dx = m.kx - last[0], dy = m.ky - last[1], dz = m.kz - last[2];
+                    double d = dx * dx + dy * dy;
+                    d2 = d + dz * dz;
+                }
+            }
+            oidx[i * k + r] = index;
+            od2[i * k + r] = d2;
+        }
+        for (int r = kk; r < k; r++) {
+            oidx[i * k + r] = -1;
+            od2[i * k + r] = INFINITY;
+        }
+    }
+}
+
+__global__ void k_lod_vertices(const char* cloud, int64_t n, int ci0, int ci1, int ci2, float* v) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double* p = (const double*)(cloud + i * PCP_AOS48_STRIDE);
+        v[3 * i + 0] = (float)(p[0] - ci0);
+        v[3 * i + 1] = (float)(p[1] - ci1);
+        v[3 * i + 2] = (float)(p[2] - ci2);
+    }
+}
+
+int pick_k(int k) {
+    if (k <= 1) return 1;
+    if (k <= 4) return 4;
+    if (k <= 8) return 8;
+    if (k <= 16) return 16;
+    if (k <= 32) return 32;
+    if (k <= 64) return 64;
+    return 0;
+}
+
+unsigned blocks_for(int64_t n) { return grid_for(n, kB, 1 << 22); }
+
+int check_f64_index(pcp_ctx* ctx, const pcp_index* ix) {
+    if (!ctx || !ix) return PCP_ERR_ARG;
+    if (!ix->is_f64) return set_error(ctx, PCP_ERR_ARG, "fp64 (FLANN-contract) index required");
+    return PCP_OK;
+}
+
+}  // namespace
+
+int centroid_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, double c[4], uint32_t* count);
+
+}  // namespace pcp
+
+using namespace pcp;
+
+extern "C" {
+
+int pcp_knn(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t qstride, int64_t nq, int k,
+            int32_t* oidx, double* od2) {
+    PCP_TRY(check_f64_index(ctx, ix));
+    if (nq < 0 || k <= 0 || (nq > 0 && (!q || !oidx))) return set_error(ctx, PCP_ERR_ARG, "pcp_knn: bad arguments");
+    if (qstride == 0) qstride = 3 * sizeof(double);
+    if (nq == 0) return PCP_OK;
+    const int kk = (int)(k < ix->n ? k : ix->n);  // kd_tree.h:820-821
+    const int K = pick_k(kk);
+    if (!K) return set_error(ctx, PCP_ERR_UNSUPPORTED, "pcp_knn: k=%d > 64 not supported yet", k);
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    const double mc = cell_margin64(ix->g);
+    const double4* pts = (const double4*)ix->pts;
+#define LAUNCH_KNN(KV)                                                                               \
+    hipLaunchKernelGGL(k_knn<KV>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping, \
+                       ix->identity, q, qstride, nq, k, kk, mc, oidx, od2)
+    switch (K) {
+        case 1: LAUNCH_KNN(1); break;
+        case 4: LAUNCH_KNN(4); break;
+        case 8: LAUNCH_KNN(8); break;
+        case 16: LAUNCH_KNN(16); break;
+        case 32: LAUNCH_KNN(32); break;
+        default: LAUNCH_KNN(64); break;
+    }
+#undef LAUNCH_KNN
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+static uint32_t radius_cap(const pcp_index* ix, uint32_t max_nn) {
+    // max_nn == 0 or > total => unlimited (kd_tree.h:873-883)
+    if (max_nn == 0 || (int64_t)max_nn >= ix->n) return UINT32_MAX;
+    return max_nn;
+}
+
+int pcp_radius_count(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t qstride, int64_t nq, double radius,
+                     uint32_t max_nn, int32_t* ocnt) {
+    PCP_TRY(check_f64_index(ctx, ix));
+    if (nq < 0 || (nq > 0 && (!q || !ocnt)) || !(radius >= 0))
+        return set_error(ctx, PCP_ERR_ARG, "pcp_radius_count: bad arguments");
+    if (qstride == 0) qstride = 3 * sizeof(double);
+    if (nq == 0) return PCP_OK;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_radius_count, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g,
+                       (const double4*)ix->pts, q, qstride, nq, radius * radius, radius_cap(ix, max_nn),
+                       cell_margin64(ix->g), ocnt);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_radius_fill(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t qstride, int64_t nq, double radius,
+                    uint32_t max_nn, const int64_t* off, int32_t* oidx, double* od2) {
+    PCP_TRY(check_f64_index(ctx, ix));
+    if (nq < 0 || (nq > 0 && (!q || !off || !oidx || !od2)) || !(radius >= 0))
+        return set_error(ctx, PCP_ERR_ARG, "pcp_radius_fill: bad arguments");
+    (void)max_nn;  // row lengths were fixed by the count pass
+    if (qstride == 0) qstride = 3 * sizeof(double);
+    if (nq == 0) return PCP_OK;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_radius_fill, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g,
+                       (const double4*)ix->pts, ix->mapping, ix->identity, q, qstride, nq, radius * radius,
+                       cell_margin64(ix->g), off, oidx, od2);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, int64_t n_out) {
+    PCP_TRY(check_f64_index(ctx, ix));
+    if (k <= 0 || n_out < 0 || (n_out > 0 && !out)) return set_error(ctx, PCP_ERR_ARG, "pcp_normals_knn: bad arguments");
+    if (n_out < ix->n_in) return set_error(ctx, PCP_ERR_CAPACITY, "pcp_normals_knn: n_out < cloud size");
+    const int kk = (int)(k < ix->n ? k : ix->n);
+    const int K = pick_k(kk);
+    if (!K || K > 32) return set_error(ctx, PCP_ERR_UNSUPPORTED, "pcp_normals_knn: k=%d > 32 not supported yet", k);
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (n_out > 0) hipLaunchKernelGGL(k_plane_default, dim3(blocks_for(n_out)), dim3(kB), 0, ctx->stream, out, n_out);
+    if (ix->n == 0 || kk <= 3) return PCP_OK;  // rpca's N > 3 guard (calculate_feature.cpp:237)
+    const double mc = cell_margin64(ix->g);
+    const double4* pts = (const double4*)ix->pts;
+#define LAUNCH_NRM(KV)                                                                                  \
+    hipLaunchKernelGGL(k_normals<KV>, dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping, \
+                       ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out)
+    switch (K) {
+        case 1: LAUNCH_NRM(1); break;
+        case 4: LAUNCH_NRM(4); break;
+        case 8: LAUNCH_NRM(8); break;
+        case 16: LAUNCH_NRM(16); break;
+        default: LAUNCH_NRM(32); break;
+    }
+#undef LAUNCH_NRM
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_knn_lod(pcp_ctx* ctx, const void* cloud, int64_t n, const void* q, int64_t nq, int k, int32_t* oidx,
+                double* od2) {
+    if (!ctx || n < 0 || nq < 0 || k <= 0 || (n > 0 && !cloud) || (nq > 0 && (!q || !oidx || !od2)))
+        return set_error(ctx, PCP_ERR_ARG, "pcp_knn_lod: bad arguments");
+    if (n == 0 || nq == 0) return PCP_OK;
+    const int kk = (int)(k < n ? k : n);
+    const int K = pick_k(kk);
+    if (!K || K > 32) return set_error(ctx, PCP_ERR_UNSUPPORTED, "pcp_knn_lod: k=%d > 32 not supported yet", k);
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    // c = Vector3i truncation of the centroid (kd_tree_lod/kd_tree.cpp:33-37)
+    double c[4];
+    uint32_t cnt = 0;
+    PCP_TRY(centroid_aos48_dev(ctx, cloud, n, 1, c, &cnt));
+    const int ci0 = (int)c[0], ci1 = (int)c[1], ci2 = (int)c[2];
+    float* v = nullptr;
+    PCP_TRY(dmalloc(ctx, &v, 3 * (size_t)n));
+    hipLaunchKernelGGL(k_lod_vertices, dim3(blocks_for(n)), dim3(kB), 0, ctx->stream, (const char*)cloud, n, ci0, ci1,
+                       ci2, v);
+    pcp_index* fi = nullptr;
+    pcp_index* di = nullptr;
+    int rc = pcp_index_build_f32(ctx, v, 3 * sizeof(float), n, 0.0, &fi);
+    if (rc == PCP_OK) rc = pcp_index_build_f64(ctx, (const double*)cloud, PCP_AOS48_STRIDE, n, nullptr, 0, 0.0, &di);
+    if (rc == PCP_OK) {
+        const GridDesc& gf = fi->g;
+        const int nmax = std::max(gf.n[0], std::max(gf.n[1], gf.n[2]));
+        const float mcf = 1e-5f + 8e-7f * (float)nmax;
+#define LAUNCH_LOD(KV)                                                                                     \
+    hipLaunchKernelGGL(k_lod<KV>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, fi->g, (const float4*)fi->pts, \
+                       di->g, (const double4*)di->pts, di->mapping, di->identity, (const char*)cloud, n,           \
+                       (const char*)q, nq, k, kk, mcf, cell_margin64(di->g), ci0, ci1, ci2, oidx, od2)
+        switch (K) {
+            case 1: LAUNCH_LOD(1); break;
+            case 4: LAUNCH_LOD(4); break;
+            case 8: LAUNCH_LOD(8); break;
+            case 16: LAUNCH_LOD(16); break;
+            default: LAUNCH_LOD(32); break;
+        }
+#undef LAUNCH_LOD
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) rc = hip_fail(ctx, e, "k_lod", __FILE__, __LINE__);
+    }
+    if (fi) pcp_index_destroy(fi);
+    if (di) pcp_index_destroy(di);
+    hipFree(v);
+    return rc;
+}
+
+}  // extern "C"

@@ -209,8 +209,7 @@ def remove_duplicate(ctx, cloud, leaf, is_dense=True):
 
 def normals_knn(index, k):
     ctx = index.ctx
-    n = ctx.lib.pcp_index_size(index.h)
-    n_out = index.src.shape[0] if index.indices is None else index.indices.numel()
+    n_out = index.src.shape[0]  # outputs are indexed by the caller's cloud index
     out = torch.empty((max(n_out, 1), 6), dtype=torch.float32, device=ctx.device)
     ctx.check(ctx.lib.pcp_normals_knn(ctx.h, index.h, int(k), _ptr(out), n_out))
     return out[:n_out]

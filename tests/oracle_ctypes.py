@@ -52,6 +52,7 @@ def load():
     lib.ora_voxel_filter.argtypes = [vp, C.c_int, C.c_int, C.c_double, C.c_double,
                                      C.c_double, C.c_int, vp, vp]
     lib.ora_remove_duplicate.argtypes = [vp, C.c_int, C.c_int, C.c_float, vp]
+    lib.ora_remove_duplicate_c.argtypes = [vp, C.c_int, C.c_int, C.c_float, vp, vp]
     lib.ora_plane_h_points.argtypes = [vp, C.c_int, vp]
     lib.ora_normals_knn.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_int, vp, C.c_int]
     lib.ora_eigen_sym3.argtypes = [vp, vp, vp]
@@ -140,6 +141,16 @@ def remove_duplicate(cloud, leaf, is_dense=True):
     out = np.zeros(max(len(cloud), 1), dtype=POINT48)
     m = lib.ora_remove_duplicate(cloud.ctypes.data, len(cloud), int(is_dense),
                                  float(leaf), out.ctypes.data)
+    return out[:m]
+
+
+def remove_duplicate_c(cloud, leaf, c, is_dense=True):
+    lib = load()
+    cloud = np.ascontiguousarray(cloud)
+    out = np.zeros(max(len(cloud), 1), dtype=POINT48)
+    c = np.ascontiguousarray(np.asarray(c, dtype=np.float64)[:3])
+    m = lib.ora_remove_duplicate_c(cloud.ctypes.data, len(cloud), int(is_dense), float(leaf),
+                                   c.ctypes.data, out.ctypes.data)
     return out[:m]
 
 
