@@ -118,6 +118,9 @@ int pcp_scan_counts(pcp_ctx* ctx, const int32_t* count_dev, int64_t n, int64_t* 
 int pcp_knn_bruteforce(pcp_ctx* ctx, const double* target_dev, size_t t_stride_bytes,
                        int64_t nt, const double* q_dev, size_t q_stride_bytes, int64_t nq,
                        int k, int32_t* out_idx_dev, double* out_d2_dev);
+/* Queries of the last pcp_knn_bruteforce on this context whose MFMA candidate set could
+ * not be certified and were re-done by the exact fp64 scan (diagnostic). */
+int pcp_knn_bruteforce_last_fallback(const pcp_ctx* ctx, int64_t* n);
 
 /* kd_tree_lod KdTree::nearestKSearch (kd_tree_lod/kd_tree.cpp:78-117) over an AoS48 cloud:
  * integer-truncated centroid, float search, first j with point_dis2 <= FLT_EPSILON

@@ -16,6 +16,7 @@ struct pcp_ctx {
     // grow-only scratch arena (one per context; contexts are not shared across threads)
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
+    uint32_t bf_fallback = 0;  // queries of the last pcp_knn_bruteforce that needed the exact scan
 };
 
 namespace pcp {

@@ -104,6 +104,13 @@ __global__ void k_mark(GridDesc g, const T* cxyz, int64_t n, int32_t* brick) {
     }
 }
 
+// dense mode: brick occupancy for the two-level ring search (0 = occupied, -1 = empty)
+__global__ void k_brick_flag(int32_t* brick, int64_t nb) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nb;
+         i += (int64_t)gridDim.x * blockDim.x)
+        brick[i] = brick[i] ? 0 : -1;
+}
+
 __global__ void k_brick_bits(const int32_t* brick, int64_t nb, uint32_t* bits) {
     int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (w >= (nb + 31) / 32) return;
@@ -309,7 +316,11 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         if (g.dense) {
             ncells = ncells_dense;
             g.nslots = 0;
-            g.brick = nullptr;
+            if ((rc = dmalloc(ctx, &ix->brick, g.nbricks))) break;
+            PCP_HIP(ctx, hipMemsetAsync(ix->brick, 0, (size_t)g.nbricks * sizeof(int32_t), st));
+            if (n > 0) hipLaunchKernelGGL(k_mark<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, ix->brick);
+            hipLaunchKernelGGL(k_brick_flag, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks);
+            g.brick = ix->brick;
         } else {
             if ((rc = dmalloc(ctx, &ix->brick, g.nbricks))) break;
             PCP_HIP(ctx, hipMemsetAsync(ix->brick, 0, (size_t)g.nbricks * sizeof(int32_t), st));

@@ -71,20 +71,100 @@ __device__ __forceinline__ bool cell_range(const GridDesc& g, int cx, int cy, in
     return e > s;
 }
 
-// Exact ring search over cells in order of Chebyshev distance from the query's cell.
+// Exact two-level ring search.  Phase 1 visits cells in order of Chebyshev distance from
+// the query's cell up to kCellRings; phase 2 (only when the visitor's bound still reaches
+// further) walks rings of 4x4x4-cell bricks, skipping empty bricks through the brick
+// occupancy table and the cells phase 1 already covered -- so an isolated query costs
+// O((r/4h)^3) brick probes instead of O((r/h)^3) cell probes.
 //   V::bound()       current pruning radius^2 (in the index precision's units), may shrink
 //   V::visit(s, e)   scan sorted points [s,e)
-// Cells (and whole rings) whose box distance exceeds bound() (with a conservative margin
-// `mc` in cell units covering floor() rounding of both the cells and the query) are skipped
-// without touching memory.  Visiting order never changes the result: visitors keep a
-// lexicographic (d2, index) order.
+// Cells, bricks and whole rings whose box distance exceeds bound() (with a conservative
+// margin `mc` in cell units covering floor() rounding of both the cells and the query) are
+// skipped without touching their points.  Visiting order never changes the result:
+// visitors keep a lexicographic (d2, index) order.
+constexpr int kCellRings = 3;
+
+template <typename T>
+__device__ __forceinline__ T axis_gap(int c, int cq, T l) {
+    // cells between the query (cell cq, offset l in it) and cell c along one axis
+    return c < cq ? (l + (T)(cq - c - 1)) : (c > cq ? ((T)1 - l + (T)(c - cq - 1)) : (T)0);
+}
+
+template <typename T>
+__device__ __forceinline__ T sq_gap(T gcell, T mc) {
+    return gcell > mc ? (gcell - mc) * (gcell - mc) : (T)0;
+}
+
 template <typename T, typename Vis>
-__device__ __forceinline__ void ring_search(const GridDesc& g, T qx, T qy, T qz, T mc, Vis& vis) {
+__device__ void brick_search(const GridDesc& g, T fx, T fy, T fz, int cx, int cy, int cz, T lx, T ly, T lz,
+                             T mc, Vis& vis) {
+    const T h2 = (T)g.h * (T)g.h;
+    const int bx = cx >> 2, by = cy >> 2, bz = cz >> 2;  // floor division
+    // query offset inside its brick (cells) and the distance to the nearest brick face
+    const T ox = fx - (T)(4 * bx), oy = fy - (T)(4 * by), oz = fz - (T)(4 * bz);
+    const T bdmin = fmin(fmin(fmin(ox, (T)4 - ox), fmin(oy, (T)4 - oy)), fmin(oz, (T)4 - oz));
+    int far = 0;
+    far = max(far, max(bx - (g.nb[0] - 1), -bx));
+    far = max(far, max(by - (g.nb[1] - 1), -by));
+    far = max(far, max(bz - (g.nb[2] - 1), -bz));
+    const int sbmax = far + max(g.nb[0], max(g.nb[1], g.nb[2]));
+    for (int sb = 0; sb <= sbmax; sb++) {
+        if (sb > 0) {
+            const T rmin = (T)(4 * (sb - 1)) + bdmin - mc;
+            if (rmin > (T)0 && rmin * rmin * h2 > vis.bound()) return;
+        }
+        const int z0 = max(bz - sb, 0), z1 = min(bz + sb, g.nb[2] - 1);
+        const int y0 = max(by - sb, 0), y1 = min(by + sb, g.nb[1] - 1);
+        const int x0 = max(bx - sb, 0), x1 = min(bx + sb, g.nb[0] - 1);
+        if (z0 > z1 || y0 > y1 || x0 > x1) continue;
+        for (int zb = z0; zb <= z1; zb++) {
+            const bool zface = (zb == bz - sb) || (zb == bz + sb);
+            // brick box gap along z (cells)
+            const T gz = zb < bz ? (oz + (T)(4 * (bz - zb - 1))) : (zb > bz ? ((T)4 - oz + (T)(4 * (zb - bz - 1))) : (T)0);
+            const T gz2 = sq_gap(gz, mc);
+            if (gz2 * h2 > vis.bound()) continue;
+            for (int yb = y0; yb <= y1; yb++) {
+                const bool yface = zface || (yb == by - sb) || (yb == by + sb);
+                const T gy = yb < by ? (oy + (T)(4 * (by - yb - 1))) : (yb > by ? ((T)4 - oy + (T)(4 * (yb - by - 1))) : (T)0);
+                const T gyz2 = gz2 + sq_gap(gy, mc);
+                if (gyz2 * h2 > vis.bound()) continue;
+                const int step = yface ? 1 : 2 * sb;
+                for (int xb = yface ? x0 : bx - sb; xb <= x1; xb += (step > 0 ? step : 1)) {
+                    if (xb < x0) continue;
+                    const T gx = xb < bx ? (ox + (T)(4 * (bx - xb - 1))) : (xb > bx ? ((T)4 - ox + (T)(4 * (xb - bx - 1))) : (T)0);
+                    if ((gyz2 + sq_gap(gx, mc)) * h2 > vis.bound()) continue;
+                    if (g.brick[((int64_t)zb * g.nb[1] + yb) * g.nb[0] + xb] < 0) continue;  // empty brick
+                    // the brick's cells not covered by phase 1
+                    for (int z = 4 * zb; z < min(4 * zb + 4, g.n[2]); z++) {
+                        const T cz2 = sq_gap(axis_gap<T>(z, cz, lz), mc);
+                        const bool zin = abs(z - cz) <= kCellRings;
+                        for (int y = 4 * yb; y < min(4 * yb + 4, g.n[1]); y++) {
+                            const T cyz2 = cz2 + sq_gap(axis_gap<T>(y, cy, ly), mc);
+                            if (cyz2 * h2 > vis.bound()) continue;
+                            const bool yzin = zin && abs(y - cy) <= kCellRings;
+                            for (int x = 4 * xb; x < min(4 * xb + 4, g.n[0]); x++) {
+                                if (yzin && abs(x - cx) <= kCellRings) continue;
+                                if ((cyz2 + sq_gap(axis_gap<T>(x, cx, lx), mc)) * h2 > vis.bound()) continue;
+                                uint32_t st, en;
+                                if (cell_range(g, x, y, z, st, en)) vis.visit(st, en);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// kFar = false: cell rings only; returns false when the bound still reaches past them (the
+// caller then re-runs the query with kFar = true).  kFar = true: complete two-level search.
+template <typename T, typename Vis, bool kFar = true>
+__device__ __forceinline__ bool ring_search(const GridDesc& g, T qx, T qy, T qz, T mc, Vis& vis) {
     const T fx = cell_f<T>(g, qx, 0), fy = cell_f<T>(g, qy, 1), fz = cell_f<T>(g, qz, 2);
     const int cx = (int)Real<T>::floor_(fx), cy = (int)Real<T>::floor_(fy), cz = (int)Real<T>::floor_(fz);
     // offsets inside the query's own cell
     const T lx = fx - (T)cx, ly = fy - (T)cy, lz = fz - (T)cz;
-    const T h = (T)g.h;
+    const T h2 = (T)g.h * (T)g.h;
     const T dmin = fmin(fmin(fmin(lx, (T)1 - lx), fmin(ly, (T)1 - ly)), fmin(lz, (T)1 - lz));
     // the furthest ring that can still intersect the grid
     int far = 0;
@@ -92,37 +172,39 @@ __device__ __forceinline__ void ring_search(const GridDesc& g, T qx, T qy, T qz,
     far = max(far, max(cy - (g.n[1] - 1), -cy));
     far = max(far, max(cz - (g.n[2] - 1), -cz));
     const int rmax = far + max(g.n[0], max(g.n[1], g.n[2]));
-    for (int s = 0; s <= rmax; s++) {
+    const int smax = min(rmax, kCellRings);
+    for (int s = 0; s <= smax + 1; s++) {
         if (s > 0) {
             const T rmin = ((T)(s - 1) + dmin - mc);
-            if (rmin > (T)0 && rmin * rmin * h * h > vis.bound()) break;
+            if (rmin > (T)0 && rmin * rmin * h2 > vis.bound()) return true;
         }
+        if (s > smax) break;
         const int z0 = max(cz - s, 0), z1 = min(cz + s, g.n[2] - 1);
         const int y0 = max(cy - s, 0), y1 = min(cy + s, g.n[1] - 1);
         const int x0 = max(cx - s, 0), x1 = min(cx + s, g.n[0] - 1);
         if (z0 > z1 || y0 > y1 || x0 > x1) continue;
         for (int z = z0; z <= z1; z++) {
             const bool zface = (z == cz - s) || (z == cz + s);
-            const T gz = z < cz ? (lz + (T)(cz - z - 1)) : (z > cz ? ((T)1 - lz + (T)(z - cz - 1)) : (T)0);
-            const T gz2 = gz > mc ? (gz - mc) * (gz - mc) : (T)0;
-            if (gz2 * h * h > vis.bound()) continue;
+            const T gz2 = sq_gap(axis_gap<T>(z, cz, lz), mc);
+            if (gz2 * h2 > vis.bound()) continue;
             for (int y = y0; y <= y1; y++) {
                 const bool yface = zface || (y == cy - s) || (y == cy + s);
-                const T gy = y < cy ? (ly + (T)(cy - y - 1)) : (y > cy ? ((T)1 - ly + (T)(y - cy - 1)) : (T)0);
-                const T gyz2 = gz2 + (gy > mc ? (gy - mc) * (gy - mc) : (T)0);
-                if (gyz2 * h * h > vis.bound()) continue;
+                const T gyz2 = gz2 + sq_gap(axis_gap<T>(y, cy, ly), mc);
+                if (gyz2 * h2 > vis.bound()) continue;
                 const int step = yface ? 1 : 2 * s;
                 for (int x = yface ? x0 : cx - s; x <= x1; x += (step > 0 ? step : 1)) {
                     if (x < x0) continue;
-                    const T gx = x < cx ? (lx + (T)(cx - x - 1)) : (x > cx ? ((T)1 - lx + (T)(x - cx - 1)) : (T)0);
-                    const T g2 = gyz2 + (gx > mc ? (gx - mc) * (gx - mc) : (T)0);
-                    if (g2 * h * h > vis.bound()) continue;
+                    if ((gyz2 + sq_gap(axis_gap<T>(x, cx, lx), mc)) * h2 > vis.bound()) continue;
                     uint32_t st, en;
                     if (cell_range(g, x, y, z, st, en)) vis.visit(st, en);
                 }
             }
         }
     }
+    if (rmax <= kCellRings) return true;
+    if (!kFar) return false;
+    brick_search<T>(g, fx, fy, fz, cx, cy, cz, lx, ly, lz, mc, vis);
+    return true;
 }
 
 }  // namespace pcp

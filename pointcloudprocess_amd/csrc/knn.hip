@@ -10,29 +10,18 @@
 // so distances are bit-identical to the reference's and ties break on internal j exactly
 // like FLANN's "first found in index order" result set after sorting.
 #include <cfloat>
+#include <cstdlib>
 #include <climits>
 #include <cmath>
 #include <vector>
 
 #include "grid.hpp"
+#include "topk.hpp"
 
 namespace pcp {
 namespace {
 
 constexpr int kB = 256;
-
-__device__ __forceinline__ bool lex_less(double da, int ja, double db, int jb) {
-    return da < db || (da == db && ja < jb);
-}
-
-// FLANN L2_Simple<double> (external): r = 0; r += d0*d0; ...
-__device__ __forceinline__ double l2_simple(double qx, double qy, double qz, const double4& p) {
-    const double d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
-    double r = d0 * d0;
-    r = r + d1 * d1;
-    r = r + d2 * d2;
-    return r;
-}
 
 // pruning margin in cell units: floor() rounding of query and point cell coordinates
 __host__ __device__ inline double cell_margin64(const GridDesc& g) {
@@ -40,47 +29,13 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
     return 1e-9 + 8e-16 * (double)nmax;
 }
 
-// k best (d2, j) in registers; only the first `k` (runtime, <= K) entries are maintained.
-template <int K>
-struct TopK {
-    double d[K];
-    int j[K];
-    double kth;
-    int kthj;
-    int k;
-    __device__ void init(int k_) {
-        k = k_;
-#pragma unroll
-        for (int i = 0; i < K; i++) { d[i] = INFINITY; j[i] = INT_MAX; }
-        kth = INFINITY;
-        kthj = INT_MAX;
-    }
-    // pruning radius^2: a cell whose box lower bound exceeds it holds no point that could
-    // enter (1e-12 covers the rounding of the box bound and of d2 itself)
-    __device__ double bound() const { return kth * (1.0 + 1e-12); }
-    __device__ __forceinline__ void push(double x, int jx) {
-        if (!lex_less(x, jx, kth, kthj)) return;
-        bool c[K];
-#pragma unroll
-        for (int i = 0; i < K; i++) c[i] = lex_less(x, jx, d[i], j[i]);
-#pragma unroll
-        for (int i = K - 1; i >= 1; i--) {
-            if (c[i - 1]) { d[i] = d[i - 1]; j[i] = j[i - 1]; }
-            else if (c[i]) { d[i] = x; j[i] = jx; }
-        }
-        if (c[0]) { d[0] = x; j[0] = jx; }
-#pragma unroll
-        for (int i = 0; i < K; i++)
-            if (i == k - 1) { kth = d[i]; kthj = j[i]; }
-    }
-};
-
 template <int K>
 struct KnnVisitor {
     const double4* pts;
     double qx, qy, qz;
     TopK<K> top;
-    __device__ double bound() const { return top.bound(); }
+    // pruning radius^2 (1e-12 covers the rounding of the cell-box bound and of d2)
+    __device__ double bound() const { return top.kth() * (1.0 + 1e-12); }
     __device__ void visit(uint32_t s, uint32_t e) {
         for (uint32_t t = s; t < e; t++) {
             const double4 p = pts[t];
@@ -93,30 +48,54 @@ __device__ __forceinline__ const double* qptr(const double* q, size_t stride, in
     return (const double*)((const char*)q + (size_t)i * stride);
 }
 
+// Two-pass scheduling of the ring search (grid.hpp): the near pass (FAR = false) runs the
+// cell rings only and appends queries whose bound reaches past them to `far_list`; the far
+// pass (FAR = true) re-runs exactly those (or every query when far_list is null) with the
+// brick-level search.  Keeps the common path's register footprint small.
+struct FarList {
+    int32_t* list;
+    uint32_t* count;
+};
+
+// Deferred queries are few but each is expensive, so the far pass gives every one its own
+// wave (lane 0) to spread them over all CUs instead of packing them into a few waves.
+template <bool FAR>
+__device__ __forceinline__ int64_t work_count(const FarList& f, int64_t n) {
+    if (FAR && f.list) return (threadIdx.x & 63) ? 0 : (int64_t)*f.count * 64;
+    return n;
+}
+template <bool FAR>
+__device__ __forceinline__ int64_t work_item(const FarList& f, int64_t w) {
+    return (FAR && f.list) ? (int64_t)f.list[w >> 6] : w;
+}
+__device__ __forceinline__ void defer(const FarList& f, int64_t i) { f.list[atomicAdd(f.count, 1u)] = (int32_t)i; }
+
 // K3: batch nearestKSearch.  Rows ascending by (d2, internal j), indices mapped through
 // index_mapping_ (kd_tree.h:837-842); entries past min(k, size) are -1 / +inf.
-template <int K>
+template <int K, bool FAR>
 __global__ __launch_bounds__(kB) void k_knn(GridDesc g, const double4* pts, const int32_t* mapping, int identity,
                                             const double* q, size_t qstride, int64_t nq, int k, int kk,
-                                            double mc, int32_t* oidx, double* od2) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+                                            double mc, int32_t* oidx, double* od2, FarList far) {
+    const int64_t nw = work_count<FAR>(far, nq);
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = work_item<FAR>(far, w);
         const double* qp = qptr(q, qstride, i);
         KnnVisitor<K> v;
         v.pts = pts;
         v.qx = qp[0]; v.qy = qp[1]; v.qz = qp[2];
         v.top.init(kk);
-        if (kk > 0 && finite3(v.qx, v.qy, v.qz)) ring_search<double>(g, v.qx, v.qy, v.qz, mc, v);
+        if (kk > 0 && finite3(v.qx, v.qy, v.qz) &&
+            !ring_search<double, KnnVisitor<K>, FAR>(g, v.qx, v.qy, v.qz, mc, v)) {
+            defer(far, i);
+            continue;
+        }
         int32_t* ri = oidx + i * k;
         double* rd = od2 + i * k;
-#pragma unroll
-        for (int r = 0; r < K; r++) {
-            if (r < kk) {
-                const int j = v.top.j[r];
-                const bool ok = j != INT_MAX;
-                ri[r] = ok ? (identity ? j : mapping[j]) : -1;
-                if (od2) rd[r] = ok ? v.top.d[r] : INFINITY;
-            }
-        }
+        v.top.for_each_ascending(kk, [&](int r, double d, int j) {
+            const bool ok = j != INT_MAX;
+            ri[r] = ok ? (identity ? j : mapping[j]) : -1;
+            if (od2) rd[r] = ok ? d : INFINITY;
+        });
         for (int r = kk; r < k; r++) {
             ri[r] = -1;
             if (od2) rd[r] = INFINITY;
@@ -135,12 +114,19 @@ struct CountVisitor {
     }
 };
 
+template <bool FAR>
 __global__ __launch_bounds__(kB) void k_radius_count(GridDesc g, const double4* pts, const double* q, size_t qstride,
-                                                     int64_t nq, double r2, uint32_t cap, double mc, int32_t* ocnt) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+                                                     int64_t nq, double r2, uint32_t cap, double mc, int32_t* ocnt,
+                                                     FarList far) {
+    const int64_t nw = work_count<FAR>(far, nq);
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = work_item<FAR>(far, w);
         const double* qp = qptr(q, qstride, i);
         CountVisitor v{pts, qp[0], qp[1], qp[2], r2, r2 * (1.0 + 1e-12), 0u};
-        if (finite3(v.qx, v.qy, v.qz)) ring_search<double>(g, v.qx, v.qy, v.qz, mc, v);
+        if (finite3(v.qx, v.qy, v.qz) && !ring_search<double, CountVisitor, FAR>(g, v.qx, v.qy, v.qz, mc, v)) {
+            defer(far, i);
+            continue;
+        }
         ocnt[i] = (int32_t)(v.cnt < cap ? v.cnt : cap);
     }
 }
@@ -175,16 +161,22 @@ struct FillVisitor {
     }
 };
 
+template <bool FAR>
 __global__ __launch_bounds__(kB) void k_radius_fill(GridDesc g, const double4* pts, const int32_t* mapping,
                                                     int identity, const double* q, size_t qstride, int64_t nq,
                                                     double r2, double mc, const int64_t* off, int32_t* oidx,
-                                                    double* od2) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+                                                    double* od2, FarList far) {
+    const int64_t nw = work_count<FAR>(far, nq);
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = work_item<FAR>(far, w);
         const int64_t o = off[i], m = off[i + 1] - o;
         if (m <= 0) continue;
         const double* qp = qptr(q, qstride, i);
         FillVisitor v{pts, qp[0], qp[1], qp[2], r2, r2 * (1.0 + 1e-12), oidx + o, od2 + o, m, 0};
-        ring_search<double>(g, v.qx, v.qy, v.qz, mc, v);
+        if (!ring_search<double, FillVisitor, FAR>(g, v.qx, v.qy, v.qz, mc, v)) {
+            defer(far, i);  // the far pass rebuilds the row from scratch
+            continue;
+        }
         if (!identity)
             for (int64_t r = 0; r < v.filled; r++) v.ri[r] = mapping[v.ri[r]];
     }
@@ -283,38 +275,39 @@ __global__ void k_plane_default(pcp_plane* out, int64_t n) {
 }
 
 // queries = the indexed points themselves, walked in the index's spatial order
-template <int K>
+template <int K, bool FAR>
 __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, const int32_t* mapping, int identity,
                                                 const int32_t* pos_of_j, int64_t n, int kk, double mc,
-                                                pcp_plane* out, int64_t n_out) {
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+                                                pcp_plane* out, int64_t n_out, FarList far) {
+    const int64_t nw = work_count<FAR>(far, n);
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = work_item<FAR>(far, w);
         const double4 qp = pts[s];
         KnnVisitor<K> v;
         v.pts = pts;
         v.qx = qp.x; v.qy = qp.y; v.qz = qp.z;
         v.top.init(kk);
-        ring_search<double>(g, v.qx, v.qy, v.qz, mc, v);
+        if (!ring_search<double, KnnVisitor<K>, FAR>(g, v.qx, v.qy, v.qz, mc, v)) {
+            defer(far, s);
+            continue;
+        }
         const int jq = (int)qp.w;
         const int64_t oi = identity ? jq : mapping[jq];
         if (oi >= n_out) continue;
         // mean, sequential in kNN order (:131-142)
         double xa = 0, ya = 0, za = 0;
-#pragma unroll
-        for (int r = 0; r < K; r++)
-            if (r < kk) {
-                const double4 p = pts[pos_of_j[v.top.j[r]]];
-                xa += p.x; ya += p.y; za += p.z;
-            }
+        v.top.for_each_ascending(kk, [&](int, double, int j) {
+            const double4 p = pts[pos_of_j[j]];
+            xa += p.x; ya += p.y; za += p.z;
+        });
         xa /= kk; ya /= kk; za /= kk;
         double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
-#pragma unroll
-        for (int r = 0; r < K; r++)
-            if (r < kk) {
-                const double4 p = pts[pos_of_j[v.top.j[r]]];
-                const double x0 = p.x - xa, x1 = p.y - ya, x2 = p.z - za;
-                c00 += x0 * x0; c01 += x0 * x1; c02 += x0 * x2;
-                c11 += x1 * x1; c12 += x1 * x2; c22 += x2 * x2;
-            }
+        v.top.for_each_ascending(kk, [&](int, double, int j) {
+            const double4 p = pts[pos_of_j[j]];
+            const double x0 = p.x - xa, x1 = p.y - ya, x2 = p.z - za;
+            c00 += x0 * x0; c01 += x0 * x1; c02 += x0 * x2;
+            c11 += x1 * x1; c12 += x1 * x2; c22 += x2 * x2;
+        });
         const double C[9] = {c00, c01, c02, c01, c11, c12, c02, c12, c22};
         pcp_plane pl;
         plane_from_cov(C, xa, ya, za, pl);
@@ -326,43 +319,11 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
 // fp32 kNN over the float vertices float(p - c) (kd_tree_lod/kd_tree.cpp:39-43, 62-68;
 // the trimesh2 search is external: exact k nearest, ties by vertex index).
 template <int K>
-struct TopKf {
-    float d[K];
-    int j[K];
-    float kth;
-    int kthj;
-    int k;
-    __device__ void init(int k_) {
-        k = k_;
-#pragma unroll
-        for (int i = 0; i < K; i++) { d[i] = INFINITY; j[i] = INT_MAX; }
-        kth = INFINITY;
-        kthj = INT_MAX;
-    }
-    __device__ static bool less(float a, int ja, float b, int jb) { return a < b || (a == b && ja < jb); }
-    __device__ void push(float x, int jx) {
-        if (!less(x, jx, kth, kthj)) return;
-        bool c[K];
-#pragma unroll
-        for (int i = 0; i < K; i++) c[i] = less(x, jx, d[i], j[i]);
-#pragma unroll
-        for (int i = K - 1; i >= 1; i--) {
-            if (c[i - 1]) { d[i] = d[i - 1]; j[i] = j[i - 1]; }
-            else if (c[i]) { d[i] = x; j[i] = jx; }
-        }
-        if (c[0]) { d[0] = x; j[0] = jx; }
-#pragma unroll
-        for (int i = 0; i < K; i++)
-            if (i == k - 1) { kth = d[i]; kthj = j[i]; }
-    }
-};
-
-template <int K>
 struct LodVisitor {
     const float4* pts;
     float qx, qy, qz;
-    TopKf<K> top;
-    __device__ float bound() const { return top.kth * (1.0f + 1e-5f); }
+    TopK<K, float> top;
+    __device__ float bound() const { return top.kth() * (1.0f + 1e-5f); }
     __device__ void visit(uint32_t s, uint32_t e) {
         for (uint32_t t = s; t < e; t++) {
             const float4 p = pts[t];
@@ -411,10 +372,7 @@ __global__ __launch_bounds__(kB) void k_lod(GridDesc gf, const float4* fpts, Gri
         v.top.init(kk);
         ring_search<float>(gf, v.qx, v.qy, v.qz, mcf, v);
         const double* last = (const double*)(cloud + (n - 1) * PCP_AOS48_STRIDE);
-#pragma unroll
-        for (int r = 0; r < K; r++) {
-            if (r >= kk) continue;
-            const int jv = v.top.j[r];
+        v.top.for_each_ascending(kk, [&](int r, float, int jv) {
             int index = -1;
             double d2 = INFINITY;
             if (jv != INT_MAX) {
@@ -429,13 +387,13 @@ __global__ __launch_bounds__(kB) void k_lod(GridDesc gf, const float4* fpts, Gri
                     d2 = m.bestd;
                 } else {  // no match: k_dis2 = residual to the last scanned point (:100)
                     const double dx = m.kx - last[0], dy = m.ky - last[1], dz = m.kz - last[2];
-                    double d = dx * dx + dy * dy;
-                    d2 = d + dz * dz;
+                    double dd = dx * dx + dy * dy;
+                    d2 = dd + dz * dz;
                 }
             }
             oidx[i * k + r] = index;
             od2[i * k + r] = d2;
-        }
+        });
         for (int r = kk; r < k; r++) {
             oidx[i * k + r] = -1;
             od2[i * k + r] = INFINITY;
@@ -474,6 +432,22 @@ int check_f64_index(pcp_ctx* ctx, const pcp_index* ix) {
 
 int centroid_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, double c[4], uint32_t* count);
 
+// deferred-query list of one call (freed on scope exit; hipFree synchronises)
+struct FarBuf {
+    FarList f{nullptr, nullptr};
+    ~FarBuf() { hipFree(f.list); hipFree(f.count); }
+    int alloc(pcp_ctx* ctx, int64_t n) {
+        PCP_TRY(dmalloc(ctx, &f.list, n));
+        PCP_TRY(dmalloc(ctx, &f.count, 1));
+        PCP_HIP(ctx, hipMemsetAsync(f.count, 0, sizeof(uint32_t), ctx->stream));
+        return PCP_OK;
+    }
+};
+constexpr unsigned kFarBlocks = 2048;
+
+// a fixed radius that reaches past the near pass's cell rings goes straight to the far pass
+bool radius_needs_far(const pcp_index* ix, double radius) { return radius * ix->g.inv_h >= (double)kCellRings; }
+
 }  // namespace pcp
 
 using namespace pcp;
@@ -492,9 +466,13 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t qstride, 
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     const double mc = cell_margin64(ix->g);
     const double4* pts = (const double4*)ix->pts;
-#define LAUNCH_KNN(KV)                                                                               \
-    hipLaunchKernelGGL(k_knn<KV>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping, \
-                       ix->identity, q, qstride, nq, k, kk, mc, oidx, od2)
+    FarBuf fb;
+    PCP_TRY(fb.alloc(ctx, nq));
+#define LAUNCH_KNN(KV)                                                                                          \
+    hipLaunchKernelGGL((k_knn<KV, false>), dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,  \
+                       ix->identity, q, qstride, nq, k, kk, mc, oidx, od2, fb.f);                                  \
+    hipLaunchKernelGGL((k_knn<KV, true>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,        \
+                       ix->identity, q, qstride, nq, k, kk, mc, oidx, od2, fb.f)
     switch (K) {
         case 1: LAUNCH_KNN(1); break;
         case 4: LAUNCH_KNN(4); break;
@@ -505,6 +483,11 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t qstride, 
     }
 #undef LAUNCH_KNN
     PCP_LAUNCH_CHECK(ctx);
+    if (getenv("PCP_KNN_DEBUG")) {
+        uint32_t c = 0;
+        hipMemcpy(&c, fb.f.count, 4, hipMemcpyDeviceToHost);
+        fprintf(stderr, "pcp_knn: k=%d nq=%lld deferred to the far pass: %u\n", k, (long long)nq, c);
+    }
     return PCP_OK;
 }
 
@@ -522,9 +505,20 @@ int pcp_radius_count(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t 
     if (qstride == 0) qstride = 3 * sizeof(double);
     if (nq == 0) return PCP_OK;
     PCP_HIP(ctx, hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(k_radius_count, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g,
-                       (const double4*)ix->pts, q, qstride, nq, radius * radius, radius_cap(ix, max_nn),
-                       cell_margin64(ix->g), ocnt);
+    const double4* pts = (const double4*)ix->pts;
+    const uint32_t cap = radius_cap(ix, max_nn);
+    const double mc = cell_margin64(ix->g);
+    if (radius_needs_far(ix, radius)) {
+        hipLaunchKernelGGL(k_radius_count<true>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, q, qstride,
+                           nq, radius * radius, cap, mc, ocnt, FarList{nullptr, nullptr});
+    } else {
+        FarBuf fb;
+        PCP_TRY(fb.alloc(ctx, nq));
+        hipLaunchKernelGGL(k_radius_count<false>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, q,
+                           qstride, nq, radius * radius, cap, mc, ocnt, fb.f);
+        hipLaunchKernelGGL(k_radius_count<true>, dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, q, qstride,
+                           nq, radius * radius, cap, mc, ocnt, fb.f);
+    }
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }
@@ -538,9 +532,19 @@ int pcp_radius_fill(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t q
     if (qstride == 0) qstride = 3 * sizeof(double);
     if (nq == 0) return PCP_OK;
     PCP_HIP(ctx, hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(k_radius_fill, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g,
-                       (const double4*)ix->pts, ix->mapping, ix->identity, q, qstride, nq, radius * radius,
-                       cell_margin64(ix->g), off, oidx, od2);
+    const double4* pts = (const double4*)ix->pts;
+    const double mc = cell_margin64(ix->g);
+    if (radius_needs_far(ix, radius)) {
+        hipLaunchKernelGGL(k_radius_fill<true>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,
+                           ix->identity, q, qstride, nq, radius * radius, mc, off, oidx, od2, FarList{nullptr, nullptr});
+    } else {
+        FarBuf fb;
+        PCP_TRY(fb.alloc(ctx, nq));
+        hipLaunchKernelGGL(k_radius_fill<false>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts,
+                           ix->mapping, ix->identity, q, qstride, nq, radius * radius, mc, off, oidx, od2, fb.f);
+        hipLaunchKernelGGL(k_radius_fill<true>, dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,
+                           ix->identity, q, qstride, nq, radius * radius, mc, off, oidx, od2, fb.f);
+    }
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }
@@ -557,9 +561,13 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
     if (ix->n == 0 || kk <= 3) return PCP_OK;  // rpca's N > 3 guard (calculate_feature.cpp:237)
     const double mc = cell_margin64(ix->g);
     const double4* pts = (const double4*)ix->pts;
-#define LAUNCH_NRM(KV)                                                                                  \
-    hipLaunchKernelGGL(k_normals<KV>, dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping, \
-                       ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out)
+    FarBuf fb;
+    PCP_TRY(fb.alloc(ctx, ix->n));
+#define LAUNCH_NRM(KV)                                                                                              \
+    hipLaunchKernelGGL((k_normals<KV, false>), dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts,          \
+                       ix->mapping, ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb.f);                      \
+    hipLaunchKernelGGL((k_normals<KV, true>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,      \
+                       ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb.f)
     switch (K) {
         case 1: LAUNCH_NRM(1); break;
         case 4: LAUNCH_NRM(4); break;

@@ -154,6 +154,12 @@ def knn_bruteforce(ctx, target, q, k):
     return idx, d2
 
 
+def knn_bruteforce_last_fallback(ctx):
+    n = C.c_int64()
+    ctx.check(ctx.lib.pcp_knn_bruteforce_last_fallback(ctx.h, C.byref(n)))
+    return n.value
+
+
 def knn_lod(ctx, cloud, q, k):
     nq = q.shape[0]
     idx = torch.empty((nq, k), dtype=torch.int32, device=ctx.device)
