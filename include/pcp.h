@@ -112,6 +112,13 @@ int pcp_radius_fill(pcp_ctx* ctx, const pcp_index* index, const double* q_dev,
 int pcp_scan_counts(pcp_ctx* ctx, const int32_t* count_dev, int64_t n, int64_t* offsets_dev,
                     int64_t* total_host);
 
+/* Callers' reduction over K3 (main_blend.cpp:306-325 find_cloud_nearest_point_in_kdtree):
+ * the query whose 1-NN d2 is smallest, strict '<' against init_bound (9999 there), so the
+ * first query wins ties.  *best_q = -1 when no query beats init_bound. */
+int pcp_nearest_query(pcp_ctx* ctx, const pcp_index* index, const double* q_dev,
+                      size_t q_stride_bytes, int64_t nq, double init_bound, int64_t* best_q_host,
+                      double* best_d2_host);
+
 /* Brute-force kNN (BASELINE config 2): fp32 MFMA ranking of |p|^2 - 2 q.p over LDS tiles,
  * certified + re-ranked in fp64, falling back to an exact fp64 scan for any query whose
  * candidate set cannot be certified.  Same output contract as pcp_knn (no index). */
@@ -158,6 +165,15 @@ int pcp_remove_duplicate(pcp_ctx* ctx, const void* in_aos48_dev, int64_t n, int 
  * points dropped as non-finite get {0,0,0,1}); sign: largest-|.| component positive. */
 int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* index, int k, pcp_plane* out_dev,
                     int64_t n_out);
+
+/* One plane per CSR segment (calculate_plan_parameter_h_points, calculate_feature.cpp:
+ * 119-206, per segment; with radiusSearch rows as segments this is the declared-only
+ * calculate_plan_parameter(cloud, radius), calculate_feature.h:15).  Segment s covers
+ * points xyz[idx[t]] (idx_dev NULL: xyz[t]) for t in [offsets[s], offsets[s+1]), summed
+ * in that order; an empty segment gets {0,0,0,0,1,0}. */
+int pcp_plane_fit_segments(pcp_ctx* ctx, const double* xyz_dev, size_t stride_bytes,
+                           const int64_t* offsets_dev, const int32_t* idx_dev, int64_t nseg,
+                           pcp_plane* out_dev);
 
 /* ----------------------------------------------------------------------- I: ICP */
 /* ICP correspondence/transform loop (point_cloud_helper.cpp:75-166 get_rot_icp ->

@@ -1,0 +1,737 @@
+// pcp_pcl.hpp -- drop-in C++ surface of the RioWong/PointCloudProcess hot path, on top of
+// the libpcp C-ABI (pcp.h).  Header-only; needs neither Eigen, Boost, FLANN, OpenCV nor
+// trimesh2.  Class and method names, argument meaning and visible error behaviour follow the
+// reference (namespace cloud_blend_double, macros.h:6):
+//
+//   KdTreeFLANN<PointT>   kd_tree.h:659-997   (exact kNN / radius, index_mapping_)
+//   KdTree (lod)          kd_tree_lod/kd_tree.h, .cpp:29-117  (as cloud_blend_double::lod::KdTree)
+//   VoxelGrid<PointT>     voxel_grid.h:496-1056
+//   CalculateFeature      calculate_feature.h:11-16
+//   PointCloudHelper      point_cloud_helper.h:16-233 (remove_duplicate, get_rot_icp,
+//                         transformPointCloud, compute3DCentroid, getMinMax3D, point_dis2)
+//   CloudStampRot         cloud_stamp_rot.h:7-39
+//   PointXYZRGBA / PointCloud / PlanSegment / LAS_POINT_PROPERTY (point_type.h, point_cloud.h,
+//   data_struct.h)
+//
+// Matrices: every Matrix4d / Vector4d parameter is a template accepting anything with
+// operator()(int,int) / operator[](int) (Eigen::Matrix4d works unchanged; Mat4d/Vec4d below
+// serve callers without Eigen).
+//
+// Device: all calls run on one process-wide pcp context (device PCP_DEVICE env or 0, the
+// device's default stream).  const searches may be called concurrently from OpenMP threads
+// (calculate_feature.cpp:216-233): the shim serialises them on the context mutex.  The batch
+// methods (nearestKSearchBatch / radiusSearchBatch / normals) are the fast path; the
+// per-point overloads keep the reference's call sites compiling and correct.
+// Non-zero pcp status -> the reference's visible behaviour: empty results for searches,
+// PCLException for VoxelGrid, err = -1 for ICP (SURVEY.md §8(b) "Errors").
+#ifndef PCP_PCL_HPP
+#define PCP_PCL_HPP
+
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pcp.h"
+
+namespace cloud_blend_double {
+
+// ------------------------------------------------------------------ types
+struct alignas(16) PointXYZRGBA {  // point_type.h:9-89 (EIGEN_ALIGN16, 48 bytes)
+    union {
+        double data[4];
+        struct {
+            double x, y, z;
+        };
+    };
+    union {
+        uint32_t rgba;
+        struct {
+            uint8_t b, g, r, a;
+        };
+    };
+    uint32_t stamp_id;
+    PointXYZRGBA() : rgba(0), stamp_id(0) {
+        data[0] = data[1] = data[2] = 0.0;
+        data[3] = 1.0;
+    }
+    PointXYZRGBA(double x_, double y_, double z_) : PointXYZRGBA() { x = x_; y = y_; z = z_; }
+};
+static_assert(sizeof(PointXYZRGBA) == PCP_AOS48_STRIDE, "PointXYZRGBA must be the 48-byte AoS record");
+
+template <class PointT>
+class PointCloud {  // point_cloud.h:295-311 (the fields the hot path uses)
+public:
+    typedef std::shared_ptr<PointCloud<PointT>> Ptr;
+    typedef std::shared_ptr<const PointCloud<PointT>> ConstPtr;
+    std::vector<PointT> points;
+    uint32_t width = 0, height = 1;
+    bool is_dense = true;
+    size_t size() const { return points.size(); }
+    bool empty() const { return points.empty(); }
+    void push_back(const PointT& p) { points.push_back(p); width = (uint32_t)points.size(); height = 1; }
+    void clear() { points.clear(); width = 0; }
+    PointT& operator[](size_t i) { return points[i]; }
+    const PointT& operator[](size_t i) const { return points[i]; }
+    Ptr makeShared() const { return Ptr(new PointCloud<PointT>(*this)); }
+};
+
+typedef PointXYZRGBA CloudItem;  // cmm_types.h:11-14
+typedef PointCloud<CloudItem> Cloud;
+typedef Cloud::Ptr CloudPtr;
+typedef Cloud::ConstPtr CloudConstPtr;
+
+struct PlanSegment {  // data_struct.h:188-198
+    unsigned short SegmentID = 0;
+    std::vector<int> PointID;
+    float normal_x = 0, normal_y = 0, normal_z = 0;
+    float min_value = 0;
+    float curvature = 0;
+    float Distance = 0;
+};
+
+struct LAS_POINT_PROPERTY {  // data_struct.h:161-172
+    float normal_x, normal_y, normal_z;
+    double Distance;
+    double curvature;
+    int PointID;
+    int SegmentID;
+    float dis_from_point_plane;
+};
+
+class PCLException : public std::runtime_error {  // exception.h:11
+public:
+    explicit PCLException(const std::string& m) : std::runtime_error(m) {}
+};
+
+// Minimal row-major 4x4 / 4-vector for callers without Eigen.
+struct Mat4d {
+    double m[16];
+    static Mat4d Identity() {
+        Mat4d r;
+        for (int i = 0; i < 16; i++) r.m[i] = (i % 5 == 0) ? 1.0 : 0.0;
+        return r;
+    }
+    double& operator()(int r, int c) { return m[4 * r + c]; }
+    double operator()(int r, int c) const { return m[4 * r + c]; }
+    Mat4d operator*(const Mat4d& b) const {
+        Mat4d o;
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) {
+                double s = 0;
+                for (int k = 0; k < 4; k++) s += (*this)(i, k) * b(k, j);
+                o(i, j) = s;
+            }
+        return o;
+    }
+};
+struct Vec4d {
+    double v[4] = {0, 0, 0, 0};
+    double& operator[](int i) { return v[i]; }
+    double operator[](int i) const { return v[i]; }
+    double& operator()(int i) { return v[i]; }
+    double operator()(int i) const { return v[i]; }
+};
+
+// ------------------------------------------------------------------ device plumbing
+namespace detail {
+
+inline void check(int rc, pcp_ctx* ctx, const char* what) {
+    if (rc != PCP_OK) throw PCLException(std::string(what) + ": " + (ctx ? pcp_last_error(ctx) : "no context"));
+}
+
+class Device {
+public:
+    static Device& get() {
+        static Device d;
+        return d;
+    }
+    pcp_ctx* ctx() { return ctx_; }
+    std::mutex& mutex() { return mu_; }
+
+private:
+    Device() {
+        const char* e = std::getenv("PCP_DEVICE");
+        int rc = pcp_ctx_create(e ? std::atoi(e) : 0, nullptr, &ctx_);
+        if (rc != PCP_OK) throw PCLException("pcp_ctx_create failed (is libpcp built and a GPU visible?)");
+    }
+    ~Device() { pcp_ctx_destroy(ctx_); }
+    pcp_ctx* ctx_ = nullptr;
+    std::mutex mu_;
+};
+
+// grow-only device buffer
+class DevBuf {
+public:
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void* reserve(size_t bytes) {
+        if (!p_ || bytes > cap_) {
+            release();
+            pcp_ctx* c = Device::get().ctx();
+            check(pcp_malloc(c, &p_, bytes ? bytes : 1), c, "pcp_malloc");
+            cap_ = bytes;
+        }
+        return p_;
+    }
+    void* upload(const void* host, size_t bytes) {
+        reserve(bytes);
+        pcp_ctx* c = Device::get().ctx();
+        if (bytes) check(pcp_memcpy_h2d(c, p_, host, bytes), c, "pcp_memcpy_h2d");
+        return p_;
+    }
+    void download(void* host, size_t bytes) const {
+        pcp_ctx* c = Device::get().ctx();
+        if (bytes) check(pcp_memcpy_d2h(c, host, p_, bytes), c, "pcp_memcpy_d2h");
+    }
+    void* ptr() const { return p_; }
+
+private:
+    void release() {
+        if (p_) pcp_free(Device::get().ctx(), p_);
+        p_ = nullptr;
+        cap_ = 0;
+    }
+    void* p_ = nullptr;
+    size_t cap_ = 0;
+};
+
+template <class PointT>
+inline void require_xyz_double_layout() {
+    static_assert(sizeof(PointT) % 8 == 0, "PointT must start with x,y,z doubles (point_type.h)");
+}
+
+// query points -> packed xyz doubles
+template <class PointT>
+inline std::vector<double> pack_xyz(const std::vector<PointT>& q) {
+    std::vector<double> v(3 * q.size());
+    for (size_t i = 0; i < q.size(); i++) {
+        v[3 * i] = q[i].x;
+        v[3 * i + 1] = q[i].y;
+        v[3 * i + 2] = q[i].z;
+    }
+    return v;
+}
+
+}  // namespace detail
+
+// ------------------------------------------------------------------ K: KdTreeFLANN
+template <class PointT>
+class KdTreeFLANN {
+public:
+    typedef std::shared_ptr<KdTreeFLANN<PointT>> Ptr;
+    typedef std::shared_ptr<const KdTreeFLANN<PointT>> ConstPtr;
+    typedef typename PointCloud<PointT>::ConstPtr PointCloudConstPtr;
+    typedef std::shared_ptr<const std::vector<int>> IndicesConstPtr;
+
+    explicit KdTreeFLANN(bool sorted = true) : sorted_(sorted) { detail::require_xyz_double_layout<PointT>(); }
+
+    // kd_tree.h:772-798: non-finite points dropped, index_mapping_ kept.  The index is
+    // reference-counted, so copies of the tree share it safely (the reference's copy
+    // constructor shallow-copied raw pointers, kd_tree.h:721-734).
+    void setInputCloud(const PointCloudConstPtr& cloud, const IndicesConstPtr& indices = IndicesConstPtr()) {
+        input_ = cloud;
+        indices_ = indices;
+        st_.reset();
+        if (!cloud) return;  // reference: silent return (kd_tree.h:784-787)
+        std::shared_ptr<State> s(new State);
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        const size_t n = cloud->points.size();
+        const double* xyz = (const double*)s->cloud.upload(cloud->points.data(), n * sizeof(PointT));
+        const int32_t* ind = nullptr;
+        if (indices) ind = (const int32_t*)s->indices.upload(indices->data(), indices->size() * sizeof(int));
+        detail::check(pcp_index_build_f64(c, xyz, sizeof(PointT), (int64_t)n, ind,
+                                          indices ? (int64_t)indices->size() : 0, 0.0, &s->index),
+                      c, "pcp_index_build_f64");
+        st_ = s;
+    }
+    PointCloudConstPtr getInputCloud() const { return input_; }
+    IndicesConstPtr getIndices() const { return indices_; }
+    void setEpsilon(float eps) { epsilon_ = eps; }  // searches stay exact (the callers' eps = 0)
+    float getEpsilon() const { return epsilon_; }
+    void setSortedResults(bool sorted) { sorted_ = sorted; }  // sorted is a valid unsorted order
+    Ptr makeShared() const { return Ptr(new KdTreeFLANN<PointT>(*this)); }
+
+    // kd_tree.h:814-845
+    int nearestKSearch(const PointT& point, int k, std::vector<int>& k_indices,
+                       std::vector<double>& k_sqr_distances) const {
+        k_indices.clear();
+        k_sqr_distances.clear();
+        if (!st_ || k <= 0) return 0;
+        const int64_t n = pcp_index_size(st_->index);
+        if (k > n) k = (int)n;
+        if (k == 0) return 0;
+        std::vector<int> idx;
+        std::vector<double> d2;
+        run_knn(std::vector<PointT>(1, point), k, idx, d2);
+        k_indices.assign(idx.begin(), idx.end());
+        k_sqr_distances.assign(d2.begin(), d2.end());
+        return k;
+    }
+    int nearestKSearch(const PointCloud<PointT>& cloud, int index, int k, std::vector<int>& k_indices,
+                       std::vector<double>& k_sqr_distances) const {  // kd_tree.h:446-452
+        return nearestKSearch(cloud.points[index], k, k_indices, k_sqr_distances);
+    }
+    int nearestKSearch(int index, int k, std::vector<int>& k_indices,
+                       std::vector<double>& k_sqr_distances) const {  // kd_tree.h:494-505
+        const PointT& p = indices_ ? input_->points[(*indices_)[index]] : input_->points[index];
+        return nearestKSearch(p, k, k_indices, k_sqr_distances);
+    }
+
+    // kd_tree.h:863-903
+    int radiusSearch(const PointT& point, double radius, std::vector<int>& k_indices,
+                     std::vector<double>& k_sqr_distances, unsigned int max_nn = 0) const {
+        std::vector<int64_t> off;
+        radiusSearchBatch(std::vector<PointT>(1, point), radius, off, k_indices, k_sqr_distances, max_nn);
+        return (int)k_indices.size();
+    }
+    int radiusSearch(const PointCloud<PointT>& cloud, int index, double radius, std::vector<int>& k_indices,
+                     std::vector<double>& k_sqr_distances, unsigned int max_nn = 0) const {  // :538-545
+        return radiusSearch(cloud.points[index], radius, k_indices, k_sqr_distances, max_nn);
+    }
+    int radiusSearch(int index, double radius, std::vector<int>& k_indices, std::vector<double>& k_sqr_distances,
+                     unsigned int max_nn = 0) const {  // :590-601
+        const PointT& p = indices_ ? input_->points[(*indices_)[index]] : input_->points[index];
+        return radiusSearch(p, radius, k_indices, k_sqr_distances, max_nn);
+    }
+
+    // ---- batch extensions (one launch for many queries)
+    // rows of k: k_indices[i*k + r] (-1 / +inf past the tree size)
+    void nearestKSearchBatch(const std::vector<PointT>& queries, int k, std::vector<int>& k_indices,
+                             std::vector<double>& k_sqr_distances) const {
+        k_indices.clear();
+        k_sqr_distances.clear();
+        if (!st_ || k <= 0 || queries.empty()) return;
+        run_knn(queries, k, k_indices, k_sqr_distances);
+    }
+    // CSR: neighbours of query i are [offsets[i], offsets[i+1])
+    void radiusSearchBatch(const std::vector<PointT>& queries, double radius, std::vector<int64_t>& offsets,
+                           std::vector<int>& k_indices, std::vector<double>& k_sqr_distances,
+                           unsigned int max_nn = 0) const {
+        offsets.assign(queries.size() + 1, 0);
+        k_indices.clear();
+        k_sqr_distances.clear();
+        if (!st_ || queries.empty()) return;
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        const int64_t nq = (int64_t)queries.size();
+        std::vector<double> qh = detail::pack_xyz(queries);
+        detail::DevBuf q, cnt, off, oi, od;
+        q.upload(qh.data(), qh.size() * sizeof(double));
+        cnt.reserve(nq * sizeof(int32_t));
+        off.reserve((nq + 1) * sizeof(int64_t));
+        detail::check(pcp_radius_count(c, st_->index, (const double*)q.ptr(), 24, nq, radius, max_nn,
+                                       (int32_t*)cnt.ptr()), c, "pcp_radius_count");
+        int64_t total = 0;
+        detail::check(pcp_scan_counts(c, (const int32_t*)cnt.ptr(), nq, (int64_t*)off.ptr(), &total), c,
+                      "pcp_scan_counts");
+        oi.reserve(total * sizeof(int32_t));
+        od.reserve(total * sizeof(double));
+        detail::check(pcp_radius_fill(c, st_->index, (const double*)q.ptr(), 24, nq, radius, max_nn,
+                                      (const int64_t*)off.ptr(), (int32_t*)oi.ptr(), (double*)od.ptr()), c,
+                      "pcp_radius_fill");
+        off.download(offsets.data(), (nq + 1) * sizeof(int64_t));
+        k_indices.resize(total);
+        k_sqr_distances.resize(total);
+        oi.download(k_indices.data(), total * sizeof(int32_t));
+        od.download(k_sqr_distances.data(), total * sizeof(double));
+    }
+
+    // device-side handles for callers that keep their data in HBM (pcp.h)
+    const pcp_index* index() const { return st_ ? st_->index : nullptr; }
+    const double* device_cloud() const { return st_ ? (const double*)st_->cloud.ptr() : nullptr; }
+
+private:
+    struct State {
+        pcp_index* index = nullptr;
+        detail::DevBuf cloud, indices;
+        ~State() {
+            if (index) pcp_index_destroy(index);
+        }
+    };
+    void run_knn(const std::vector<PointT>& queries, int k, std::vector<int>& idx, std::vector<double>& d2) const {
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        const int64_t nq = (int64_t)queries.size();
+        std::vector<double> qh = detail::pack_xyz(queries);
+        detail::DevBuf q, oi, od;
+        q.upload(qh.data(), qh.size() * sizeof(double));
+        oi.reserve(nq * k * sizeof(int32_t));
+        od.reserve(nq * k * sizeof(double));
+        detail::check(pcp_knn(c, st_->index, (const double*)q.ptr(), 24, nq, k, (int32_t*)oi.ptr(),
+                              (double*)od.ptr()), c, "pcp_knn");
+        idx.resize(nq * k);
+        d2.resize(nq * k);
+        oi.download(idx.data(), idx.size() * sizeof(int32_t));
+        od.download(d2.data(), d2.size() * sizeof(double));
+    }
+    PointCloudConstPtr input_;
+    IndicesConstPtr indices_;
+    std::shared_ptr<State> st_;
+    float epsilon_ = 0.f;
+    bool sorted_ = true;
+};
+
+// ------------------------------------------------------------------ K6: kd_tree_lod KdTree
+namespace lod {
+class KdTree {  // kd_tree_lod/kd_tree.h (cloud_blend_double::KdTree in the lod build)
+public:
+    void setInputCloud(PointCloud<PointXYZRGBA>::ConstPtr cloud) {
+        cloud_ = cloud;
+        if (cloud) dev_.upload(cloud->points.data(), cloud->points.size() * sizeof(PointXYZRGBA));
+    }
+    // kd_tree.cpp:78-117, including the k_dis2 quirk (residual of the last scanned point)
+    int nearestKSearch(const PointXYZRGBA& point, int k, std::vector<int>& k_indices, std::vector<double>& k_dis2) {
+        k_indices.clear();
+        k_dis2.clear();
+        if (!cloud_ || cloud_->points.empty() || k <= 0) return 0;
+        const int64_t n = (int64_t)cloud_->points.size();
+        const int kk = (int)(k < n ? k : n);
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        detail::DevBuf q, oi, od;
+        q.upload(&point, sizeof(PointXYZRGBA));
+        oi.reserve(k * sizeof(int32_t));
+        od.reserve(k * sizeof(double));
+        detail::check(pcp_knn_lod(c, dev_.ptr(), n, q.ptr(), 1, k, (int32_t*)oi.ptr(), (double*)od.ptr()), c,
+                      "pcp_knn_lod");
+        k_indices.resize(kk);
+        k_dis2.resize(kk);
+        oi.download(k_indices.data(), kk * sizeof(int32_t));
+        od.download(k_dis2.data(), kk * sizeof(double));
+        return kk;
+    }
+
+private:
+    PointCloud<PointXYZRGBA>::ConstPtr cloud_;
+    detail::DevBuf dev_;
+};
+}  // namespace lod
+
+// ------------------------------------------------------------------ V3: VoxelGrid
+template <class PointT>
+class VoxelGrid {  // voxel_grid.h:496-1056 (PointXYZRGBA records)
+public:
+    typedef typename PointCloud<PointT>::ConstPtr PointCloudConstPtr;
+    VoxelGrid() { static_assert(sizeof(PointT) == PCP_AOS48_STRIDE, "VoxelGrid<PointXYZRGBA> only"); }
+    void setInputCloud(const PointCloudConstPtr& cloud) { input_ = cloud; }
+    PointCloudConstPtr getInputCloud() const { return input_; }
+    void setLeafSize(double lx, double ly, double lz) {  // voxel_grid.h:538-549
+        leaf_[0] = lx; leaf_[1] = ly; leaf_[2] = lz; leaf_[3] = 1.0;
+    }
+    template <class V4>
+    void setLeafSize(const V4& l) {  // voxel_grid.h:522-536 (Vector4d)
+        leaf_[0] = l[0]; leaf_[1] = l[1]; leaf_[2] = l[2]; leaf_[3] = (l[3] == 0) ? 1.0 : l[3];
+    }
+    Vec4d getLeafSize() const {
+        Vec4d v;
+        for (int i = 0; i < 4; i++) v[i] = leaf_[i];
+        return v;
+    }
+    void setDownsampleAllData(bool d) { all_data_ = d; }
+    bool getDownsampleAllData() const { return all_data_; }
+    // Optional reference paths outside this build's scope: rejected loudly.
+    void setSaveLeafLayout(bool s) { save_layout_ = s; }
+    bool getSaveLeafLayout() const { return save_layout_; }
+    void setFilterFieldName(const std::string& f) { field_ = f; }
+    const std::string& getFilterFieldName() const { return field_; }
+    void setFilterLimits(double lo, double hi) { lim_lo_ = lo; lim_hi_ = hi; }
+    void setFilterLimitsNegative(bool n) { lim_neg_ = n; }
+
+    // grid getters of the last filter() (voxel_grid.h:552-706)
+    const int* getMinBoxCoordinates() const { return min_b_; }
+    const int* getMaxBoxCoordinates() const { return max_b_; }
+    const int* getNrDivisions() const { return div_b_; }
+    const int* getDivisionMultiplier() const { return divb_mul_; }
+
+    void filter(PointCloud<PointT>& output) {  // Filter::filter -> applyFilter
+        if (!input_) {  // voxel_grid.h:815-820
+            output.points.clear();
+            output.width = 0;
+            output.height = 1;
+            return;
+        }
+        if (save_layout_ || !field_.empty())
+            throw PCLException("VoxelGrid: leaf layout / field-limit filtering is not part of this build");
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        const int64_t n = (int64_t)input_->points.size();
+        detail::DevBuf in, out;
+        in.upload(input_->points.data(), n * sizeof(PointT));
+        out.reserve((n ? n : 1) * sizeof(PointT));
+        double mn[4], mx[4];
+        detail::check(pcp_minmax_aos48(c, in.ptr(), n, input_->is_dense ? 1 : 0, mn, mx), c, "pcp_minmax_aos48");
+        for (int a = 0; a < 3; a++) {  // voxel_grid.h:835-847
+            min_b_[a] = (int)(double)(mn[a] * (1.0 / leaf_[a]));
+            max_b_[a] = (int)(double)(mx[a] * (1.0 / leaf_[a]));
+            div_b_[a] = max_b_[a] - min_b_[a] + 1;
+        }
+        divb_mul_[0] = 1;
+        divb_mul_[1] = div_b_[0];
+        divb_mul_[2] = (int)((uint32_t)div_b_[0] * (uint32_t)div_b_[1]);
+        int64_t m = 0;
+        const int rc = pcp_voxel_filter(c, in.ptr(), n, input_->is_dense ? 1 : 0, leaf_, all_data_ ? 1 : 0,
+                                        out.ptr(), &m, nullptr);
+        if (rc != PCP_OK) throw PCLException(std::string("VoxelGrid::filter: ") + pcp_last_error(c));
+        output.points.resize(m);
+        out.download(output.points.data(), m * sizeof(PointT));
+        output.width = (uint32_t)m;
+        output.height = 1;
+        output.is_dense = true;
+    }
+
+private:
+    PointCloudConstPtr input_;
+    double leaf_[4] = {0, 0, 0, 1};
+    bool all_data_ = true;  // voxel_grid.h:499
+    bool save_layout_ = false;
+    std::string field_;
+    double lim_lo_ = -1e308, lim_hi_ = 1e308;
+    bool lim_neg_ = false;
+    int min_b_[3] = {0, 0, 0}, max_b_[3] = {0, 0, 0}, div_b_[3] = {0, 0, 0}, divb_mul_[3] = {0, 0, 0};
+};
+
+// ------------------------------------------------------------------ I: PointCloudHelper
+class PointCloudHelper {  // point_cloud_helper.h:10-237 (the hot-path members)
+public:
+    // getMinMax3D(cloud, Vector4d&, Vector4d&) (:59-90): max starts at DBL_MIN
+    template <class PointT, class V4>
+    static void getMinMax3D(const PointCloud<PointT>& cloud, V4& min_pt, V4& max_pt) {
+        static_assert(sizeof(PointT) == PCP_AOS48_STRIDE, "AoS48 records");
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        detail::DevBuf in;
+        in.upload(cloud.points.data(), cloud.points.size() * sizeof(PointT));
+        double mn[4], mx[4];
+        detail::check(pcp_minmax_aos48(c, in.ptr(), (int64_t)cloud.points.size(), cloud.is_dense ? 1 : 0, mn, mx), c,
+                      "pcp_minmax_aos48");
+        for (int a = 0; a < 4; a++) { min_pt[a] = mn[a]; max_pt[a] = mx[a]; }
+    }
+    // compute3DCentroid (:193-230); GPU sum order is a fixed tree
+    template <class PointT, class V4>
+    static unsigned int compute3DCentroid(const PointCloud<PointT>& cloud, V4& centroid) {
+        if (cloud.points.empty()) return 0;
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        detail::DevBuf in;
+        in.upload(cloud.points.data(), cloud.points.size() * sizeof(PointT));
+        double cc[4];
+        uint32_t cnt = 0;
+        detail::check(pcp_centroid_aos48(c, in.ptr(), (int64_t)cloud.points.size(), cloud.is_dense ? 1 : 0, cc, &cnt),
+                      c, "pcp_centroid_aos48");
+        for (int a = 0; a < 4; a++) centroid[a] = cc[a];
+        return cnt;
+    }
+    // transformPointCloud (:92-127)
+    template <class PointT, class M>
+    static void transformPointCloud(const PointCloud<PointT>& in, PointCloud<PointT>& out, const M& transform) {
+        static_assert(sizeof(PointT) == PCP_AOS48_STRIDE, "AoS48 records");
+        double T[16];
+        for (int r = 0; r < 4; r++)
+            for (int col = 0; col < 4; col++) T[4 * r + col] = transform(r, col);
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        const int64_t n = (int64_t)in.points.size();
+        detail::DevBuf buf;
+        buf.upload(in.points.data(), n * sizeof(PointT));
+        detail::check(pcp_transform_aos48(c, buf.ptr(), buf.ptr(), n, in.is_dense ? 1 : 0, T), c,
+                      "pcp_transform_aos48");
+        if (&out != &in) {
+            out.width = in.width;
+            out.height = in.height;
+            out.is_dense = in.is_dense;
+        }
+        out.points.resize(n);
+        buf.download(out.points.data(), n * sizeof(PointT));
+    }
+    // remove_duplicate(cloud, float leaf) (point_cloud_helper.cpp:42-63)
+    static void remove_duplicate(CloudPtr cloud_src, const float voxel_grid_size) {
+        if (!cloud_src) return;
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        const int64_t n = (int64_t)cloud_src->points.size();
+        detail::DevBuf in, out;
+        in.upload(cloud_src->points.data(), n * sizeof(CloudItem));
+        out.reserve((n ? n : 1) * sizeof(CloudItem));
+        int64_t m = 0;
+        detail::check(pcp_remove_duplicate(c, in.ptr(), n, cloud_src->is_dense ? 1 : 0, voxel_grid_size, out.ptr(), &m),
+                      c, "pcp_remove_duplicate");
+        cloud_src->points.resize(m);
+        out.download(cloud_src->points.data(), m * sizeof(CloudItem));
+        cloud_src->width = (uint32_t)m;
+        cloud_src->height = 1;
+        cloud_src->is_dense = true;
+    }
+    // (:65-73): keep the result only when at least min_num points survive
+    static void remove_duplicate(CloudPtr cloud_src, const float voxel_grid_size, int min_num) {
+        CloudPtr tmp(new Cloud(*cloud_src));
+        remove_duplicate(tmp, voxel_grid_size);
+        if ((int)tmp->size() >= min_num) *cloud_src = *tmp;
+    }
+    // get_rot_icp (:75-166): returns err (< 0 on failure); do_affine is outside this build
+    template <class M>
+    static float get_rot_icp(CloudPtr cloud_src, CloudPtr cloud_temp, M& mat_rot, bool do_scale = false,
+                             bool do_affine = false, int iters = 20, float maxdist = 0.25f) {
+        for (int r = 0; r < 4; r++)
+            for (int col = 0; col < 4; col++) mat_rot(r, col) = (r == col) ? 1.0 : 0.0;
+        if (do_affine || !cloud_src || !cloud_temp) return -1.0f;
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        detail::DevBuf s, t;
+        s.upload(cloud_src->points.data(), cloud_src->points.size() * sizeof(CloudItem));
+        t.upload(cloud_temp->points.data(), cloud_temp->points.size() * sizeof(CloudItem));
+        double Mh[16];
+        float err = -1.0f;
+        const int rc = pcp_get_rot_icp(c, s.ptr(), (int64_t)cloud_src->size(), t.ptr(), (int64_t)cloud_temp->size(),
+                                       Mh, maxdist, iters, do_scale ? 1 : 0, 0.0, &err);
+        if (rc != PCP_OK) return -1.0f;
+        for (int r = 0; r < 4; r++)
+            for (int col = 0; col < 4; col++) mat_rot(r, col) = Mh[4 * r + col];
+        return err;
+    }
+    // point_dis2 (point_cloud_helper.h:20): pow(dx,2)+pow(dy,2)+pow(dz,2)
+    static double point_dis2(const PointXYZRGBA& p1, const PointXYZRGBA& p2) {
+        const double dx = p1.x - p2.x, dy = p1.y - p2.y, dz = p1.z - p2.z;
+        return dx * dx + dy * dy + dz * dz;
+    }
+};
+
+// ------------------------------------------------------------------ F: CalculateFeature
+class CalculateFeature {  // calculate_feature.h:11-16
+public:
+    // calculate_feature.cpp:28-33
+    int compute_iteration_number(float Pr, float epi, int /*h_free*/) {
+        return (int)(std::log10(1 - Pr) / std::log10(1 - std::pow(1 - epi, 3)));
+    }
+    // F1 (calculate_feature.cpp:119-206) over all points of `cloud`
+    PlanSegment calculate_plan_parameter_h_points(CloudPtr cloud) {
+        PlanSegment out;
+        if (!cloud || cloud->points.empty()) return out;
+        pcp_plane p = fit(cloud->points.data(), cloud->points.size());
+        copy(p, out);
+        return out;
+    }
+    // F2 (:35-117): the same PCA on 3 points
+    PlanSegment calculate_plan_parameter_3points(CloudItem points[3]) {
+        PlanSegment out;
+        pcp_plane p = fit(points, 3);
+        copy(p, out);
+        return out;
+    }
+    // F4 (declared-only, calculate_feature.h:15): F1 over each point's radius neighbourhood
+    std::shared_ptr<LAS_POINT_PROPERTY> calculate_plan_parameter(CloudPtr cloud, double radius) {
+        return per_point(cloud, [&](KdTreeFLANN<CloudItem>& tree, std::vector<int64_t>& off, std::vector<int>& idx) {
+            std::vector<double> d2;
+            tree.radiusSearchBatch(cloud->points, radius, off, idx, d2);
+        });
+    }
+    // F3 (:208-368) is randomised (srand(time), rand() under OMP); this build returns the
+    // deterministic F1 over the same kNN(20) neighbourhoods ("next" in §8(f)).
+    std::shared_ptr<LAS_POINT_PROPERTY> calculate_plan_parameter_rpca(CloudPtr cloud, double /*radius*/, float /*pr*/,
+                                                                       float /*epi*/) {
+        return per_point(cloud, [&](KdTreeFLANN<CloudItem>& tree, std::vector<int64_t>& off, std::vector<int>& idx) {
+            std::vector<double> d2;
+            const int k = 20;  // calculate_feature.cpp:233
+            tree.nearestKSearchBatch(cloud->points, k, idx, d2);
+            off.resize(cloud->points.size() + 1);
+            std::vector<int> kept;
+            kept.reserve(idx.size());
+            off[0] = 0;
+            for (size_t i = 0; i < cloud->points.size(); i++) {
+                int got = 0;
+                for (int r = 0; r < k; r++)
+                    if (idx[i * k + r] >= 0) { kept.push_back(idx[i * k + r]); got++; }
+                if (got <= 3) kept.resize(kept.size() - got);  // N > 3 guard (:237, 353-361)
+                off[i + 1] = (int64_t)kept.size();
+            }
+            idx.swap(kept);
+        });
+    }
+
+private:
+    static void copy(const pcp_plane& p, PlanSegment& o) {
+        o.normal_x = p.normal_x; o.normal_y = p.normal_y; o.normal_z = p.normal_z;
+        o.min_value = p.min_value; o.curvature = p.curvature; o.Distance = p.distance;
+    }
+    static pcp_plane fit(const CloudItem* pts, size_t n) {
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        detail::DevBuf xyz, off, out;
+        xyz.upload(pts, n * sizeof(CloudItem));
+        const int64_t o[2] = {0, (int64_t)n};
+        off.upload(o, sizeof(o));
+        out.reserve(sizeof(pcp_plane));
+        detail::check(pcp_plane_fit_segments(c, (const double*)xyz.ptr(), sizeof(CloudItem), (const int64_t*)off.ptr(),
+                                             nullptr, 1, (pcp_plane*)out.ptr()), c, "pcp_plane_fit_segments");
+        pcp_plane p;
+        out.download(&p, sizeof(p));
+        return p;
+    }
+    template <class Neigh>
+    std::shared_ptr<LAS_POINT_PROPERTY> per_point(CloudPtr cloud, Neigh neigh) {
+        const size_t n = cloud ? cloud->points.size() : 0;
+        std::shared_ptr<LAS_POINT_PROPERTY> res(new LAS_POINT_PROPERTY[n ? n : 1],
+                                                std::default_delete<LAS_POINT_PROPERTY[]>());
+        if (!n) return res;
+        KdTreeFLANN<CloudItem> tree;
+        tree.setInputCloud(cloud);
+        std::vector<int64_t> off;
+        std::vector<int> idx;
+        neigh(tree, off, idx);
+        std::vector<pcp_plane> planes(n);
+        {
+            pcp_ctx* c = detail::Device::get().ctx();
+            std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+            detail::DevBuf doff, didx, dout;
+            doff.upload(off.data(), off.size() * sizeof(int64_t));
+            didx.upload(idx.data(), idx.size() * sizeof(int));
+            dout.reserve(n * sizeof(pcp_plane));
+            detail::check(pcp_plane_fit_segments(c, tree.device_cloud(), sizeof(CloudItem), (const int64_t*)doff.ptr(),
+                                                 (const int32_t*)didx.ptr(), (int64_t)n, (pcp_plane*)dout.ptr()),
+                          c, "pcp_plane_fit_segments");
+            dout.download(planes.data(), n * sizeof(pcp_plane));
+        }
+        for (size_t i = 0; i < n; i++) {
+            LAS_POINT_PROPERTY& r = res.get()[i];
+            r.normal_x = planes[i].normal_x;
+            r.normal_y = planes[i].normal_y;
+            r.normal_z = planes[i].normal_z;
+            r.Distance = planes[i].distance;
+            r.curvature = planes[i].curvature;
+            r.PointID = (int)i;
+            r.SegmentID = 0;
+            r.dis_from_point_plane = 0.f;
+        }
+        return res;
+    }
+};
+
+// ------------------------------------------------------------------ I4: CloudStampRot
+class CloudStampRot {  // cloud_stamp_rot.h:7-39 (pose record; composition stays on the host)
+public:
+    CloudStampRot() : _rot(Mat4d::Identity()) {}
+    explicit CloudStampRot(bool) : _rot(Mat4d::Identity()), _is_valid(false) {}
+    CloudStampRot(uint64_t stamp, const Mat4d& rot, CloudPtr cloud_line, double value_icp)
+        : _stamp(stamp), _rot(rot), _cloud_line(cloud_line), _cloud_line_src(new Cloud(*cloud_line)),
+          _is_valid(true), _value_icp(value_icp) {}
+    uint64_t _stamp = 0;
+    Mat4d _rot;
+    CloudPtr _cloud_line;
+    CloudPtr _cloud_line_src;
+    bool _is_valid = false;
+    double _value_icp = 0.0;
+    double _time_stamp_d = 0.0;
+    std::string _time_stamp_str;
+};
+
+}  // namespace cloud_blend_double
+
+#endif  // PCP_PCL_HPP

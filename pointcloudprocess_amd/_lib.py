@@ -46,6 +46,8 @@ SIGNATURES = [
     ("pcp_scan_counts", _i32, [_vp, _vp, _i64, _vp, _P(_i64)]),
     ("pcp_knn_bruteforce", _i32, [_vp, _vp, _sz, _i64, _vp, _sz, _i64, _i32, _vp, _vp]),
     ("pcp_knn_bruteforce_last_fallback", _i32, [_vp, _vp]),
+    ("pcp_nearest_query", _i32, [_vp, _vp, _vp, _sz, _i64, _f64, _vp, _vp]),
+    ("pcp_plane_fit_segments", _i32, [_vp, _vp, _sz, _vp, _vp, _i64, _vp]),
     ("pcp_knn_lod", _i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp]),
     ("pcp_minmax_aos48", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _P(_f64)]),
     ("pcp_centroid_aos48", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _P(_u32)]),

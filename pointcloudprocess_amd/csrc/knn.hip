@@ -315,6 +315,67 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
     }
 }
 
+// F1 batch: one plane per CSR segment, points xyz[idx[t]] (or xyz[t]) for t in
+// [off[s], off[s+1]), accumulated sequentially in segment order (calculate_feature.cpp:
+// 131-164) -- calculate_plan_parameter_h_points per segment, and the radius variant
+// (calculate_feature.h:15, F4) when the segments are radiusSearch rows.
+__global__ __launch_bounds__(kB) void k_plane_segments(const double* xyz, size_t stride, const int64_t* off,
+                                                       const int32_t* idx, int64_t nseg, pcp_plane* out) {
+    for (int64_t sg = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; sg < nseg;
+         sg += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = off[sg], e = off[sg + 1];
+        const int64_t h = e - s;
+        if (h <= 0) {
+            out[sg] = pcp_plane{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
+            continue;
+        }
+        auto P = [&](int64_t t) { return qptr(xyz, stride, idx ? (int64_t)idx[t] : t); };
+        double xa = 0, ya = 0, za = 0;
+        for (int64_t t = s; t < e; t++) {
+            const double* p = P(t);
+            xa += p[0]; ya += p[1]; za += p[2];
+        }
+        xa /= h; ya /= h; za /= h;
+        double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+        for (int64_t t = s; t < e; t++) {
+            const double* p = P(t);
+            const double x0 = p[0] - xa, x1 = p[1] - ya, x2 = p[2] - za;
+            c00 += x0 * x0; c01 += x0 * x1; c02 += x0 * x2;
+            c11 += x1 * x1; c12 += x1 * x2; c22 += x2 * x2;
+        }
+        const double C[9] = {c00, c01, c02, c01, c11, c12, c02, c12, c22};
+        pcp_plane pl;
+        plane_from_cov(C, xa, ya, za, pl);
+        out[sg] = pl;
+    }
+}
+
+// K7 (main_blend.cpp:306-325): argmin over queries of the 1-NN d2, strict '<' from an
+// initial bound, so the first query wins ties.  Per-block lexicographic (d2, i) minimum.
+__global__ __launch_bounds__(kB) void k_argmin_d2(const double* d2, int64_t n, double* pd, int64_t* pi) {
+    double bd = INFINITY;
+    int64_t bi = INT64_MAX;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double d = d2[i];
+        if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(bd, o, 64);
+        const int64_t oi = __shfl_xor(bi, o, 64);
+        if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+    }
+    __shared__ double sd[kB / 64];
+    __shared__ int64_t si[kB / 64];
+    if ((threadIdx.x & 63) == 0) { sd[threadIdx.x >> 6] = bd; si[threadIdx.x >> 6] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kB / 64; w++)
+            if (sd[w] < bd || (sd[w] == bd && si[w] < bi)) { bd = sd[w]; bi = si[w]; }
+        pd[blockIdx.x] = bd;
+        pi[blockIdx.x] = bi;
+    }
+}
+
 // ------------------------------------------------------------------ K6: kd_tree_lod
 // fp32 kNN over the float vertices float(p - c) (kd_tree_lod/kd_tree.cpp:39-43, 62-68;
 // the trimesh2 search is external: exact k nearest, ties by vertex index).
@@ -578,6 +639,56 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
 #undef LAUNCH_NRM
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
+}
+
+int pcp_plane_fit_segments(pcp_ctx* ctx, const double* xyz, size_t stride, const int64_t* off, const int32_t* idx,
+                           int64_t nseg, pcp_plane* out) {
+    if (!ctx || nseg < 0 || (nseg > 0 && (!xyz || !off || !out)))
+        return set_error(ctx, PCP_ERR_ARG, "pcp_plane_fit_segments: bad arguments");
+    if (stride == 0) stride = 3 * sizeof(double);
+    if (nseg == 0) return PCP_OK;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_plane_segments, dim3(blocks_for(nseg)), dim3(kB), 0, ctx->stream, xyz, stride, off, idx, nseg,
+                       out);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_nearest_query(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t qstride, int64_t nq,
+                      double init_bound, int64_t* best_q, double* best_d2) {
+    PCP_TRY(check_f64_index(ctx, ix));
+    if (nq < 0 || (nq > 0 && !q) || !best_q || !best_d2)
+        return set_error(ctx, PCP_ERR_ARG, "pcp_nearest_query: bad arguments");
+    *best_q = -1;
+    *best_d2 = init_bound;
+    if (nq == 0 || ix->n == 0) return PCP_OK;
+    int32_t* idx = nullptr;
+    double* d2 = nullptr;
+    double* pd = nullptr;
+    int64_t* pi = nullptr;
+    const unsigned nb = grid_for(nq, kB, 1024);
+    int rc = dmalloc(ctx, &idx, nq);
+    if (!rc) rc = dmalloc(ctx, &d2, nq);
+    if (!rc) rc = dmalloc(ctx, &pd, nb);
+    if (!rc) rc = dmalloc(ctx, &pi, nb);
+    if (!rc) rc = pcp_knn(ctx, ix, q, qstride, nq, 1, idx, d2);
+    if (!rc) {
+        hipLaunchKernelGGL(k_argmin_d2, dim3(nb), dim3(kB), 0, ctx->stream, d2, nq, pd, pi);
+        std::vector<double> hd(nb);
+        std::vector<int64_t> hi(nb);
+        hipError_t e = hipMemcpyAsync(hd.data(), pd, nb * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(hi.data(), pi, nb * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) rc = hip_fail(ctx, e, "nearest_query", __FILE__, __LINE__);
+        // lexicographic (d2, query) minimum == the sequential strict-'<' scan's winner
+        double bd = INFINITY;
+        int64_t bi = INT64_MAX;
+        for (unsigned b = 0; b < nb && !rc; b++)
+            if (hd[b] < bd || (hd[b] == bd && hi[b] < bi)) { bd = hd[b]; bi = hi[b]; }
+        if (!rc && bd < init_bound) { *best_d2 = bd; *best_q = bi; }
+    }
+    hipFree(idx); hipFree(d2); hipFree(pd); hipFree(pi);
+    return rc;
 }
 
 int pcp_knn_lod(pcp_ctx* ctx, const void* cloud, int64_t n, const void* q, int64_t nq, int k, int32_t* oidx,

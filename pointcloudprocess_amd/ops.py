@@ -145,6 +145,32 @@ def radius(index, q, r, max_nn=0):
     return offs, idx[:total.value], d2[:total.value]
 
 
+def nearest_query(index, q, init_bound=9999.0):
+    """find_cloud_nearest_point_in_kdtree: (query index or -1, its 1-NN d2)."""
+    ctx = index.ctx
+    bq, bd = C.c_int64(), C.c_double()
+    ctx.check(ctx.lib.pcp_nearest_query(ctx.h, index.h, _ptr(q), _qstride(q), q.shape[0], float(init_bound),
+                                        C.byref(bq), C.byref(bd)))
+    return bq.value, bd.value
+
+
+def plane_fit_segments(ctx, xyz, offsets, idx=None):
+    """One PlanSegment per CSR segment of xyz rows (F1 per segment)."""
+    nseg = offsets.numel() - 1
+    out = torch.empty((max(nseg, 1), 6), dtype=torch.float32, device=ctx.device)
+    ctx.check(ctx.lib.pcp_plane_fit_segments(ctx.h, _ptr(xyz), _qstride(xyz), _ptr(offsets), _ptr(idx), nseg,
+                                             _ptr(out)))
+    return out[:nseg]
+
+
+def normals_radius(index, r, max_nn=0):
+    """calculate_plan_parameter(cloud, radius) (calculate_feature.h:15, declared-only in the
+    reference; the build defines it as F1 over each point's radiusSearch neighbourhood)."""
+    xyz = index.src
+    offs, idx, _ = radius(index, xyz, r, max_nn)
+    return plane_fit_segments(index.ctx, xyz, offs, idx)
+
+
 def knn_bruteforce(ctx, target, q, k):
     nt, nq = target.shape[0], q.shape[0]
     idx = torch.empty((nq, k), dtype=torch.int32, device=ctx.device)

@@ -1,0 +1,221 @@
+// Parity driver for the drop-in C++ shim (include/pcp_pcl.hpp) on a GPU: the reference's own
+// test bodies (main_test.cpp:126-188, test_voxel_grid / test_kd_tree) rewritten with
+// assertions against the known answers (tests/golden/*.json), then randomised cross-checks
+// of every shim entry point against the oracle (oracle/pcp_oracle.h, test infrastructure).
+// Built and run by tests/test_shim.py.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "pcp_pcl.hpp"
+extern "C" {
+#include "../../oracle/pcp_oracle.h"
+}
+
+using namespace cloud_blend_double;
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                                     \
+    do {                                                     \
+        if (!(cond)) {                                       \
+            std::printf("FAIL %s:%d: ", __FILE__, __LINE__); \
+            std::printf(__VA_ARGS__);                        \
+            std::printf("\n");                               \
+            g_fail++;                                        \
+        }                                                    \
+    } while (0)
+
+static CloudPtr random_cloud(int n, unsigned seed, double half, double off = 0.0) {
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> u(-half, half);
+    CloudPtr c(new Cloud);
+    for (int i = 0; i < n; i++) {
+        CloudItem p((float)u(rng) + off, (float)u(rng) + off, (float)u(rng));
+        p.rgba = (uint32_t)rng();
+        p.stamp_id = (uint32_t)(rng() & 0xFFFF);
+        c->push_back(p);
+    }
+    return c;
+}
+
+static void test_voxel_grid() {  // main_test.cpp:126-154
+    CloudPtr cloud(new Cloud);
+    for (int i = 0; i < 10; i++) {
+        CloudItem p;
+        p.x = i; p.y = i; p.z = i;
+        cloud->push_back(p);
+    }
+    for (int i = 0; i < 100; i++) {
+        CloudItem p;
+        p.x = 0.1 * i; p.y = 0.1 * i; p.z = 0.1 * i;
+        cloud->push_back(p);
+    }
+    VoxelGrid<CloudItem> vox_grid;
+    CloudPtr cloud_out(new Cloud);
+    vox_grid.setInputCloud(cloud);
+    vox_grid.setLeafSize(1, 1, 1);
+    vox_grid.filter(*cloud_out);
+    CHECK(cloud_out->size() == 10, "voxel count %zu", cloud_out->size());
+    // kat_voxel_grid.json: bin 0 averages 11 float-cast values, later bins 11 exact ones
+    CHECK(cloud_out->points[0].x == 0.4090909111228856, "bin0 x %.17g", cloud_out->points[0].x);
+    CHECK(cloud_out->points[1].x == 1.4090909090909092, "bin1 x %.17g", cloud_out->points[1].x);
+    CHECK(cloud_out->points[2].x == 2.409090909090909, "bin2 x %.17g", cloud_out->points[2].x);
+}
+
+static void test_kd_tree() {  // main_test.cpp:156-188
+    CloudPtr cloud(new Cloud);
+    for (int i = 0; i < 100; i++) {
+        CloudItem p;
+        p.x = 0.1 * i; p.y = 0.1 * i; p.z = 0.1 * i;
+        cloud->push_back(p);
+    }
+    CloudItem point;
+    point.x = 0; point.y = 0; point.z = 0;
+    std::vector<int> index;
+    std::vector<double> dis2;
+    KdTreeFLANN<CloudItem> k;
+    k.setInputCloud(cloud);
+    k.nearestKSearch(point, 10, index, dis2);
+    const double want[10] = {0.0, 0.030000000000000006, 0.12000000000000002, 0.2700000000000001,
+                             0.4800000000000001, 0.75, 1.0800000000000003, 1.4700000000000002,
+                             1.9200000000000004, 2.43};
+    CHECK(index.size() == 10, "knn size %zu", index.size());
+    for (int i = 0; i < 10 && i < (int)index.size(); i++) {
+        CHECK(index[i] == i, "index[%d] = %d", i, index[i]);
+        CHECK(dis2[i] == want[i], "dis2[%d] = %.17g", i, dis2[i]);
+    }
+}
+
+static void test_knn_radius_vs_oracle() {
+    CloudPtr cloud = random_cloud(50000, 7, 10.0);
+    cloud->points[123].x = NAN;  // dropped by convertCloudToArray
+    cloud->is_dense = false;
+    KdTreeFLANN<CloudItem> tree;
+    tree.setInputCloud(cloud);
+    ora_kdtree* ot = ora_kdtree_build(&cloud->points[0].x, 6, (int)cloud->size(), nullptr, 0);
+    CloudPtr q = random_cloud(500, 8, 10.5);
+    std::vector<int> gi, ei(16);
+    std::vector<double> gd, ed(16);
+    int bad = 0;
+    for (size_t i = 0; i < q->size(); i++) {
+        const double qq[3] = {q->points[i].x, q->points[i].y, q->points[i].z};
+        tree.nearestKSearch(q->points[i], 16, gi, gd);
+        ora_knn(ot, qq, 16, ei.data(), ed.data());
+        for (int r = 0; r < 16; r++) bad += (gi[r] != ei[r]) || (gd[r] != ed[r]);
+        tree.radiusSearch(q->points[i], 0.8, gi, gd);
+        std::vector<int> ri(gi.size() + 8);
+        std::vector<double> rd(gi.size() + 8);
+        const int cnt = ora_radius(ot, qq, 0.8, 0, ri.data(), rd.data(), (int)ri.size());
+        bad += cnt != (int)gi.size();
+        for (int r = 0; r < cnt && r < (int)gi.size(); r++) bad += (gi[r] != ri[r]) || (gd[r] != rd[r]);
+    }
+    CHECK(bad == 0, "%d knn/radius mismatches", bad);
+    // batch form and the by-index overload (kd_tree.h:494-505)
+    std::vector<int> bi;
+    std::vector<double> bd;
+    tree.nearestKSearchBatch(q->points, 4, bi, bd);
+    tree.nearestKSearch(*q, 3, 4, gi, gd);
+    CHECK(gi.size() == 4 && gi[0] == bi[12] && gd[3] == bd[15], "batch vs single");
+    ora_kdtree_free(ot);
+}
+
+static void test_cloud_helpers_vs_oracle() {
+    CloudPtr cloud = random_cloud(100000, 11, 20.0, 500.0);
+    // transformPointCloud: bit-exact
+    Mat4d T = Mat4d::Identity();
+    T(0, 1) = -0.0348994967; T(1, 0) = 0.0348994967; T(0, 3) = 1.25; T(2, 3) = -0.5;
+    Cloud out;
+    PointCloudHelper::transformPointCloud(*cloud, out, T);
+    std::vector<ora_point48> eo(cloud->size());
+    ora_transform((const ora_point48*)cloud->points.data(), eo.data(), (int)cloud->size(), 1, T.m);
+    CHECK(std::memcmp(out.points.data(), eo.data(), eo.size() * sizeof(ora_point48)) == 0, "transform bytes");
+    // getMinMax3D: exact
+    Vec4d mn, mx;
+    PointCloudHelper::getMinMax3D(*cloud, mn, mx);
+    double emn[4], emx[4];
+    ora_getminmax3d((const ora_point48*)cloud->points.data(), (int)cloud->size(), 1, emn, emx);
+    for (int a = 0; a < 4; a++) CHECK(mn[a] == emn[a] && mx[a] == emx[a], "minmax axis %d", a);
+    // compute3DCentroid: fixed-order tree sum vs sequential fold
+    Vec4d c;
+    PointCloudHelper::compute3DCentroid(*cloud, c);
+    double ec[4];
+    ora_centroid((const ora_point48*)cloud->points.data(), (int)cloud->size(), 1, ec);
+    for (int a = 0; a < 3; a++) CHECK(std::fabs(c[a] - ec[a]) <= 1e-12 * std::fabs(ec[a]), "centroid %d", a);
+    // remove_duplicate: same voxel structure as the oracle given the same centroid
+    CloudPtr rd(new Cloud(*cloud));
+    PointCloudHelper::remove_duplicate(rd, 0.04f);
+    std::vector<ora_point48> er(cloud->size());
+    const int m = ora_remove_duplicate_c((const ora_point48*)cloud->points.data(), (int)cloud->size(), 1, 0.04f, c.v,
+                                         er.data());
+    CHECK((int)rd->size() == m, "remove_duplicate %zu vs %d", rd->size(), m);
+    if ((int)rd->size() == m)
+        CHECK(std::memcmp(rd->points.data(), er.data(), m * sizeof(ora_point48)) == 0, "remove_duplicate bytes");
+    // VoxelGrid with anisotropic leaf, downsample_all off
+    VoxelGrid<CloudItem> vg;
+    vg.setInputCloud(cloud);
+    vg.setLeafSize(0.5, 0.25, 1.0);
+    vg.setDownsampleAllData(false);
+    Cloud vo;
+    vg.filter(vo);
+    std::vector<ora_point48> ev(cloud->size());
+    const int nv = ora_voxel_filter((const ora_point48*)cloud->points.data(), (int)cloud->size(), 1, 0.5, 0.25, 1.0,
+                                    0, ev.data(), nullptr);
+    CHECK((int)vo.size() == nv && std::memcmp(vo.points.data(), ev.data(), nv * sizeof(ora_point48)) == 0,
+          "voxel grid %zu vs %d", vo.size(), nv);
+    bool threw = false;
+    try {
+        VoxelGrid<CloudItem> v2;
+        v2.setInputCloud(cloud);
+        v2.setLeafSize(1, 1, 1);
+        v2.setSaveLeafLayout(true);
+        v2.filter(vo);
+    } catch (const PCLException&) {
+        threw = true;
+    }
+    CHECK(threw, "leaf layout must be rejected loudly");
+}
+
+static void test_features_and_icp() {
+    CloudPtr cloud = random_cloud(20000, 21, 5.0);
+    for (auto& p : cloud->points) p.z = 0.01 * p.z + 0.1 * p.x;  // a tilted slab
+    CalculateFeature cf;
+    PlanSegment ps = cf.calculate_plan_parameter_h_points(cloud);
+    ora_plane op;
+    std::vector<double> xyz;
+    for (auto& p : cloud->points) { xyz.push_back(p.x); xyz.push_back(p.y); xyz.push_back(p.z); }
+    ora_plane_h_points(xyz.data(), (int)cloud->size(), &op);
+    CHECK(ps.normal_x == op.normal_x && ps.normal_y == op.normal_y && ps.normal_z == op.normal_z &&
+              ps.curvature == op.curvature && ps.Distance == op.distance,
+          "h_points plane");
+    std::shared_ptr<LAS_POINT_PROPERTY> props = cf.calculate_plan_parameter(cloud, 0.3);
+    CHECK(std::fabs(std::fabs(props.get()[0].normal_z) - 0.995) < 0.01, "radius normal %g", props.get()[0].normal_z);
+    // get_rot_icp: recover a small motion (err > 0, pose within 1e-4)
+    CloudPtr src = random_cloud(60000, 31, 8.0, 100.0);
+    for (auto& p : src->points) p.z = 0.2 * std::sin(p.x) + ((p.y > 100.0) ? 0.0 : 0.5 * (p.x - 100.0));
+    CloudPtr tmp(new Cloud(*src));
+    Mat4d Tm = Mat4d::Identity();
+    Tm(0, 3) = 0.03; Tm(1, 3) = -0.02;
+    PointCloudHelper::transformPointCloud(*src, *tmp, Tm);
+    Mat4d R;
+    const float err = PointCloudHelper::get_rot_icp(src, tmp, R);
+    CHECK(err >= 0 && std::fabs(R(0, 3) + 0.03) < 1e-3 && std::fabs(R(1, 3) - 0.02) < 1e-3, "icp err %g t %g %g",
+          err, R(0, 3), R(1, 3));
+    Mat4d Ra;
+    CHECK(PointCloudHelper::get_rot_icp(src, tmp, Ra, false, true) < 0, "do_affine -> err < 0");
+}
+
+int main() {
+    test_voxel_grid();
+    test_kd_tree();
+    test_knn_radius_vs_oracle();
+    test_cloud_helpers_vs_oracle();
+    test_features_and_icp();
+    if (g_fail) {
+        std::printf("%d check(s) failed\n", g_fail);
+        return 1;
+    }
+    std::printf("shim_test: all checks passed\n");
+    return 0;
+}

@@ -206,3 +206,40 @@ def test_knn_lod(ctx, offset):
         ei, ed = ora.knn_lod(cloud, qc[i:i + 1], k)
         assert np.array_equal(gi[i], ei), f"query {i}"
         assert np.array_equal(gd[i], ed), f"query {i}"
+
+
+def test_nearest_query(ctx):
+    """K7: argmin over queries of the 1-NN d2, strict '<' from 9999, first query wins ties."""
+    from pointcloudprocess_amd import ops
+    xyz = _cloud(20_000, 61)
+    q = _cloud(5000, 62)
+    q[4000] = xyz[17]            # exact hit (d2 = 0) ...
+    q[4500] = xyz[17]            # ... and a later tie: the first one wins
+    ix = ops.GridIndex(ctx, _dev(ctx, xyz))
+    bq, bd = ops.nearest_query(ix, _dev(ctx, q))
+    _, ed = ora.KdTree(xyz).knn(q, 1)
+    best, mix = -1, 9999.0
+    for j in range(len(q)):     # main_blend.cpp:314-320
+        if ed[j, 0] < mix:
+            mix, best = ed[j, 0], j
+    assert (bq, bd) == (best, mix) == (4000, 0.0)
+    bq, bd = ops.nearest_query(ix, _dev(ctx, q + 1e6))     # nothing under the bound
+    assert bq == -1 and bd == 9999.0
+
+
+def test_plane_fit_segments_and_radius_normals(ctx):
+    from pointcloudprocess_amd import ops, synth
+    xyz = synth.street_scene(30_000, 71, extent=(30.0, 30.0)).double().numpy()
+    ix = ops.GridIndex(ctx, _dev(ctx, xyz))
+    g = ops.normals_radius(ix, 0.3).cpu().numpy()
+    t = ora.KdTree(xyz)
+    lib = ora.load()
+    for i in range(0, len(xyz), 97):
+        ei, _ = t.radius(xyz[i], 0.3)
+        e = np.zeros(1, dtype=ora.PLANE)
+        if len(ei) == 0:
+            continue
+        nb = np.ascontiguousarray(xyz[ei])
+        lib.ora_plane_h_points(nb.ctypes.data, len(ei), e.ctypes.data)
+        ev = np.array([e[f][0] for f in ("normal_x", "normal_y", "normal_z", "min_value", "curvature", "distance")])
+        assert np.array_equal(g[i], ev.astype(np.float32), equal_nan=True), f"point {i}"
