@@ -189,6 +189,20 @@ int pcp_icp_destroy(pcp_icp* icp);
  * winner per query in the ORIGINAL query order (-1 / +inf when rejected). */
 int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T_host[16], float rmax,
                  double* acc_dev, int32_t* corr_idx_dev, float* corr_d2_dev);
+/* Target-sharded multi-GPU mode: each rank indexes one shard of the
+ * target (global indices [target_offset, target_offset + shard size)) and runs the ICP query
+ * set against it.  pcp_icp_keys writes, per query in the ORIGINAL order (nq keys), the u64
+ * key (fp32 bits of d2) << 32 | global target index, or INT64_MAX when no target of this
+ * shard is within rmax; an element-wise MIN over ranks (all-reduce) yields the global
+ * lexicographic (d2, index) winner.  pcp_icp_accumulate_keys then adds the 24 accumulators
+ * of the queries whose global winner lies in this rank's shard [lo, hi) (shard_xyz_dev:
+ * the shard's fp32 points in shard order); a SUM over ranks gives the full accumulators. */
+int pcp_icp_keys(pcp_ctx* ctx, pcp_icp* icp, const double T_host[16], float rmax,
+                 int64_t target_offset, uint64_t* keys_dev);
+int pcp_icp_accumulate_keys(pcp_ctx* ctx, pcp_icp* icp, const double T_host[16],
+                            const uint64_t* keys_dev, int64_t lo, int64_t hi,
+                            const float* shard_xyz_dev, size_t shard_stride_bytes,
+                            double* acc_dev);
 /* Host Kabsch/Umeyama solve of the increment dT from 24 accumulators (host memory). */
 int pcp_icp_solve(const double acc_host[24], int do_scale, double dT_host[16]);
 /* Full loop: T_inout (row-major), `iters` iterations (stops early when the increment's

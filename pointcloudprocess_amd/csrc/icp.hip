@@ -426,6 +426,88 @@ __global__ void k_fill_corr(int32_t* idx, float* d2, int64_t n) {
     }
 }
 
+// ---- target-sharded mode: per-query u64 key = (fp32 bits of d2) << 32 |
+// global target index, so a MIN over ranks is the lexicographic (d2, index) winner (non-
+// negative fp32 bit patterns order like the values).  No correspondence = INT64_MAX.
+constexpr uint64_t kNoKey = 0x7fffffffffffffffull;
+
+__global__ void k_fill_keys(uint64_t* keys, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        keys[i] = kNoKey;
+}
+
+__global__ void k_make_keys(const float4* q, const int32_t* win, const float* wd2, int64_t n, uint32_t offset,
+                            uint64_t* keys) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int oq = __float_as_int(q[i].w);
+        const int w = win[i];
+        keys[oq] = w < 0 ? kNoKey
+                         : (((uint64_t)__float_as_uint(wd2[i]) << 32) | (uint64_t)(uint32_t)((uint32_t)w + offset));
+    }
+}
+
+// accumulators over the queries whose global winner lies in [lo, hi) (this rank's shard);
+// float products are exact in fp64, so only the summation order differs from the oracle
+__global__ void __launch_bounds__(256) k_acc_keys(const float4* q, int64_t n, const uint64_t* keys, uint64_t lo,
+                                                  uint64_t hi, const float* shard, size_t stride_f, IcpArgs a,
+                                                  double* partials) {
+    double acc[kAcc - 1];
+#pragma unroll
+    for (int k = 0; k < kAcc - 1; k++) acc[k] = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 qq = q[i];
+        const uint64_t key = keys[__float_as_int(qq.w)];
+        if (key == kNoKey) continue;
+        const uint64_t g = key & 0xffffffffull;
+        if (g < lo || g >= hi) continue;
+        const float* p = shard + (size_t)(g - lo) * stride_f;
+        float x, y, z;
+        xform(a, qq, x, y, z);
+        const double qv[3] = {x, y, z}, pv[3] = {p[0], p[1], p[2]};
+        acc[0] += 1.0;
+#pragma unroll
+        for (int c = 0; c < 3; c++) { acc[1 + c] += qv[c]; acc[4 + c] += pv[c]; }
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) acc[7 + 3 * r + c] += qv[r] * pv[c];
+        acc[16] += qv[0] * qv[0]; acc[17] += qv[0] * qv[1]; acc[18] += qv[0] * qv[2];
+        acc[19] += qv[1] * qv[1]; acc[20] += qv[1] * qv[2]; acc[21] += qv[2] * qv[2];
+        acc[22] += (double)__uint_as_float((uint32_t)(key >> 32));
+    }
+    __shared__ double sm[4][kAcc];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kAcc - 1; k++) {
+        double v = acc[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) sm[wv][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kAcc) {
+        double v = 0.0;
+        if (threadIdx.x < kAcc - 1)
+            for (int w = 0; w < 4; w++) v += sm[w][threadIdx.x];
+        partials[(int64_t)blockIdx.x * kAcc + threadIdx.x] = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sum_partials(const double* part, int nb, double* out) {
+    __shared__ double s[256];
+    for (int k = 0; k < kAcc; k++) {
+        double v = 0.0;
+        for (int b = threadIdx.x; b < nb; b += 256) v += part[(int64_t)b * kAcc + k];
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[k] = s[0];
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ host 3x3 solve
 // One-sided Jacobi SVD of a 3x3 matrix: A = U diag(s) V^T (columns of U, V).
 void svd3(const double Ain[9], double U[9], double s[3], double V[9]) {
@@ -698,6 +780,52 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
         std::fprintf(stderr, "[pcp icp dbg=%d] octant %.4f ms  fallback %.4f ms  n_fallback %u\n", icp->dbg, m1,
                      ms - m1, icp->last_fallback);
     }
+    return PCP_OK;
+}
+
+int pcp_icp_keys(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, int64_t target_offset,
+                 uint64_t* keys_dev) {
+    if (!ctx || !icp || !T || !keys_dev || !(rmax >= 0.f) || target_offset < 0 ||
+        target_offset + pcp_index_size(icp->target) > ((int64_t)1 << 32))
+        return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    icp->ctx = ctx;
+    const int saved = icp->dbg;
+    icp->dbg |= pcp::kDbgNoAccum;  // correspondences only
+    const int rc = pcp::icp_launch(icp, T, rmax, icp->acc, nullptr, nullptr);
+    icp->dbg = saved;
+    PCP_TRY(rc);
+    if (icp->nq_in > icp->nq)
+        hipLaunchKernelGGL(pcp::k_fill_keys, dim3(pcp::grid_for(icp->nq_in, 256)), dim3(256), 0, ctx->stream, keys_dev,
+                           icp->nq_in);
+    if (icp->nq > 0)
+        hipLaunchKernelGGL(pcp::k_make_keys, dim3(pcp::grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, icp->q,
+                           (const int32_t*)icp->win, (const float*)icp->wd2, icp->nq, (uint32_t)target_offset,
+                           keys_dev);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_icp_accumulate_keys(pcp_ctx* ctx, pcp_icp* icp, const double T[16], const uint64_t* keys_dev,
+                            int64_t lo, int64_t hi, const float* shard_xyz_dev, size_t shard_stride_bytes,
+                            double* acc_dev) {
+    if (!ctx || !icp || !T || !keys_dev || !acc_dev || lo < 0 || hi < lo || (hi > lo && !shard_xyz_dev))
+        return PCP_ERR_ARG;
+    if (shard_stride_bytes == 0) shard_stride_bytes = 3 * sizeof(float);
+    if (shard_stride_bytes % sizeof(float)) return pcp::set_error(ctx, PCP_ERR_ARG, "shard stride must be whole floats");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    pcp::IcpArgs a{};
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) a.R[3 * r + c] = (float)T[4 * r + c];
+        a.t[r] = (float)T[4 * r + 3];
+    }
+    const int nb = (int)std::min<int64_t>(std::max<int64_t>(1, (icp->nq + 255) / 256), icp->nb_fast + icp->nb_ring);
+    hipLaunchKernelGGL(pcp::k_acc_keys, dim3(nb), dim3(256), 0, ctx->stream, icp->q, icp->nq, keys_dev,
+                       (uint64_t)lo, (uint64_t)hi, shard_xyz_dev, shard_stride_bytes / sizeof(float), a,
+                       icp->partials);
+    hipLaunchKernelGGL(pcp::k_sum_partials, dim3(1), dim3(256), 0, ctx->stream, (const double*)icp->partials, nb,
+                       acc_dev);
+    PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }
 

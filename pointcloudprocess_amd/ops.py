@@ -258,6 +258,7 @@ class ICP:
         ctx.check(ctx.lib.pcp_icp_create(ctx.h, target_index.h, _ptr(q), q.stride(0) * q.element_size(),
                                          q.shape[0], C.byref(h)))
         self.h = h
+        self.nq_in = q.shape[0]
         self.acc = torch.zeros(24, dtype=torch.float64, device=ctx.device)
 
     def step(self, T, rmax, corr=False):
@@ -280,6 +281,23 @@ class ICP:
         if rc not in (0, -6):
             ctx.check(rc)
         return float(err.value), np.array(T[:]).reshape(4, 4)
+
+    def keys(self, T, rmax, target_offset=0):
+        """Target-sharded mode: per-query int64 keys (fp32 d2 bits << 32 | global target
+        index, INT64_MAX = none) in the original query order."""
+        ctx = self.ctx
+        keys = torch.empty(self.nq_in, dtype=torch.int64, device=ctx.device)
+        Tm = _lib.f64arr(np.asarray(T, dtype=np.float64).reshape(16))
+        ctx.check(ctx.lib.pcp_icp_keys(ctx.h, self.h, Tm, float(rmax), int(target_offset), _ptr(keys)))
+        return keys
+
+    def accumulate_keys(self, T, keys, lo, hi, shard_xyz):
+        """24 accumulators of the queries whose (MIN-reduced) winner is in [lo, hi)."""
+        ctx = self.ctx
+        Tm = _lib.f64arr(np.asarray(T, dtype=np.float64).reshape(16))
+        ctx.check(ctx.lib.pcp_icp_accumulate_keys(ctx.h, self.h, Tm, _ptr(keys), int(lo), int(hi), _ptr(shard_xyz),
+                                                  shard_xyz.stride(0) * shard_xyz.element_size(), _ptr(self.acc)))
+        return self.acc
 
     def last_kernel_ms(self):
         ms, n = C.c_double(), C.c_int()

@@ -1,0 +1,78 @@
+"""Multi-rank protocol of the ICP loop on CPU: world_size 2 over gloo,
+each rank driving pointcloudprocess_amd.distributed with the oracle engine.  Both
+partitionings must reproduce the single-process ICP (same correspondences; fp64 sums in a
+different order -> poses equal to 1e-12)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _data():
+    from pointcloudprocess_amd import synth
+    T_true = synth.rigid(0.3, 0.1, -0.1, (0.06, -0.04, 0.02))
+    tgt, q = synth.icp_pair(40_000, 40_000, 81, 82, T_true, extent=(30.0, 30.0))
+    return tgt.numpy(), q.numpy(), T_true
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, out):
+    import sys
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle_engine import OracleEngine
+    from pointcloudprocess_amd import distributed as D
+    tgt, q, _ = _data()
+    if mode == "copartitioned":
+        # x-slabs of the query set; the target tile carries a 1 m halo (>> rmax + motion)
+        cut = 0.0
+        lo_x, hi_x = (-np.inf, cut) if rank == 0 else (cut, np.inf)
+        qm = (q[:, 0] >= lo_x) & (q[:, 0] < hi_x)
+        tm = (tgt[:, 0] >= lo_x - 1.0) & (tgt[:, 0] < hi_x + 1.0)
+        eng = OracleEngine(tgt[tm], q[qm])
+        err, T = D.run_copartitioned(eng, np.eye(4), 0.25, 8)
+    else:
+        lo, hi = D.shard_range(len(tgt), world, rank)
+        eng = OracleEngine(tgt[lo:hi], q)
+        err, T = D.run_target_sharded(eng, np.eye(4), 0.25, 8, lo, hi)
+    out[rank] = (err, T)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["copartitioned", "target_sharded"])
+def test_two_ranks_match_single_process(mode):
+    import oracle_ctypes as ora
+    tgt, q, T_true = _data()
+    e_err, e_T = ora.icp(tgt, q, np.eye(4), 0.25, 8)
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        err, T = out[r]
+        assert np.abs(T - e_T).max() < 1e-12, f"rank {r}: {np.abs(T - e_T).max()}"
+        assert abs(err - e_err) < 1e-9
+    assert np.abs(out[0][1] - T_true).max() < 1e-2  # converging towards the true motion
+
+
+def test_shard_range_covers():
+    from pointcloudprocess_amd.distributed import shard_range
+    for n in (0, 1, 7, 1000):
+        for w in (1, 2, 3, 8):
+            rs = [shard_range(n, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))

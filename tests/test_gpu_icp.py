@@ -116,3 +116,32 @@ def test_sparse_grid_matches_oracle(ctx):
     acc, ci, cd = icp.step(T, 0.1, corr=True)
     ei, ed = ora.F32Index(tgt).correspond(q, T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32), 0.1)
     assert np.array_equal(ci.cpu().numpy(), ei)
+
+
+def test_target_sharded_keys_match_oracle(ctx):
+    """Target-sharded mode emulated on one GPU: two shard engines, MIN of
+    their keys = the oracle's global correspondences (bit-exact); the per-shard accumulators
+    sum to the oracle's fp64 accumulators (same exact products, different order)."""
+    import torch
+    from pointcloudprocess_amd import distributed as D, synth
+    T_true = synth.rigid()
+    tgt, q = _pair(120_000, 31, T_true)
+    n = tgt.shape[0]
+    dq = q.to(ctx.device)
+    shards = [D.shard_range(n, 2, r) for r in range(2)]
+    engines = [D.GpuEngine(ctx, tgt[lo:hi].to(ctx.device), dq, cell_size=0.1) for lo, hi in shards]
+    T = synth.rigid(0.1, 0.05, 0.0, (0.02, 0.01, 0.0))
+    keys = torch.minimum(engines[0].keys(T, 0.25, shards[0][0]), engines[1].keys(T, 0.25, shards[1][0]))
+    k = keys.cpu().numpy()
+    R = T[:3, :3].astype(np.float32)
+    t = T[:3, 3].astype(np.float32)
+    ei, ed = ora.F32Index(tgt.numpy()).correspond(q.numpy(), R, t, 0.25)
+    none = k == np.iinfo(np.int64).max
+    assert np.array_equal(none, ei < 0)
+    assert np.array_equal((k[~none] & 0xFFFFFFFF).astype(np.int32), ei[~none])
+    assert np.array_equal((k[~none] >> 32).astype(np.uint32).view(np.float32), ed[~none])
+    acc = sum(e.accumulate_keys(T, keys, lo, hi).cpu().numpy().copy() for e, (lo, hi) in zip(engines, shards))
+    eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
+    assert np.allclose(acc[:23], eacc[:23], rtol=1e-12, atol=1e-12 * np.abs(eacc[:23]).max())
+    for e in engines:
+        e.close()
