@@ -238,6 +238,7 @@ __global__ __launch_bounds__(kB) void k_centre_f32(const P48* in, int64_t n, dou
 
 // device buffers of one voxel-filter call
 struct VoxBufs {
+    pcp_ctx* ctx;
     uint32_t* flag = nullptr;
     uint32_t* k0 = nullptr;
     uint32_t* k1 = nullptr;
@@ -246,7 +247,8 @@ struct VoxBufs {
     uint32_t* head = nullptr;
     void* tmp = nullptr;
     ~VoxBufs() {
-        hipFree(flag); hipFree(k0); hipFree(k1); hipFree(v0); hipFree(v1); hipFree(head); hipFree(tmp);
+        dfree(ctx, flag); dfree(ctx, k0); dfree(ctx, k1); dfree(ctx, v0); dfree(ctx, v1); dfree(ctx, head);
+        dfree(ctx, tmp);
     }
 };
 
@@ -262,7 +264,7 @@ int minmax_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, doub
     std::vector<double> h(8 * nb);
     hipError_t e = hipMemcpyAsync(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    hipFree(part);
+    dfree(ctx, part);
     if (e != hipSuccess) return hip_fail(ctx, e, "minmax", __FILE__, __LINE__);
     for (unsigned b = 0; b < nb; b++)
         for (int a = 0; a < 4; a++) {
@@ -283,7 +285,7 @@ static int sums_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense,
     std::vector<double> h(5 * nb);
     hipError_t e = hipMemcpyAsync(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    hipFree(part);
+    dfree(ctx, part);
     if (e != hipSuccess) return hip_fail(ctx, e, "centroid", __FILE__, __LINE__);
     for (unsigned b = 0; b < nb; b++)
         for (int a = 0; a < 5; a++) s[a] += h[5 * b + a];
@@ -332,7 +334,7 @@ static int voxel_filter_impl(pcp_ctx* ctx, const P48* in, int64_t n, int is_dens
     g.mul1 = (uint32_t)div_b[0];  // divb_mul_ in wrapping int32 (:847)
     g.mul2 = (uint32_t)div_b[0] * (uint32_t)div_b[1];
 
-    VoxBufs b;
+    VoxBufs b{ctx};
     PCP_TRY(dmalloc(ctx, &b.k0, n));
     PCP_TRY(dmalloc(ctx, &b.k1, n));
     PCP_TRY(dmalloc(ctx, &b.v0, n));
@@ -431,7 +433,7 @@ int pcp_remove_duplicate(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, 
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
         if (e != hipSuccess) rc = hip_fail(ctx, e, "remove_duplicate", __FILE__, __LINE__);
     }
-    hipFree(tmp);
+    dfree(ctx, tmp);
     if (rc == PCP_OK) *n_out = m;
     return rc;
 }
@@ -482,8 +484,8 @@ int pcp_get_rot_icp(pcp_ctx* ctx, const void* src, int64_t ns, const void* tmp, 
     }
     if (icp) pcp_icp_destroy(icp);
     if (ix) pcp_index_destroy(ix);
-    hipFree(fs);
-    hipFree(ft);
+    dfree(ctx, fs);
+    dfree(ctx, ft);
     return rc;
 }
 

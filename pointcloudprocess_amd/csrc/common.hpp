@@ -4,7 +4,9 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <map>
 #include <string>
+#include <unordered_map>
 
 #include "../../include/pcp.h"
 
@@ -17,6 +19,14 @@ struct pcp_ctx {
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
     uint32_t bf_fallback = 0;  // queries of the last pcp_knn_bruteforce that needed the exact scan
+    // Caching device allocator for the library's internal buffers (index builds, ICP state,
+    // per-call scratch): blocks are reused in stream order on this context's stream instead
+    // of paying a synchronising hipMalloc/hipFree each time.  Objects allocated through a
+    // context must be destroyed before it.
+    std::multimap<size_t, void*> free_blocks;
+    std::unordered_map<void*, size_t> block_size;
+    size_t cached_bytes = 0;
+    size_t cache_cap = (size_t)16 << 30;
 };
 
 namespace pcp {
@@ -40,19 +50,18 @@ int scratch(pcp_ctx* ctx, size_t bytes, void** out);
 
 #define PCP_LAUNCH_CHECK(ctx) PCP_HIP(ctx, hipGetLastError())
 
+// cached device allocation of `bytes` (>= 1) on ctx; dfree returns it to ctx's cache
+int cache_alloc(pcp_ctx* ctx, size_t bytes, void** p);
+void dfree(pcp_ctx* ctx, void* p);
+void cache_release(pcp_ctx* ctx);
+
 template <typename T>
 int dmalloc(pcp_ctx* ctx, T** p, size_t count) {
-    *p = nullptr;
-    if (count == 0) count = 1;
-    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        return set_error(ctx, PCP_ERR_NOMEM, "hipMalloc(%zu bytes) failed: %s",
-                         count * sizeof(T), hipGetErrorString(e));
-    }
-    return PCP_OK;
+    void* v = nullptr;
+    const int rc = cache_alloc(ctx, (count ? count : 1) * sizeof(T), &v);
+    *p = (T*)v;
+    return rc;
 }
-
 inline unsigned grid_for(int64_t n, int block, int64_t cap = 1 << 20) {
     int64_t g = (n + block - 1) / block;
     if (g < 1) g = 1;

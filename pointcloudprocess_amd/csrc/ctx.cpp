@@ -1,6 +1,8 @@
 // Context, error and memory helpers of the C-ABI (host code, built by hipcc).
 #include <cstdarg>
+#include <algorithm>
 #include <cstring>
+#include <iterator>
 
 #include "common.hpp"
 
@@ -44,6 +46,66 @@ int scratch(pcp_ctx* ctx, size_t bytes, void** out) {
     return PCP_OK;
 }
 
+static size_t round_block(size_t b) {
+    const size_t g = b >= ((size_t)1 << 20) ? ((size_t)2 << 20) : 4096;
+    return (b + g - 1) / g * g;
+}
+
+int cache_alloc(pcp_ctx* ctx, size_t bytes, void** p) {
+    *p = nullptr;
+    const size_t want = round_block(bytes ? bytes : 1);
+    auto it = ctx->free_blocks.lower_bound(want);
+    if (it != ctx->free_blocks.end() && it->first <= want + want / 4 + ((size_t)2 << 20)) {
+        *p = it->second;
+        ctx->cached_bytes -= it->first;
+        ctx->free_blocks.erase(it);
+        return PCP_OK;
+    }
+    hipError_t e = hipMalloc(p, want);
+    if (e != hipSuccess && !ctx->free_blocks.empty()) {  // give the cache back and retry
+        (void)hipGetLastError();
+        cache_release(ctx);
+        e = hipMalloc(p, want);
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return set_error(ctx, PCP_ERR_NOMEM, "hipMalloc(%zu bytes) failed: %s", want, hipGetErrorString(e));
+    }
+    ctx->block_size[*p] = want;
+    return PCP_OK;
+}
+
+void dfree(pcp_ctx* ctx, void* p) {
+    if (!p) return;
+    auto it = ctx ? ctx->block_size.find(p) : decltype(ctx->block_size.end()){};
+    if (!ctx || it == ctx->block_size.end()) {
+        (void)hipFree(p);
+        return;
+    }
+    ctx->free_blocks.emplace(it->second, p);
+    ctx->cached_bytes += it->second;
+    // over the cap: drop the largest cached blocks (stream work using them is complete
+    // before hipFree returns, hipFree synchronises)
+    while (ctx->cached_bytes > ctx->cache_cap && !ctx->free_blocks.empty()) {
+        auto last = std::prev(ctx->free_blocks.end());
+        ctx->cached_bytes -= last->first;
+        ctx->block_size.erase(last->second);
+        (void)hipFree(last->second);
+        ctx->free_blocks.erase(last);
+    }
+}
+
+void cache_release(pcp_ctx* ctx) {
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->free_blocks) {
+        ctx->block_size.erase(kv.second);
+        (void)hipFree(kv.second);
+    }
+    ctx->free_blocks.clear();
+    ctx->cached_bytes = 0;
+}
+
 }  // namespace pcp
 
 extern "C" {
@@ -63,6 +125,8 @@ int pcp_ctx_create(int device, void* stream, pcp_ctx** out) {
     pcp_ctx* c = new pcp_ctx();
     c->device = device;
     c->stream = (hipStream_t)stream;  // NULL = the device's default (null) stream
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) c->cache_cap = std::min(c->cache_cap, tot / 8);
     *out = c;
     return PCP_OK;
 }
@@ -72,6 +136,7 @@ int pcp_ctx_destroy(pcp_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    pcp::cache_release(ctx);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return PCP_OK;
@@ -98,9 +163,15 @@ int pcp_sync(pcp_ctx* ctx) {
     return PCP_OK;
 }
 
-int pcp_malloc(pcp_ctx* ctx, void** p, size_t bytes) {
+int pcp_malloc(pcp_ctx* ctx, void** p, size_t bytes) {  // caller memory: not cached
     if (!ctx || !p) return PCP_ERR_ARG;
-    return pcp::dmalloc(ctx, (char**)p, bytes);
+    hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return pcp::set_error(ctx, PCP_ERR_NOMEM, "hipMalloc(%zu bytes) failed", bytes);
+    }
+    return PCP_OK;
 }
 
 int pcp_free(pcp_ctx* ctx, void* p) {

@@ -49,16 +49,13 @@ __global__ void k_compact(const T* xyz, size_t stride, int64_t n_in, const int32
     }
 }
 
+// flags -> bitmask (bit i of word i/32): one coalesced flag per lane, a wave ballot per 64
 __global__ void k_pack_bits(const uint32_t* flag, int64_t n, uint32_t* bits) {
-    int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    int64_t nw = (n + 31) / 32;
-    if (w >= nw) return;
-    uint32_t v = 0;
-    for (int b = 0; b < 32; b++) {
-        int64_t i = w * 32 + b;
-        if (i < n && flag[i]) v |= 1u << b;
-    }
-    bits[w] = v;
+    const int64_t base = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~(int64_t)63;
+    const int64_t i = base + (threadIdx.x & 63);
+    const uint64_t m = __ballot(i < n && flag[i] != 0u);
+    const int lane = threadIdx.x & 63;
+    if (lane < 2 && base + 32 * lane < n) bits[(base >> 5) + lane] = (uint32_t)(m >> (32 * lane));
 }
 
 template <typename T>
@@ -130,13 +127,16 @@ __global__ void k_brick_final(int32_t* brick, int64_t nb, const uint32_t* bits) 
     }
 }
 
+// per-cell counts and each point's arrival rank; `mark` (dense mode) also flags the
+// point's brick for the two-level search's occupancy table
 template <typename T>
-__global__ void k_count(GridDesc g, const T* cxyz, int64_t n, uint32_t* count, uint32_t* rank) {
+__global__ void k_count(GridDesc g, const T* cxyz, int64_t n, uint32_t* count, uint32_t* rank, int32_t* mark) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         int cx, cy, cz;
         cell_of_point<T>(g, cxyz + 3 * i, cx, cy, cz);
         rank[i] = atomicAdd(&count[cell_id(g, cx, cy, cz)], 1u);
+        if (mark) mark[brick_of(g, cx, cy, cz)] = 1;
     }
 }
 
@@ -243,27 +243,27 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     int rc;
     const int64_t nw = (n_in + 31) / 32;
     if ((rc = dmalloc(ctx, &flag, n_in + 1)) || (rc = dmalloc(ctx, &bits, nw + 1))) {
-        hipFree(flag); hipFree(bits);
+        dfree(ctx, flag); dfree(ctx, bits);
         return fail(rc);
     }
     uint32_t nvalid = 0;
     if (n_in > 0) {
         hipLaunchKernelGGL(k_valid<T>, dim3(grid_for(n_in, kB)), dim3(kB), 0, st, xyz, stride, n_in, indices, flag);
-        hipLaunchKernelGGL(k_pack_bits, dim3(grid_for(nw, kB)), dim3(kB), 0, st, flag, n_in, bits);
+        hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)((n_in + kB - 1) / kB)), dim3(kB), 0, st, flag, n_in, bits);
         rc = scan_u32_inplace(ctx, flag, n_in, &nvalid);
-        if (rc) { hipFree(flag); hipFree(bits); return fail(rc); }
+        if (rc) { dfree(ctx, flag); dfree(ctx, bits); return fail(rc); }
     }
     ix->n = nvalid;
     ix->identity = (indices == nullptr && (int64_t)nvalid == n_in) ? 1 : 0;
     if ((rc = dmalloc(ctx, &cxyz, 3 * (size_t)(nvalid + 1))) || (rc = dmalloc(ctx, &ix->mapping, nvalid + 1))) {
-        hipFree(flag); hipFree(bits); hipFree(cxyz);
+        dfree(ctx, flag); dfree(ctx, bits); dfree(ctx, cxyz);
         return fail(rc);
     }
     if (n_in > 0)
         hipLaunchKernelGGL(k_compact<T>, dim3(grid_for(n_in, kB)), dim3(kB), 0, st, xyz, stride, n_in,
                            indices, flag, bits, cxyz, ix->mapping);
-    hipFree(flag);
-    hipFree(bits);  // (stream-ordered frees are safe: hipFree synchronises)
+    dfree(ctx, flag);
+    dfree(ctx, bits);  // cached: reuse is stream-ordered on ctx's stream
     const int64_t n = nvalid;
 
     // ---- bbox
@@ -271,13 +271,13 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     if (n > 0) {
         const unsigned nbk = grid_for(n, kB, 1024);
         double* part;
-        if ((rc = dmalloc(ctx, &part, 6 * (size_t)nbk))) { hipFree(cxyz); return fail(rc); }
+        if ((rc = dmalloc(ctx, &part, 6 * (size_t)nbk))) { dfree(ctx, cxyz); return fail(rc); }
         hipLaunchKernelGGL(k_minmax<T>, dim3(nbk), dim3(kB), 0, st, cxyz, n, part);
         std::vector<double> hp(6 * nbk);
         hipMemcpyAsync(hp.data(), part, hp.size() * sizeof(double), hipMemcpyDeviceToHost, st);
         hipError_t e = hipStreamSynchronize(st);
-        hipFree(part);
-        if (e != hipSuccess) { hipFree(cxyz); return fail(hip_fail(ctx, e, "bbox", __FILE__, __LINE__)); }
+        dfree(ctx, part);
+        if (e != hipSuccess) { dfree(ctx, cxyz); return fail(hip_fail(ctx, e, "bbox", __FILE__, __LINE__)); }
         for (int a = 0; a < 3; a++) { mn[a] = INFINITY; mx[a] = -INFINITY; }
         for (unsigned b = 0; b < nbk; b++)
             for (int a = 0; a < 3; a++) {
@@ -303,12 +303,12 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     }
     uint32_t* count = nullptr;
     uint32_t* rank = nullptr;
-    if ((rc = dmalloc(ctx, &rank, n + 1))) { hipFree(cxyz); return fail(rc); }
+    if ((rc = dmalloc(ctx, &rank, n + 1))) { dfree(ctx, cxyz); return fail(rc); }
     for (int attempt = 0; attempt < 3; attempt++) {
         GridDesc g{};
         while (!make_geometry(g, mn, mx, h, cap)) h *= 2.0;
-        hipFree(ix->brick); ix->brick = nullptr;
-        hipFree(count); count = nullptr;
+        dfree(ctx, ix->brick); ix->brick = nullptr;
+        dfree(ctx, count); count = nullptr;
         const int64_t ncells_dense = (int64_t)g.n[0] * g.n[1] * g.n[2];
         g.dense = (!force_sparse && ncells_dense <= dense_cap) ? 1 : 0;
         g.ncells = ncells_dense;
@@ -318,9 +318,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             g.nslots = 0;
             if ((rc = dmalloc(ctx, &ix->brick, g.nbricks))) break;
             PCP_HIP(ctx, hipMemsetAsync(ix->brick, 0, (size_t)g.nbricks * sizeof(int32_t), st));
-            if (n > 0) hipLaunchKernelGGL(k_mark<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, ix->brick);
-            hipLaunchKernelGGL(k_brick_flag, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks);
-            g.brick = ix->brick;
+            g.brick = ix->brick;  // marked by k_count, turned into 0 / -1 flags below
         } else {
             if ((rc = dmalloc(ctx, &ix->brick, g.nbricks))) break;
             PCP_HIP(ctx, hipMemsetAsync(ix->brick, 0, (size_t)g.nbricks * sizeof(int32_t), st));
@@ -331,16 +329,20 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             hipLaunchKernelGGL(k_brick_bits, dim3(grid_for(nbw, kB)), dim3(kB), 0, st, ix->brick, g.nbricks, bbits);
             uint32_t nslots = 0;
             rc = scan_u32_inplace(ctx, (uint32_t*)ix->brick, g.nbricks, &nslots);
-            if (rc) { hipFree(bbits); break; }
+            if (rc) { dfree(ctx, bbits); break; }
             hipLaunchKernelGGL(k_brick_final, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks, bbits);
-            hipFree(bbits);
+            dfree(ctx, bbits);
             g.nslots = nslots;
             g.brick = ix->brick;
             ncells = (int64_t)nslots * 64;
         }
         if ((rc = dmalloc(ctx, &count, ncells + 1))) break;
         PCP_HIP(ctx, hipMemsetAsync(count, 0, (size_t)(ncells + 1) * sizeof(uint32_t), st));
-        if (n > 0) hipLaunchKernelGGL(k_count<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, count, rank);
+        if (n > 0)
+            hipLaunchKernelGGL(k_count<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, count, rank,
+                               g.dense ? ix->brick : nullptr);
+        if (g.dense)
+            hipLaunchKernelGGL(k_brick_flag, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks);
         if (auto_h && attempt < 2 && n > 0) {
             unsigned long long* d_ne;
             if ((rc = dmalloc(ctx, &d_ne, 1))) break;
@@ -349,7 +351,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             unsigned long long ne = 0;
             hipMemcpyAsync(&ne, d_ne, sizeof(ne), hipMemcpyDeviceToHost, st);
             hipStreamSynchronize(st);
-            hipFree(d_ne);
+            dfree(ctx, d_ne);
             double occ = (double)n / std::max(1.0, (double)ne);
             if (occ > 12.0) { h *= std::sqrt(4.0 / occ); continue; }   // surface-like data
             if (occ < 1.5) { h *= std::cbrt(4.0 / occ); continue; }    // sparser than assumed
@@ -370,12 +372,12 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             V4* pts2;
             int32_t* sj2;
             if ((rc = dmalloc(ctx, &pts2, n + 1))) break;
-            if ((rc = dmalloc(ctx, &sj2, n + 1))) { hipFree(pts2); break; }
+            if ((rc = dmalloc(ctx, &sj2, n + 1))) { dfree(ctx, pts2); break; }
             hipLaunchKernelGGL(k_cell_sort<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const V4*)ix->pts,
                                (const int32_t*)ix->sorted_j, n, pts2, sj2);
             PCP_HIP(ctx, hipStreamSynchronize(st));
-            hipFree(ix->pts);
-            hipFree(ix->sorted_j);
+            dfree(ctx, ix->pts);
+            dfree(ctx, ix->sorted_j);
             ix->pts = pts2;
             ix->sorted_j = sj2;
         }
@@ -387,9 +389,9 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         }
         break;
     }
-    hipFree(count);
-    hipFree(rank);
-    hipFree(cxyz);
+    dfree(ctx, count);
+    dfree(ctx, rank);
+    dfree(ctx, cxyz);
     if (rc) return fail(rc);
     PCP_HIP(ctx, hipGetLastError());
     PCP_HIP(ctx, hipStreamSynchronize(st));
@@ -426,12 +428,12 @@ int pcp_index_build_f32(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n
 int pcp_index_destroy(pcp_index* ix) {
     if (!ix) return PCP_ERR_ARG;
     if (ix->owner) (void)hipSetDevice(ix->owner->device);
-    hipFree(ix->brick);
-    hipFree(ix->cstart);
-    hipFree(ix->pts);
-    hipFree(ix->mapping);
-    hipFree(ix->sorted_j);
-    hipFree(ix->pos_of_j);
+    pcp::dfree(ix->owner, ix->brick);
+    pcp::dfree(ix->owner, ix->cstart);
+    pcp::dfree(ix->owner, ix->pts);
+    pcp::dfree(ix->owner, ix->mapping);
+    pcp::dfree(ix->owner, ix->sorted_j);
+    pcp::dfree(ix->owner, ix->pos_of_j);
     delete ix;
     return PCP_OK;
 }

@@ -110,6 +110,28 @@ struct Best {
         }
         for (; k < e; k++) consider(qx, qy, qz, pts[k], k);
     }
+    // rows r = 0..3 ([rs[r], rs[r] + rn[r])) scanned as one concatenated list, 4 loads in flight
+    template <typename P>
+    __device__ __forceinline__ void scan_rows(const P* pts, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
+                                              float qx, float qy, float qz) {
+        const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
+        auto addr = [&](uint32_t v) {
+            return v < c1 ? rs[0] + v : (v < c2 ? rs[1] + (v - c1) : (v < c3 ? rs[2] + (v - c2) : rs[3] + (v - c3)));
+        };
+        uint32_t v = 0;
+        for (; v + 4 <= L; v += 4) {
+            const uint32_t k0 = addr(v), k1 = addr(v + 1), k2 = addr(v + 2), k3 = addr(v + 3);
+            const float4 p0 = pts[k0], p1 = pts[k1], p2 = pts[k2], p3 = pts[k3];
+            consider(qx, qy, qz, p0, k0);
+            consider(qx, qy, qz, p1, k1);
+            consider(qx, qy, qz, p2, k2);
+            consider(qx, qy, qz, p3, k3);
+        }
+        for (; v < L; v++) {
+            const uint32_t k = addr(v);
+            consider(qx, qy, qz, pts[k], k);
+        }
+    }
     // [s, e) sorted by x: binary search of q.x, then sweep outward while dx^2 <= bd.  A point
     // beyond the stop has a larger |dx| and fp32 d2 >= dx*dx (monotone rounding), so it can
     // neither beat nor tie the current best: the result equals a full scan of [s, e).
@@ -299,15 +321,22 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             bz = (int)floorf(cell_f<float>(g, qz, 2) - a.rho);
         }
         if (valid && !(a.dbg & kDbgNoScan)) {
+            // the 4 x-rows of the octant: all 8 row bounds are loaded at once, then the rows
+            // are scanned as one concatenated candidate list with 4 loads in flight, so a
+            // chunk costs ~1 + L/4 memory round trips instead of 4 x (1 + len/4)
             const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
-            if (xa <= xb) {
-                for (int r = 0; r < 4; r++) {
-                    const int y = by + (r & 1), z = bz + (r >> 1);
-                    if (y < 0 || y >= g.n[1] || z < 0 || z >= g.n[2]) continue;
-                    const int64_t cc = dense_id(g, xa, y, z);
-                    b.scan(a.tp, g.cstart[cc], g.cstart[cc + (xb - xa + 1)], qx, qy, qz);
-                }
+            uint32_t rs[4], rn[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int y = by + (r & 1), z = bz + (r >> 1);
+                const bool in = xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
+                const int64_t cc = in ? dense_id(g, xa, y, z) : 0;
+                rs[r] = in ? g.cstart[cc] : 0u;
+                rn[r] = in ? g.cstart[cc + (xb - xa + 1)] : 0u;
             }
+#pragma unroll
+            for (int r = 0; r < 4; r++) rn[r] -= rs[r];
+            b.scan_rows(a.tp, rs, rn, qx, qy, qz);
         }
         // ---- epilogue: results, fallback list, accumulators
         const bool found = b.bj != 0x7fffffff;
@@ -744,15 +773,15 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
 int pcp_icp_destroy(pcp_icp* icp) {
     if (!icp) return PCP_ERR_ARG;
     (void)hipSetDevice(icp->ctx->device);
-    hipFree(icp->q);
-    hipFree(icp->partials);
-    hipFree(icp->acc);
-    hipFree(icp->win);
-    hipFree(icp->wd2);
-    hipFree(icp->fb);
-    hipFree(icp->fb_count);
-    hipFree(icp->fb_off);
-    hipFree(icp->fbc);
+    pcp::dfree(icp->ctx, icp->q);
+    pcp::dfree(icp->ctx, icp->partials);
+    pcp::dfree(icp->ctx, icp->acc);
+    pcp::dfree(icp->ctx, icp->win);
+    pcp::dfree(icp->ctx, icp->wd2);
+    pcp::dfree(icp->ctx, icp->fb);
+    pcp::dfree(icp->ctx, icp->fb_count);
+    pcp::dfree(icp->ctx, icp->fb_off);
+    pcp::dfree(icp->ctx, icp->fbc);
     if (icp->ev0) hipEventDestroy(icp->ev0);
     if (icp->ev1) hipEventDestroy(icp->ev1);
     if (icp->ev_mid) hipEventDestroy(icp->ev_mid);

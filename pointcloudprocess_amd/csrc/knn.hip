@@ -493,11 +493,13 @@ int check_f64_index(pcp_ctx* ctx, const pcp_index* ix) {
 
 int centroid_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, double c[4], uint32_t* count);
 
-// deferred-query list of one call (freed on scope exit; hipFree synchronises)
+// deferred-query list of one call (returned to the context's cache on scope exit)
 struct FarBuf {
     FarList f{nullptr, nullptr};
-    ~FarBuf() { hipFree(f.list); hipFree(f.count); }
-    int alloc(pcp_ctx* ctx, int64_t n) {
+    pcp_ctx* ctx = nullptr;
+    ~FarBuf() { dfree(ctx, f.list); dfree(ctx, f.count); }
+    int alloc(pcp_ctx* c, int64_t n) {
+        ctx = c;
         PCP_TRY(dmalloc(ctx, &f.list, n));
         PCP_TRY(dmalloc(ctx, &f.count, 1));
         PCP_HIP(ctx, hipMemsetAsync(f.count, 0, sizeof(uint32_t), ctx->stream));
@@ -687,7 +689,7 @@ int pcp_nearest_query(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t
             if (hd[b] < bd || (hd[b] == bd && hi[b] < bi)) { bd = hd[b]; bi = hi[b]; }
         if (!rc && bd < init_bound) { *best_d2 = bd; *best_q = bi; }
     }
-    hipFree(idx); hipFree(d2); hipFree(pd); hipFree(pi);
+    dfree(ctx, idx); dfree(ctx, d2); dfree(ctx, pd); dfree(ctx, pi);
     return rc;
 }
 
@@ -735,7 +737,7 @@ int pcp_knn_lod(pcp_ctx* ctx, const void* cloud, int64_t n, const void* q, int64
     }
     if (fi) pcp_index_destroy(fi);
     if (di) pcp_index_destroy(di);
-    hipFree(v);
+    dfree(ctx, v);
     return rc;
 }
 

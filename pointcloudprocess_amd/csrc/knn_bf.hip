@@ -354,10 +354,10 @@ int pcp_knn_bruteforce(pcp_ctx* ctx, const double* t, size_t tstride, int64_t nt
             if (e != hipSuccess) rc = hip_fail(ctx, e, "k_bf_mfma", __FILE__, __LINE__);
         }
     }
-    hipFree(t4);
-    hipFree(part);
-    hipFree(fb);
-    hipFree(fbc);
+    dfree(ctx, t4);
+    dfree(ctx, part);
+    dfree(ctx, fb);
+    dfree(ctx, fbc);
     return rc;
 }
 

@@ -121,6 +121,112 @@ int64_t scan_tmp_elems(int64_t n) {
     return total + 16;
 }
 
+// ---- single-pass u32 exclusive scan with decoupled look-back (one read + one write of the
+// data): tiles take ids in launch order from an atomic counter, publish their aggregate at
+// once and their inclusive prefix after looking back over predecessors (64 at a time, one
+// per lane of wave 0).  Status word = (2-bit state << 62) | 32-bit value.
+constexpr int kLbBlock = 256;
+constexpr int kLbSeg = 4;                       // segments of 1024 elements per tile
+constexpr int kLbTile = kLbBlock * 4 * kLbSeg;  // 4096 elements
+constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStMask = 3ull << 62;
+
+__device__ __forceinline__ uint64_t st_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(kLbBlock) k_scan_lookback(uint32_t* data, int64_t n, uint64_t* status,
+                                                            uint32_t* tile_ctr, uint32_t* total_out) {
+    __shared__ uint32_t s_tile, s_prefix;
+    __shared__ uint32_t s_wsum[kLbBlock / 64][kLbSeg];
+    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const int64_t base = (int64_t)tile * kLbTile;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t v[kLbSeg][4], sum[kLbSeg];
+#pragma unroll
+    for (int k = 0; k < kLbSeg; k++) {
+        const int64_t idx = base + k * 1024 + 4 * threadIdx.x;
+        if (idx + 3 < n) {
+            const uint4 u = *(const uint4*)(data + idx);
+            v[k][0] = u.x; v[k][1] = u.y; v[k][2] = u.z; v[k][3] = u.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[k][j] = idx + j < n ? data[idx + j] : 0u;
+        }
+        sum[k] = v[k][0] + v[k][1] + v[k][2] + v[k][3];
+    }
+    uint32_t incl[kLbSeg];
+#pragma unroll
+    for (int k = 0; k < kLbSeg; k++) {
+        incl[k] = wave_incl_scan(sum[k]);
+        if (lane == 63) s_wsum[wid][k] = incl[k];
+    }
+    __syncthreads();
+    uint32_t excl[kLbSeg], segpre[kLbSeg], tile_total = 0;
+#pragma unroll
+    for (int k = 0; k < kLbSeg; k++) {
+        uint32_t wofs = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kLbBlock / 64; w++) {
+            const uint32_t x = s_wsum[w][k];
+            wofs += w < wid ? x : 0u;
+            tot += x;
+        }
+        excl[k] = wofs + incl[k] - sum[k];
+        segpre[k] = tile_total;
+        tile_total += tot;
+    }
+    if (wid == 0) {
+        uint32_t prefix = 0;
+        if (tile == 0) {
+            if (lane == 0) st_store(&status[0], kStPre | tile_total);
+        } else {
+            if (lane == 0) st_store(&status[tile], kStAgg | tile_total);
+            int64_t top = (int64_t)tile - 1;
+            while (true) {
+                const int64_t p = top - lane;
+                const uint64_t st = p >= 0 ? st_load(&status[p]) : kStPre;
+                const uint64_t flag = st & kStMask;
+                const uint64_t pre = __ballot(flag == kStPre);
+                const uint64_t notready = __ballot(flag == 0);
+                const int first = pre ? __ffsll((long long)pre) - 1 : 64;
+                const uint64_t need = first >= 63 ? ~0ull : ((1ull << (first + 1)) - 1);
+                if (notready & need) continue;  // a predecessor has not published yet
+                uint32_t x = lane <= first ? (uint32_t)st : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+                prefix += x;
+                if (first < 64) break;
+                top -= 64;
+            }
+            if (lane == 0) st_store(&status[tile], kStPre | (prefix + tile_total));
+        }
+        if (lane == 0) s_prefix = prefix;
+    }
+    __syncthreads();
+    const uint32_t pfx = s_prefix;
+    if (total_out && threadIdx.x == 0 && base + kLbTile >= n) *total_out = pfx + tile_total;
+#pragma unroll
+    for (int k = 0; k < kLbSeg; k++) {
+        const int64_t idx = base + k * 1024 + 4 * threadIdx.x;
+        uint32_t run = pfx + segpre[k] + excl[k];
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) { o[j] = run; run += v[k][j]; }
+        if (idx + 3 < n) {
+            *(uint4*)(data + idx) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (idx + j < n) data[idx + j] = o[j];
+        }
+    }
+}
+
 }  // namespace
 
 int scan_u32_inplace(pcp_ctx* ctx, uint32_t* data, int64_t n, uint32_t* total_host) {
@@ -128,20 +234,18 @@ int scan_u32_inplace(pcp_ctx* ctx, uint32_t* data, int64_t n, uint32_t* total_ho
         if (total_host) *total_host = 0;
         return PCP_OK;
     }
-    int64_t tmp_elems = scan_tmp_elems(n);
+    const int64_t tiles = (n + kLbTile - 1) / kLbTile;
+    // scratch: [status (tiles u64)] [tile counter, total (u32)]
     void* tmp;
-    // +2 for the last value and the total
-    PCP_TRY(scratch(ctx, (tmp_elems + 2) * sizeof(uint32_t), &tmp));
-    uint32_t* t = (uint32_t*)tmp;
-    uint32_t* last = t + tmp_elems;
-    if (total_host)
-        PCP_HIP(ctx, hipMemcpyAsync(last, data + n - 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, ctx->stream));
-    PCP_TRY((scan_rec<uint32_t, uint32_t>(ctx, data, n, data, t, tmp_elems)));
+    PCP_TRY(scratch(ctx, (size_t)tiles * sizeof(uint64_t) + 16, &tmp));
+    uint64_t* status = (uint64_t*)tmp;
+    uint32_t* ctr = (uint32_t*)(status + tiles);
+    PCP_HIP(ctx, hipMemsetAsync(tmp, 0, (size_t)tiles * sizeof(uint64_t) + 16, ctx->stream));
+    hipLaunchKernelGGL(k_scan_lookback, dim3((unsigned)tiles), dim3(kLbBlock), 0, ctx->stream, data, n, status, ctr,
+                       ctr + 1);
+    PCP_LAUNCH_CHECK(ctx);
     if (total_host) {
-        hipLaunchKernelGGL((write_total<uint32_t>), dim3(1), dim3(1), 0, ctx->stream, data + n - 1,
-                           last, last + 1);
-        PCP_LAUNCH_CHECK(ctx);
-        PCP_HIP(ctx, hipMemcpyAsync(total_host, last + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        PCP_HIP(ctx, hipMemcpyAsync(total_host, ctr + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
         PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     }
     return PCP_OK;
