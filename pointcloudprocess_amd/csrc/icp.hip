@@ -300,7 +300,6 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;  // global wave id = fallback segment
     const int64_t nwaves = (int64_t)gridDim.x * kW;
     const int64_t nch = (a.nq + 63) / 64;
-    const bool reject_certified = a.r2 <= a.cert2;
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
     uint32_t fbn = 0;  // wave-uniform count of this wave's fallback entries
 
@@ -314,11 +313,20 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         Best b{a.r2, 0x7fffffff, ~0u, 0.f, 0.f, 0.f};
         float qx = 0.f, qy = 0.f, qz = 0.f;
         int bx = 0, by = 0, bz = 0;
+        float cert2 = a.cert2;
         if (valid) {
             xform(a, qraw, qx, qy, qz);
-            bx = (int)floorf(cell_f<float>(g, qx, 0) - a.rho);
-            by = (int)floorf(cell_f<float>(g, qy, 1) - a.rho);
-            bz = (int)floorf(cell_f<float>(g, qz, 2) - a.rho);
+            const float fx = cell_f<float>(g, qx, 0), fy = cell_f<float>(g, qy, 1), fz = cell_f<float>(g, qz, 2);
+            bx = (int)floorf(fx - a.rho);
+            by = (int)floorf(fy - a.rho);
+            bz = (int)floorf(fz - a.rho);
+            // this query's certified radius: its distance to the nearest face of the 2x2x2
+            // block (>= 0.5 cell, the worst case a.cert2 is built from), less the margin
+            const float m = fminf(fminf(fminf(fx - (float)bx, (float)(bx + 2) - fx),
+                                        fminf(fy - (float)by, (float)(by + 2) - fy)),
+                                  fminf(fz - (float)bz, (float)(bz + 2) - fz)) - a.mc;
+            const float rr = m * g.hf;
+            cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
         }
         if (valid && !(a.dbg & kDbgNoScan)) {
             // the 4 x-rows of the octant: all 8 row bounds are loaded at once, then the rows
@@ -340,7 +348,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         }
         // ---- epilogue: results, fallback list, accumulators
         const bool found = b.bj != 0x7fffffff;
-        const bool done = valid && ((found && b.bd <= a.cert2) || (!found && reject_certified) ||
+        const bool done = valid && ((found && b.bd <= cert2) || (!found && a.r2 <= cert2) ||
                                     (a.dbg & kDbgNoFallback));
         if (valid) {  // provisional for fallback queries (an upper bound), final otherwise
             a.win[i] = found ? b.bj : -1;

@@ -48,10 +48,14 @@ def test_correspondence_bit_exact(ctx, cell):
         eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
         gacc = acc.cpu().numpy()
         assert gacc[0] == eacc[0]
-        # GPU: per-lane fp32 sums of products centred on a per-wave point, then fp64;
-        # oracle: sequential fp64.  [23] is the fallback count (diagnostic).
+        # GPU: per-chunk fp32 sums of coordinates/products centred on the chunk's first
+        # query, un-centred in fp64; oracle: sequential fp64.  The fp32 centred sums carry
+        # ~64 * extent * 6e-8 absolute error per chunk, times the centre (|c| ~ scene size)
+        # on un-centring: <= 1e-8 of the largest accumulator (measured <= 2e-9), i.e. ~1e-8
+        # rad on the solved rotation, far inside the 1e-5 pose tolerance.  [23] is the
+        # fallback count (diagnostic).
         scale = np.abs(eacc[:23]).max()
-        assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-9 * scale)
+        assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * scale)
 
 
 def test_ties_lattice(ctx):
