@@ -81,11 +81,17 @@ __device__ __forceinline__ void xform(const IcpArgs& a, const float4 q, float& x
 }
 
 // running 1-NN: best d2, its target index (tie order) and its position in the scanned array
+#ifndef PCP_SCAN_UNROLL
+#define PCP_SCAN_UNROLL 4
+#endif
+#ifndef PCP_TRACK_BEST
+#define PCP_TRACK_BEST 0
+#endif
 struct Best {
     float bd;
     int bj;
     uint32_t bk;
-    float px, py, pz;  // filled by fetch() once the scan is over
+    float px, py, pz;  // filled by fetch() once the scan is over (or tracked, PCP_TRACK_BEST)
     __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t k) {
         const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
         const float d2 = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx));
@@ -95,6 +101,11 @@ struct Best {
         bd = take ? d2 : bd;
         bj = take ? id : bj;
         bk = take ? k : bk;
+#if PCP_TRACK_BEST
+        px = take ? p.x : px;
+        py = take ? p.y : py;
+        pz = take ? p.z : pz;
+#endif
     }
     // candidates [s, e) of `pts` (LDS or global); loads issued 4 at a time so the memory
     // latency of a candidate is not serialised behind the previous update
@@ -111,21 +122,26 @@ struct Best {
         for (; k < e; k++) consider(qx, qy, qz, pts[k], k);
     }
     // rows r = 0..3 ([rs[r], rs[r] + rn[r])) scanned as one concatenated list, 4 loads in flight
-    template <typename P>
-    __device__ __forceinline__ void scan_rows(const P* pts, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
+    template <typename P, int NR>
+    __device__ __forceinline__ void scan_rows(const P* pts, const uint32_t (&rs)[NR], const uint32_t (&rn)[NR],
                                               float qx, float qy, float qz) {
-        const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
+        static_assert(NR == 3 || NR == 4, "3 or 4 rows");
+        const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = NR == 4 ? c3 + rn[NR - 1] : c3;
         auto addr = [&](uint32_t v) {
-            return v < c1 ? rs[0] + v : (v < c2 ? rs[1] + (v - c1) : (v < c3 ? rs[2] + (v - c2) : rs[3] + (v - c3)));
+            return v < c1 ? rs[0] + v
+                          : (v < c2 ? rs[1] + (v - c1) : ((NR == 3 || v < c3) ? rs[2] + (v - c2) : rs[NR - 1] + (v - c3)));
         };
         uint32_t v = 0;
-        for (; v + 4 <= L; v += 4) {
-            const uint32_t k0 = addr(v), k1 = addr(v + 1), k2 = addr(v + 2), k3 = addr(v + 3);
-            const float4 p0 = pts[k0], p1 = pts[k1], p2 = pts[k2], p3 = pts[k3];
-            consider(qx, qy, qz, p0, k0);
-            consider(qx, qy, qz, p1, k1);
-            consider(qx, qy, qz, p2, k2);
-            consider(qx, qy, qz, p3, k3);
+        constexpr int U = PCP_SCAN_UNROLL;
+        for (; v + U <= L; v += U) {
+            uint32_t k[U];
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) k[u] = addr(v + u);
+#pragma unroll
+            for (int u = 0; u < U; u++) p[u] = pts[k[u]];
+#pragma unroll
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, p[u], k[u]);
         }
         for (; v < L; v++) {
             const uint32_t k = addr(v);
@@ -363,7 +379,9 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         }
         fbn += (uint32_t)__popcll(fbm);
         const bool acc_ok = done && found && !(a.dbg & kDbgNoAccum);
+#if !PCP_TRACK_BEST
         if (acc_ok) b.fetch(a.tp);
+#endif
         chunk_accumulate(acc_ok, qx, qy, qz, b, s_acc[wid], lane);
     }
     if (lane == 0) a.fb_count[gw] = fbn;
@@ -395,7 +413,39 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_ring(IcpArgs a
                 b.bd = a.wd2[i];
                 b.bj = a.win[i];
             }
-            box_search(a.g, a.tp, qx, qy, qz, a.mc, b);
+            bool done = false;
+            if (!a.ring_all) {
+                // stage 2: the 3x3x3 cells around the query, as 3 planes of 3 x-rows scanned
+                // like the octant pass; certifies any winner within the distance to the
+                // block's faces (>= 1 cell).  Only what is left goes to the general search.
+                const GridDesc& g = a.g;
+                const float fx = cell_f<float>(g, qx, 0), fy = cell_f<float>(g, qy, 1), fz = cell_f<float>(g, qz, 2);
+                const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
+                const int xa = max(cx - 1, 0), xb = min(cx + 1, g.n[0] - 1);
+                if (xa <= xb) {
+                    for (int dz = -1; dz <= 1; dz++) {
+                        const int z = cz + dz;
+                        uint32_t rs[3], rn[3];
+#pragma unroll
+                        for (int r = 0; r < 3; r++) {
+                            const int y = cy - 1 + r;
+                            const bool in = y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
+                            const int64_t cc = in ? dense_id(g, xa, y, z) : 0;
+                            rs[r] = in ? g.cstart[cc] : 0u;
+                            rn[r] = in ? g.cstart[cc + (xb - xa + 1)] - rs[r] : 0u;
+                        }
+                        b.scan_rows(a.tp, rs, rn, qx, qy, qz);
+                    }
+                }
+                const float m = fminf(fminf(fminf(fx - (float)(cx - 1), (float)(cx + 2) - fx),
+                                            fminf(fy - (float)(cy - 1), (float)(cy + 2) - fy)),
+                                      fminf(fz - (float)(cz - 1), (float)(cz + 2) - fz)) - a.mc;
+                const float rr = m * g.hf;
+                const float c2 = rr * rr * (1.f - 2e-5f);
+                const bool found = b.bj != 0x7fffffff;
+                done = (found && b.bd <= c2) || (!found && a.r2 <= c2);
+            }
+            if (!done) box_search(a.g, a.tp, qx, qy, qz, a.mc, b);
             const bool ok = b.bj != 0x7fffffff;
             a.win[i] = ok ? b.bj : -1;
             a.wd2[i] = ok ? b.bd : INFINITY;
