@@ -107,8 +107,8 @@ __device__ __forceinline__ void group_min(double& d, int& j) {
 }
 
 // QB blocks of 16 queries per wave; L = per-(row, class) list length.
-template <int L, int QB>
-__global__ __launch_bounds__(kBlock, 2) void k_bf_mfma(BfArgs a) {
+template <int L, int QB, int W>
+__global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
     __shared__ float4 tile[kTile];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -132,12 +132,37 @@ __global__ __launch_bounds__(kBlock, 2) void k_bf_mfma(BfArgs a) {
     }
     float ls[QB][4][L];
     int lt[QB][4][L];
+    // thr = min(class L-th score, th): the score filter.  th = theta + 2E is a row-global
+    // bound: theta = k-th smallest of the 16 class bests (k distinct targets score <= theta),
+    // so a target scoring above theta + 2E has an exact d2 above theirs -- and above the
+    // k-th candidate's -- and can be dropped without weakening the certification.
+    // Both bounds only decrease, so thr is maintained as a running min without storing th.
+    float thr[QB][4];
 #pragma unroll
     for (int b = 0; b < QB; b++)
 #pragma unroll
-        for (int r = 0; r < 4; r++)
+        for (int r = 0; r < 4; r++) {
+            thr[b][r] = INFINITY;
 #pragma unroll
             for (int i = 0; i < L; i++) { ls[b][r][i] = INFINITY; lt[b][r][i] = -1; }
+        }
+    // wave-uniform fp32 score error bound E (largest |q| of the wave's queries)
+    float ew;
+    {
+        double q2 = 0.0;
+#pragma unroll
+        for (int b = 0; b < QB; b++) {
+            const int64_t qi = qbase + b * 16 + cls;
+            if (qi < a.nq && grp == 0) {
+                const double* qp = dptr(a.q, a.qstride, qi);
+                if (finite3(qp[0], qp[1], qp[2])) q2 = fmax(q2, qp[0] * qp[0] + qp[1] * qp[1] + qp[2] * qp[2]);
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) q2 = fmax(q2, __shfl_xor(q2, o, 64));
+        const double qn = sqrt(q2);
+        ew = (float)(a.E2 * (a.pmax + qn) * (a.pmax + qn) * 1.001);
+    }
+    const bool use_theta = a.kk <= 16;
 
     const int64_t ntiles = (a.nt + kTile - 1) / kTile;
     float4 pre[kPerThread];
@@ -157,22 +182,66 @@ __global__ __launch_bounds__(kBlock, 2) void k_bf_mfma(BfArgs a) {
         if (tt + 1 < ntiles) fetch((tt + 1) * kTile);
         const int tb = (int)(tt * kTile);
         const float* tf = (const float*)tile;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        // software pipeline: the MFMAs of sub-tile s+1 are in flight while the scores of
+        // sub-tile s are tested, so the matrix pipe never waits on the selection VALU work
+        f32x4 cn[QB];
+        float bnext;  // B fragment of sub-tile s+2, read from LDS a step ahead of its MFMA
+        {
+            const float bf0 = tf[cls * 4 + grp];
+            bnext = tf[(16 + cls) * 4 + grp];
+#pragma unroll
+            for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf0, z, 0, 0, 0);
+        }
 #pragma unroll 2
         for (int sub = 0; sub < kTile / 16; sub++) {
-            const float bfrag = tf[(sub * 16 + cls) * 4 + grp];
             f32x4 c[QB];
 #pragma unroll
-            for (int b = 0; b < QB; b++) {
-                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-                c[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfrag, z, 0, 0, 0);
+            for (int b = 0; b < QB; b++) c[b] = cn[b];
+            if (sub + 1 < kTile / 16) {
+                const float bfrag = bnext;
+                if (sub + 2 < kTile / 16) bnext = tf[((sub + 2) * 16 + cls) * 4 + grp];
+#pragma unroll
+                for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfrag, z, 0, 0, 0);
             }
-            const int tidx = tb + sub * 16 + cls;
+            // one combined test per step; the insertion path runs only when a lane has a hit
+            bool hit = false;
+#pragma unroll
+            for (int b = 0; b < QB; b++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) hit |= c[b][r] < thr[b][r];
+            if (hit) {
+                const int tidx = tb + sub * 16 + cls;
+#pragma unroll
+                for (int b = 0; b < QB; b++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float x = c[b][r];
+                        if (x < thr[b][r]) {
+                            list_insert<L>(ls[b][r], lt[b][r], x, tidx);
+                            thr[b][r] = fminf(ls[b][r][L - 1], thr[b][r]);
+                        }
+                    }
+            }
+        }
+        // refresh theta after tiles 1, 2, 4, 8, ... (rank of each class best in its group)
+        if (use_theta && ((tt + 1) & tt) == 0) {
 #pragma unroll
             for (int b = 0; b < QB; b++)
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                    const float x = c[b][r];
-                    if (x < ls[b][r][L - 1]) list_insert<L>(ls[b][r], lt[b][r], x, tidx);
+                    const float v = ls[b][r][0];
+                    int rank = 0;
+#pragma unroll
+                    for (int j = 0; j < 16; j++) {
+                        const float vj = __shfl(v, (lane & ~15) | j, 64);
+                        rank += (vj < v || (vj == v && j < cls)) ? 1 : 0;
+                    }
+                    float cand = rank == a.kk - 1 ? v : INFINITY;
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) cand = fminf(cand, __shfl_xor(cand, o, 64));
+                    const float t2 = cand + 2.f * ew;
+                    if (cand != INFINITY) thr[b][r] = fminf(thr[b][r], t2 + fabsf(t2) * 1e-6f);
                 }
         }
     }
@@ -248,19 +317,21 @@ __global__ __launch_bounds__(kBlock, 2) void k_bf_mfma(BfArgs a) {
         }
 }
 
-// exact fp64 scan for uncertified queries: one wave per query, per-lane register top-k,
-// then a wave merge of the 64 sorted lists
+// exact fp64 scan for uncertified queries: one 256-thread block per query, per-lane
+// register top-k, then a block merge (k rounds: wave minimum, then across the 4 waves)
 template <int K>
 __global__ __launch_bounds__(256) void k_bf_fallback(BfArgs a, const int32_t* fb, const uint32_t* fb_count) {
-    const int lane = threadIdx.x & 63;
+    __shared__ double sd[4];
+    __shared__ int sj[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t nfb = *fb_count;
-    for (uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6); w < nfb; w += gridDim.x * 4) {
+    for (uint32_t w = blockIdx.x; w < nfb; w += gridDim.x) {
         const int64_t qi = fb[w];
         const double* qp = dptr(a.q, a.qstride, qi);
         const double qx = qp[0], qy = qp[1], qz = qp[2];
         TopK<K> top;
         top.init(a.kk);
-        for (int64_t t = lane; t < a.nt; t += 64) {
+        for (int64_t t = threadIdx.x; t < a.nt; t += 256) {
             const double* p = dptr(a.t, a.tstride, t);
             if (!finite3(p[0], p[1], p[2])) continue;
             top.push(l2_simple(qx, qy, qz, make_double4(p[0], p[1], p[2], 0.0)), (int)t);
@@ -275,8 +346,16 @@ __global__ __launch_bounds__(256) void k_bf_fallback(BfArgs a, const int32_t* fb
                 const int oj = __shfl_xor(mj, o, 64);
                 if (lex_less(od, oj, md, mj)) { md = od; mj = oj; }
             }
+            if (lane == 0) { sd[wid] = md; sj[wid] = mj; }
+            __syncthreads();
+            md = sd[0];
+            mj = sj[0];
+#pragma unroll
+            for (int v = 1; v < 4; v++)
+                if (lex_less(sd[v], sj[v], md, mj)) { md = sd[v]; mj = sj[v]; }
+            __syncthreads();
             if (top.best_j() == mj && mj != INT_MAX) top.pop_best();
-            if (lane == 0) {
+            if (threadIdx.x == 0) {
                 a.oidx[qi * a.k + rr] = mj == INT_MAX ? -1 : mj;
                 a.od2[qi * a.k + rr] = mj == INT_MAX ? INFINITY : md;
             }
@@ -336,13 +415,13 @@ int pcp_knn_bruteforce(pcp_ctx* ctx, const double* t, size_t tstride, int64_t nt
         if (!rc) {
             if (k <= 8) {
                 const int64_t per = kWaves * 16 * 2;
-                hipLaunchKernelGGL((k_bf_mfma<6, 2>), dim3((unsigned)((nq + per - 1) / per)), dim3(kBlock), 0, st, a);
+                hipLaunchKernelGGL((k_bf_mfma<6, 2, 3>), dim3((unsigned)((nq + per - 1) / per)), dim3(kBlock), 0, st, a);
             } else if (k <= 16) {
                 const int64_t per = kWaves * 16;
-                hipLaunchKernelGGL((k_bf_mfma<10, 1>), dim3((unsigned)((nq + per - 1) / per)), dim3(kBlock), 0, st, a);
+                hipLaunchKernelGGL((k_bf_mfma<10, 1, 3>), dim3((unsigned)((nq + per - 1) / per)), dim3(kBlock), 0, st, a);
             } else {
                 const int64_t per = kWaves * 16;
-                hipLaunchKernelGGL((k_bf_mfma<16, 1>), dim3((unsigned)((nq + per - 1) / per)), dim3(kBlock), 0, st, a);
+                hipLaunchKernelGGL((k_bf_mfma<16, 1, 2>), dim3((unsigned)((nq + per - 1) / per)), dim3(kBlock), 0, st, a);
             }
             const unsigned fbg = 1024;
             if (k <= 8) hipLaunchKernelGGL(k_bf_fallback<8>, dim3(fbg), dim3(256), 0, st, a, fb, fbc);
