@@ -26,8 +26,21 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 4;              // waves per block
+// k <= 8 configuration: list length per (row, class), query blocks per wave, waves/SIMD
+#ifndef PCP_BF_L8
+#define PCP_BF_L8 6
+#endif
+#ifndef PCP_BF_QB8
+#define PCP_BF_QB8 1
+#endif
+#ifndef PCP_BF_W8
+#define PCP_BF_W8 4
+#endif
 constexpr int kBlock = 64 * kWaves;
-constexpr int kTile = 512;             // targets staged in LDS per step
+#ifndef PCP_BF_TILE
+#define PCP_BF_TILE 1024
+#endif
+constexpr int kTile = PCP_BF_TILE;     // targets staged in LDS per step
 constexpr int kPerThread = kTile / kBlock;
 
 __device__ __forceinline__ const double* dptr(const double* base, size_t stride, int64_t i) {
@@ -414,8 +427,9 @@ int pcp_knn_bruteforce(pcp_ctx* ctx, const double* t, size_t tstride, int64_t nt
         if (hipMemsetAsync(fbc, 0, sizeof(uint32_t), st) != hipSuccess) rc = set_error(ctx, PCP_ERR_HIP, "memset");
         if (!rc) {
             if (k <= 8) {
-                const int64_t per = kWaves * 16 * 2;
-                hipLaunchKernelGGL((k_bf_mfma<6, 2, 3>), dim3((unsigned)((nq + per - 1) / per)), dim3(kBlock), 0, st, a);
+                const int64_t per = kWaves * 16 * PCP_BF_QB8;
+                hipLaunchKernelGGL((k_bf_mfma<PCP_BF_L8, PCP_BF_QB8, PCP_BF_W8>), dim3((unsigned)((nq + per - 1) / per)),
+                                   dim3(kBlock), 0, st, a);
             } else if (k <= 16) {
                 const int64_t per = kWaves * 16;
                 hipLaunchKernelGGL((k_bf_mfma<10, 1, 3>), dim3((unsigned)((nq + per - 1) / per)), dim3(kBlock), 0, st, a);
