@@ -131,14 +131,16 @@ __global__ __launch_bounds__(kB) void k_radius_count(GridDesc g, const double4* 
     }
 }
 
-// K4 fill pass: the query's CSR row is kept sorted by (d2, j) by insertion (it holds the
-// m = min(count, max_nn) best found so far; m was fixed by the count pass).
+// K4 fill pass.  A row that max_nn does not truncate (m < cap) receives its points in
+// visiting order (k_sort_rows orders it afterwards); a possibly truncated row (m == cap)
+// keeps the m best found so far sorted by (d2, j) by insertion.
 struct FillVisitor {
     const double4* pts;
     double qx, qy, qz, r2, b;
     int32_t* ri;
     double* rd;
     int64_t m, filled;
+    bool append;
     __device__ double bound() const { return b; }
     __device__ void visit(uint32_t s, uint32_t e) {
         for (uint32_t t = s; t < e; t++) {
@@ -146,6 +148,10 @@ struct FillVisitor {
             const double d = l2_simple(qx, qy, qz, p);
             if (!(d < r2)) continue;
             const int j = (int)p.w;
+            if (append) {
+                if (filled < m) { rd[filled] = d; ri[filled] = j; filled++; }
+                continue;
+            }
             int64_t pos;
             if (filled < m) pos = filled++;
             else if (lex_less(d, j, rd[m - 1], ri[m - 1])) pos = m - 1;
@@ -161,24 +167,93 @@ struct FillVisitor {
     }
 };
 
+// Orders each appended CSR row by (d2, j) and maps j -> caller index.  One wave per row:
+// rows up to kSortMax elements are bitonic-sorted in the wave's LDS slice; longer rows
+// (rare) are insertion-sorted by lane 0 in place.
+constexpr int kSortMax = 1024;
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(256) void k_sort_rows(const int64_t* off, int64_t nq, uint32_t cap, int32_t* ri,
+                                                   double* rd, const int32_t* mapping, int identity) {
+    __shared__ double sd[4][kSortMax];
+    __shared__ int sj[4][kSortMax];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < nq; row += nw) {
+        const int64_t o = off[row], m = off[row + 1] - o;
+        if (m <= 0 || (uint64_t)m >= cap) {  // empty, or an insertion-sorted (truncatable) row
+            if (!identity)
+                for (int64_t t = lane; t < m; t += 64) ri[o + t] = mapping[ri[o + t]];
+            continue;
+        }
+        if (m > kSortMax) {
+            if (lane == 0) {
+                for (int64_t a = 1; a < m; a++) {
+                    const double d = rd[o + a];
+                    const int j = ri[o + a];
+                    int64_t p = a;
+                    while (p > 0 && lex_less(d, j, rd[o + p - 1], ri[o + p - 1])) {
+                        rd[o + p] = rd[o + p - 1];
+                        ri[o + p] = ri[o + p - 1];
+                        p--;
+                    }
+                    rd[o + p] = d;
+                    ri[o + p] = j;
+                }
+            }
+            wave_lds_sync();
+            if (!identity)
+                for (int64_t t = lane; t < m; t += 64) ri[o + t] = mapping[ri[o + t]];
+            continue;
+        }
+        int N = 1;
+        while (N < m) N <<= 1;
+        for (int t = lane; t < N; t += 64) {
+            sd[w][t] = t < m ? rd[o + t] : INFINITY;
+            sj[w][t] = t < m ? ri[o + t] : INT_MAX;
+        }
+        wave_lds_sync();
+        for (int k = 2; k <= N; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int t = lane; t < N; t += 64) {
+                    const int u = t ^ j;
+                    if (u > t) {
+                        const double a = sd[w][t], b = sd[w][u];
+                        const int ja = sj[w][t], jb = sj[w][u];
+                        const bool up = (t & k) == 0;
+                        if (up == lex_less(b, jb, a, ja)) {
+                            sd[w][t] = b; sd[w][u] = a;
+                            sj[w][t] = jb; sj[w][u] = ja;
+                        }
+                    }
+                }
+                wave_lds_sync();
+            }
+        for (int t = lane; t < m; t += 64) {
+            rd[o + t] = sd[w][t];
+            ri[o + t] = identity ? sj[w][t] : mapping[sj[w][t]];
+        }
+        wave_lds_sync();
+    }
+}
+
 template <bool FAR>
-__global__ __launch_bounds__(kB) void k_radius_fill(GridDesc g, const double4* pts, const int32_t* mapping,
-                                                    int identity, const double* q, size_t qstride, int64_t nq,
-                                                    double r2, double mc, const int64_t* off, int32_t* oidx,
-                                                    double* od2, FarList far) {
+__global__ __launch_bounds__(kB) void k_radius_fill(GridDesc g, const double4* pts, const double* q, size_t qstride,
+                                                    int64_t nq, double r2, uint32_t cap, double mc,
+                                                    const int64_t* off, int32_t* oidx, double* od2, FarList far) {
     const int64_t nw = work_count<FAR>(far, nq);
     for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = work_item<FAR>(far, w);
         const int64_t o = off[i], m = off[i + 1] - o;
         if (m <= 0) continue;
         const double* qp = qptr(q, qstride, i);
-        FillVisitor v{pts, qp[0], qp[1], qp[2], r2, r2 * (1.0 + 1e-12), oidx + o, od2 + o, m, 0};
-        if (!ring_search<double, FillVisitor, FAR>(g, v.qx, v.qy, v.qz, mc, v)) {
+        FillVisitor v{pts, qp[0], qp[1], qp[2], r2, r2 * (1.0 + 1e-12), oidx + o, od2 + o, m, 0,
+                      (uint64_t)m < cap};
+        if (!ring_search<double, FillVisitor, FAR>(g, v.qx, v.qy, v.qz, mc, v))
             defer(far, i);  // the far pass rebuilds the row from scratch
-            continue;
-        }
-        if (!identity)
-            for (int64_t r = 0; r < v.filled; r++) v.ri[r] = mapping[v.ri[r]];
     }
 }
 
@@ -597,17 +672,20 @@ int pcp_radius_fill(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t q
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     const double4* pts = (const double4*)ix->pts;
     const double mc = cell_margin64(ix->g);
+    const uint32_t cap = radius_cap(ix, max_nn);
     if (radius_needs_far(ix, radius)) {
-        hipLaunchKernelGGL(k_radius_fill<true>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,
-                           ix->identity, q, qstride, nq, radius * radius, mc, off, oidx, od2, FarList{nullptr, nullptr});
+        hipLaunchKernelGGL(k_radius_fill<true>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, q, qstride,
+                           nq, radius * radius, cap, mc, off, oidx, od2, FarList{nullptr, nullptr});
     } else {
         FarBuf fb;
         PCP_TRY(fb.alloc(ctx, nq));
-        hipLaunchKernelGGL(k_radius_fill<false>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts,
-                           ix->mapping, ix->identity, q, qstride, nq, radius * radius, mc, off, oidx, od2, fb.f);
-        hipLaunchKernelGGL(k_radius_fill<true>, dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,
-                           ix->identity, q, qstride, nq, radius * radius, mc, off, oidx, od2, fb.f);
+        hipLaunchKernelGGL(k_radius_fill<false>, dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, q,
+                           qstride, nq, radius * radius, cap, mc, off, oidx, od2, fb.f);
+        hipLaunchKernelGGL(k_radius_fill<true>, dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, q, qstride,
+                           nq, radius * radius, cap, mc, off, oidx, od2, fb.f);
     }
+    hipLaunchKernelGGL(k_sort_rows, dim3(grid_for((nq + 3) / 4, 1, 1 << 16)), dim3(256), 0, ctx->stream, off, nq, cap,
+                       oidx, od2, ix->mapping, ix->identity);
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }

@@ -243,3 +243,20 @@ def test_plane_fit_segments_and_radius_normals(ctx):
         lib.ora_plane_h_points(nb.ctypes.data, len(ei), e.ctypes.data)
         ev = np.array([e[f][0] for f in ("normal_x", "normal_y", "normal_z", "min_value", "curvature", "distance")])
         assert np.array_equal(g[i], ev.astype(np.float32), equal_nan=True), f"point {i}"
+
+
+def test_radius_long_rows(ctx):
+    """Rows longer than the LDS bitonic limit (1024) take the in-place path; max_nn keeps
+    the insertion path; both stay bit-exact."""
+    from pointcloudprocess_amd import ops
+    xyz = _cloud(3000, 91, half=0.5)
+    q = _cloud(40, 92, half=0.5)
+    ix = ops.GridIndex(ctx, _dev(ctx, xyz))
+    t = ora.KdTree(xyz)
+    for r, mx in ((2.0, 0), (0.3, 0), (2.0, 2999), (2.0, 100)):
+        offs, gi, gd = ops.radius(ix, _dev(ctx, q), r, mx)
+        offs, gi, gd = offs.cpu().numpy(), gi.cpu().numpy(), gd.cpu().numpy()
+        for i in range(len(q)):
+            ei, ed = t.radius(q[i], r, mx)
+            s, e = offs[i], offs[i + 1]
+            assert np.array_equal(gi[s:e], ei) and np.array_equal(gd[s:e], ed), (r, mx, i)

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs (counter_collection.csv) per kernel.
+
+FETCH_SIZE and WRITE_SIZE are in KB.  gfx950 correction (MI355X_MICROARCH.md, HBM section):
+FETCH_SIZE reports half the bytes of wide (16 B/lane) reads -> x2; WRITE_SIZE is exact.
+  python tools/pmc_summary.py <fetch_dir> <write_dir> [kernel-substring ...]
+"""
+import collections
+import csv
+import hashlib
+import json
+import os
+import re
+import sys
+
+
+def per_kernel(path, counter):
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))):
+        if r["Counter_Name"] == counter:
+            m = re.search(r"(\w+)(<[^(]*>)?\(", r["Kernel_Name"].replace("(anonymous namespace)", "anon"))
+            name = m.group(1) if m else r["Kernel_Name"]
+            vals[name].append(float(r["Counter_Value"]) * 1024.0)
+    return vals
+
+
+def main():
+    fdir, wdir = sys.argv[1], sys.argv[2]
+    keys = sys.argv[3:] or ["k_icp_octant", "k_icp_ring"]
+    f, w = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
+    out = {"source": f"{fdir}, {wdir}", "fetch_correction": 2.0, "kernels": {}}
+    for k in keys:
+        if k in f:
+            fb = [2.0 * v for v in f[k]]
+            wb = w.get(k, [])
+            out["kernels"][k] = {"launches": len(fb), "fetch_bytes_avg": sum(fb) / len(fb),
+                                 "write_bytes_avg": sum(wb) / len(wb) if wb else None}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "pointcloudprocess_amd", "csrc", "icp.hip")
+    out["icp_hip_sha1"] = hashlib.sha1(open(src, "rb").read()).hexdigest()
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
