@@ -1,12 +1,15 @@
 // Uniform-grid index build (replaces KdTreeFLANN::setInputCloud, kd_tree.h:772-798,
 // and the trimesh2 KDtree constructions at point_cloud_helper.cpp:110-111).
 //
-// Build = compaction of finite points (index_mapping_) -> bbox -> brick marking ->
-// brick-slot scan -> per-cell counting (atomics) -> cell-start scan -> scatter into
-// cell order.  All passes are HBM streams over the points; the only host round trips
-// are the bbox (to size the brick table) and the slot count.
+// Build = compaction of finite points (index_mapping_) -> bbox -> brick marking (sparse
+// mode) -> per-point cell keys -> stable device radix sort of (cell, point) -> per-cell
+// counts from the sorted runs -> cell-start scan -> gather into cell order.  Within a cell
+// points keep input order, so the layout is deterministic.  All passes are HBM streams;
+// the only host round trips are the bbox (to size the tables) and the slot count.
 #include <cmath>
 #include <vector>
+
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "grid.hpp"
 
@@ -127,46 +130,6 @@ __global__ void k_brick_final(int32_t* brick, int64_t nb, const uint32_t* bits) 
     }
 }
 
-// per-cell counts and each point's arrival rank; `mark` (dense mode) also flags the
-// point's brick for the two-level search's occupancy table
-template <typename T>
-__global__ void k_count(GridDesc g, const T* cxyz, int64_t n, uint32_t* count, uint32_t* rank, int32_t* mark) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int cx, cy, cz;
-        cell_of_point<T>(g, cxyz + 3 * i, cx, cy, cz);
-        rank[i] = atomicAdd(&count[cell_id(g, cx, cy, cz)], 1u);
-        if (mark) mark[brick_of(g, cx, cy, cz)] = 1;
-    }
-}
-
-// (x, tie) key of a sorted point: tie = caller index bits (fp32) or internal j (fp64)
-__device__ __forceinline__ bool key_less(const float4& a, const float4& b) {
-    return a.x < b.x || (a.x == b.x && __float_as_int(a.w) < __float_as_int(b.w));
-}
-__device__ __forceinline__ bool key_less(const double4& a, const double4& b) {
-    return a.x < b.x || (a.x == b.x && a.w < b.w);
-}
-
-// rank sort inside each cell: position = cell start + #(points of the cell with a smaller key)
-template <typename T>
-__global__ void k_cell_sort(GridDesc g, const typename Real<T>::V4* pts, const int32_t* sj, int64_t n,
-                            typename Real<T>::V4* out, int32_t* sj_out) {
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
-         k += (int64_t)gridDim.x * blockDim.x) {
-        const typename Real<T>::V4 p = pts[k];
-        const T c3[3] = {p.x, p.y, p.z};
-        int cx, cy, cz;
-        cell_of_point<T>(g, c3, cx, cy, cz);
-        const int64_t c = cell_id(g, cx, cy, cz);
-        const uint32_t s = g.cstart[c], e = g.cstart[c + 1];
-        uint32_t r = 0;
-        for (uint32_t j = s; j < e; j++) r += key_less(pts[j], p) ? 1u : 0u;
-        out[s + r] = p;
-        sj_out[s + r] = sj[k];
-    }
-}
-
 __global__ void k_nonempty(const uint32_t* count, int64_t ncells, unsigned long long* out) {
     unsigned long long local = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ncells;
@@ -176,22 +139,48 @@ __global__ void k_nonempty(const uint32_t* count, int64_t ncells, unsigned long 
     if ((threadIdx.x & 63) == 0) atomicAdd(out, local);
 }
 
+// Radix-sort build: key = cell id (cstart index) of each compacted point, value = its
+// internal index.  A stable LSD sort then yields cell order with ties in input order
+// (deterministic); dense mode also flags the point's brick for the two-level search.
 template <typename T>
-__global__ void k_scatter(GridDesc g, const T* cxyz, int64_t n, const uint32_t* rank,
-                          const int32_t* mapping, typename Real<T>::V4* pts, int32_t* sorted_j,
-                          int is_f64) {
+__global__ void k_cell_keys(GridDesc g, const T* cxyz, int64_t n, uint32_t* key, uint32_t* val, int32_t* mark) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         int cx, cy, cz;
-        const T* p = cxyz + 3 * i;
-        cell_of_point<T>(g, p, cx, cy, cz);
-        uint32_t dst = g.cstart[cell_id(g, cx, cy, cz)] + rank[i];
+        cell_of_point<T>(g, cxyz + 3 * i, cx, cy, cz);
+        key[i] = (uint32_t)cell_id(g, cx, cy, cz);
+        val[i] = (uint32_t)i;
+        if (mark) mark[brick_of(g, cx, cy, cz)] = 1;
+    }
+}
+
+// per-cell counts from the runs of the sorted keys (count[] zeroed): run starts record
+// their position, run ends turn it into the run length
+__global__ void k_run_start(const uint32_t* key, int64_t n, uint32_t* count) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x)
+        if (k == 0 || key[k] != key[k - 1]) count[key[k]] = (uint32_t)k;
+}
+__global__ void k_run_end(const uint32_t* key, int64_t n, uint32_t* count) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x)
+        if (k == n - 1 || key[k] != key[k + 1]) count[key[k]] = (uint32_t)(k + 1) - count[key[k]];
+}
+
+// points in cell order: w = internal j (fp64, FLANN tie order) or caller index bits (fp32)
+template <typename T>
+__global__ void k_gather(const T* cxyz, const uint32_t* val, const int32_t* mapping, int64_t n,
+                         typename Real<T>::V4* pts, int32_t* sorted_j, int is_f64) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = val[k];
+        const T* p = cxyz + 3 * (int64_t)i;
         typename Real<T>::V4 v;
         v.x = p[0]; v.y = p[1]; v.z = p[2];
-        if (is_f64) v.w = (T)(double)i;                     // internal j (FLANN tie order)
-        else v.w = (T)__int_as_float(mapping[i]);            // caller index bits (ICP)
-        pts[dst] = v;
-        sorted_j[dst] = (int32_t)i;
+        if (is_f64) v.w = (T)(double)i;
+        else v.w = (T)__int_as_float(mapping[i]);
+        pts[k] = v;
+        sorted_j[k] = (int32_t)i;
     }
 }
 
@@ -302,8 +291,13 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         if (!(h > 0)) h = 1.0;
     }
     uint32_t* count = nullptr;
-    uint32_t* rank = nullptr;
-    if ((rc = dmalloc(ctx, &rank, n + 1))) { dfree(ctx, cxyz); return fail(rc); }
+    uint32_t* rank = nullptr;  // sort input values (point index)
+    uint32_t* skey = nullptr;  // sort input keys (cell id)
+    if ((rc = dmalloc(ctx, &rank, n + 1)) || (rc = dmalloc(ctx, &skey, n + 1))) {
+        dfree(ctx, rank);
+        dfree(ctx, cxyz);
+        return fail(rc);
+    }
     for (int attempt = 0; attempt < 3; attempt++) {
         GridDesc g{};
         while (!make_geometry(g, mn, mx, h, cap)) h *= 2.0;
@@ -338,14 +332,32 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         }
         if ((rc = dmalloc(ctx, &count, ncells + 1))) break;
         PCP_HIP(ctx, hipMemsetAsync(count, 0, (size_t)(ncells + 1) * sizeof(uint32_t), st));
-        if (n > 0)
-            hipLaunchKernelGGL(k_count<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, count, rank,
+        // ---- stable radix sort of (cell id, point) pairs, then per-cell counts from the runs
+        uint32_t* key1 = nullptr;
+        uint32_t* val1 = nullptr;
+        if (n > 0) {
+            if ((rc = dmalloc(ctx, &key1, n)) || (rc = dmalloc(ctx, &val1, n))) {
+                dfree(ctx, key1);
+                break;
+            }
+            hipLaunchKernelGGL(k_cell_keys<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, skey, rank,
                                g.dense ? ix->brick : nullptr);
+            unsigned bits = 1;
+            while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)ncells) bits++;
+            size_t tmp_bytes = 0;
+            PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u, bits, st));
+            void* tmp = nullptr;
+            if ((rc = dmalloc(ctx, (char**)&tmp, tmp_bytes))) { dfree(ctx, key1); dfree(ctx, val1); break; }
+            PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u, bits, st));
+            dfree(ctx, tmp);
+            hipLaunchKernelGGL(k_run_start, dim3(grid_for(n, kB)), dim3(kB), 0, st, (const uint32_t*)key1, n, count);
+            hipLaunchKernelGGL(k_run_end, dim3(grid_for(n, kB)), dim3(kB), 0, st, (const uint32_t*)key1, n, count);
+        }
         if (g.dense)
             hipLaunchKernelGGL(k_brick_flag, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks);
         if (auto_h && attempt < 2 && n > 0) {
             unsigned long long* d_ne;
-            if ((rc = dmalloc(ctx, &d_ne, 1))) break;
+            if ((rc = dmalloc(ctx, &d_ne, 1))) { dfree(ctx, key1); dfree(ctx, val1); break; }
             PCP_HIP(ctx, hipMemsetAsync(d_ne, 0, sizeof(unsigned long long), st));
             hipLaunchKernelGGL(k_nonempty, dim3(grid_for(ncells, kB, 4096)), dim3(kB), 0, st, count, ncells, d_ne);
             unsigned long long ne = 0;
@@ -353,34 +365,28 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             hipStreamSynchronize(st);
             dfree(ctx, d_ne);
             double occ = (double)n / std::max(1.0, (double)ne);
-            if (occ > 12.0) { h *= std::sqrt(4.0 / occ); continue; }   // surface-like data
-            if (occ < 1.5) { h *= std::cbrt(4.0 / occ); continue; }    // sparser than assumed
+            bool redo = false;
+            if (occ > 12.0) { h *= std::sqrt(4.0 / occ); redo = true; }   // surface-like data
+            else if (occ < 1.5) { h *= std::cbrt(4.0 / occ); redo = true; }  // sparser than assumed
+            if (redo) { dfree(ctx, key1); dfree(ctx, val1); continue; }
         }
-        // ---- cell starts + scatter
+        // ---- cell starts + points in cell order
         rc = scan_u32_inplace(ctx, count, ncells + 1, nullptr);
-        if (rc) break;
+        if (rc) { dfree(ctx, key1); dfree(ctx, val1); break; }
         g.cstart = count;
         ix->g = g;
         ix->cstart = count;
         count = nullptr;
         using V4 = typename Real<T>::V4;
-        if ((rc = dmalloc(ctx, (V4**)&ix->pts, n + 1)) || (rc = dmalloc(ctx, &ix->sorted_j, n + 1))) break;
-        if (n > 0) {
-            hipLaunchKernelGGL(k_scatter<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, rank,
-                               ix->mapping, (V4*)ix->pts, ix->sorted_j, is_f64);
-            // order each cell by (x, index): a dense-grid row of cells is then one x-sorted run
-            V4* pts2;
-            int32_t* sj2;
-            if ((rc = dmalloc(ctx, &pts2, n + 1))) break;
-            if ((rc = dmalloc(ctx, &sj2, n + 1))) { dfree(ctx, pts2); break; }
-            hipLaunchKernelGGL(k_cell_sort<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const V4*)ix->pts,
-                               (const int32_t*)ix->sorted_j, n, pts2, sj2);
-            PCP_HIP(ctx, hipStreamSynchronize(st));
-            dfree(ctx, ix->pts);
-            dfree(ctx, ix->sorted_j);
-            ix->pts = pts2;
-            ix->sorted_j = sj2;
+        if ((rc = dmalloc(ctx, (V4**)&ix->pts, n + 1)) || (rc = dmalloc(ctx, &ix->sorted_j, n + 1))) {
+            dfree(ctx, key1); dfree(ctx, val1);
+            break;
         }
+        if (n > 0)
+            hipLaunchKernelGGL(k_gather<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, cxyz, (const uint32_t*)val1,
+                               (const int32_t*)ix->mapping, n, (V4*)ix->pts, ix->sorted_j, is_f64);
+        dfree(ctx, key1);
+        dfree(ctx, val1);
         if (is_f64) {
             if ((rc = dmalloc(ctx, &ix->pos_of_j, n + 1))) break;
             if (n > 0)
@@ -391,6 +397,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     }
     dfree(ctx, count);
     dfree(ctx, rank);
+    dfree(ctx, skey);
     dfree(ctx, cxyz);
     if (rc) return fail(rc);
     PCP_HIP(ctx, hipGetLastError());

@@ -148,30 +148,6 @@ struct Best {
             consider(qx, qy, qz, pts[k], k);
         }
     }
-    // [s, e) sorted by x: binary search of q.x, then sweep outward while dx^2 <= bd.  A point
-    // beyond the stop has a larger |dx| and fp32 d2 >= dx*dx (monotone rounding), so it can
-    // neither beat nor tie the current best: the result equals a full scan of [s, e).
-    template <typename P>
-    __device__ __forceinline__ void sweep(const P* pts, uint32_t s, uint32_t e, float qx, float qy, float qz) {
-        uint32_t lo = s, hi = e;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pts[mid].x < qx) lo = mid + 1;
-            else hi = mid;
-        }
-        for (uint32_t k = lo; k < e; k++) {
-            const float4 p = pts[k];
-            const float dx = p.x - qx;
-            if (dx * dx > bd) break;
-            consider(qx, qy, qz, p, k);
-        }
-        for (uint32_t k = lo; k > s; k--) {
-            const float4 p = pts[k - 1];
-            const float dx = qx - p.x;
-            if (dx * dx > bd) break;
-            consider(qx, qy, qz, p, k - 1);
-        }
-    }
     template <typename P>
     __device__ __forceinline__ void fetch(const P* pts) {
         const float4 p = pts[bk];
@@ -211,11 +187,11 @@ __device__ __forceinline__ void box_search(const GridDesc& g, const float4* tp, 
             if (xa > xb) continue;
             if (g.dense) {
                 const int64_t c = dense_id(g, xa, y, z);
-                b.sweep(tp, g.cstart[c], g.cstart[c + (xb - xa + 1)], qx, qy, qz);
+                b.scan(tp, g.cstart[c], g.cstart[c + (xb - xa + 1)], qx, qy, qz);
             } else {
                 for (int x = xa; x <= xb; x++) {
                     uint32_t s, e;
-                    if (cell_range(g, x, y, z, s, e)) b.sweep(tp, s, e, qx, qy, qz);
+                    if (cell_range(g, x, y, z, s, e)) b.scan(tp, s, e, qx, qy, qz);
                 }
             }
         }
