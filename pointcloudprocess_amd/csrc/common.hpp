@@ -101,8 +101,6 @@ struct GridDesc {
     const uint32_t* cstart;   // dense: ncells + 1 ; sparse: 64*nslots + 1
 };
 
-int index_build_f32_bricks(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size,
-                           pcp_index** out);
 
 }  // namespace pcp
 

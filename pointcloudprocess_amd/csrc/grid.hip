@@ -130,13 +130,96 @@ __global__ void k_brick_final(int32_t* brick, int64_t nb, const uint32_t* bits) 
     }
 }
 
-__global__ void k_nonempty(const uint32_t* count, int64_t ncells, unsigned long long* out) {
-    unsigned long long local = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ncells;
-         i += (int64_t)gridDim.x * blockDim.x)
-        local += count[i] ? 1 : 0;
-    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(out, local);
+// Cell starts without a count array or a scan.  cstart[c] = first sorted position whose key
+// is >= c, c in [0, ncells].  The cells are cut into chunks of kChunk; k_chunk_lo finds each
+// chunk's first position from the run starts (a run start fills the chunk boundaries of the
+// key gap before it; p = n is a virtual run start closing the table) and counts the runs
+// (non-empty cells, for the auto cell-size check); k_cell_starts then resolves one chunk per
+// block in LDS (run starts scattered, suffix minimum) and writes it out coalesced.
+constexpr int kChunk = 4096;
+
+__global__ void k_chunk_lo(const uint32_t* key, int64_t n, int64_t nchunk, uint32_t* lo,
+                           unsigned long long* runs) {
+    __shared__ unsigned long long s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    unsigned long long c = 0;
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t kc = p < n ? (int64_t)key[p] : nchunk * kChunk;
+        const int64_t kp = p > 0 ? (int64_t)key[p - 1] : -1;
+        if (kc == kp) continue;
+        if (p < n) c++;
+        const int64_t b0 = kp < 0 ? 0 : kp / kChunk + 1;  // chunks whose first cell is in (kp, kc]
+        const int64_t b1 = min(kc / kChunk, nchunk);
+        for (int64_t b = b0; b <= b1; b++) lo[b] = (uint32_t)p;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_cnt) atomicAdd(runs, s_cnt);
+}
+
+__global__ void __launch_bounds__(256) k_cell_starts(const uint32_t* __restrict__ key, const uint32_t* __restrict__ lo,
+                                                     int64_t ncells1, uint32_t* __restrict__ cstart) {
+    constexpr int kPer = kChunk / 256;  // 16 cells per thread
+    __shared__ uint32_t s[kChunk];
+    __shared__ uint32_t s_wmin[4];
+    const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+    const uint32_t p0 = lo[blockIdx.x], p1 = lo[blockIdx.x + 1];
+    for (int i = threadIdx.x; i < kChunk; i += 256) s[i] = p1;
+    __syncthreads();
+    for (uint32_t p = p0 + threadIdx.x; p < p1; p += 256) {
+        const uint32_t k = key[p];
+        if (p == p0 || k != key[p - 1]) s[k - c0] = p;
+    }
+    __syncthreads();
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    uint32_t v[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j += 4) {
+        const uint4 u = *(const uint4*)&s[kPer * t + j];
+        v[j] = u.x; v[j + 1] = u.y; v[j + 2] = u.z; v[j + 3] = u.w;
+    }
+#pragma unroll
+    for (int j = kPer - 2; j >= 0; j--) v[j] = min(v[j], v[j + 1]);
+    // minimum over the threads after this one
+    uint32_t x = v[0];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_down(x, o, 64);
+        if (lane + o < 64) x = min(x, y);
+    }
+    if (lane == 0) s_wmin[wid] = x;
+    uint32_t after = __shfl_down(x, 1, 64);
+    if (lane == 63) after = p1;
+    __syncthreads();
+    for (int w = wid + 1; w < 4; w++) after = min(after, s_wmin[w]);
+    const int64_t c = c0 + kPer * t;
+#pragma unroll
+    for (int j = 0; j < kPer; j += 4) {
+        const uint4 o = make_uint4(min(v[j], after), min(v[j + 1], after), min(v[j + 2], after), min(v[j + 3], after));
+        if (c + j + 3 < ncells1) {
+            *(uint4*)&cstart[c + j] = o;
+        } else {
+            if (c + j < ncells1) cstart[c + j] = o.x;
+            if (c + j + 1 < ncells1) cstart[c + j + 1] = o.y;
+            if (c + j + 2 < ncells1) cstart[c + j + 2] = o.z;
+        }
+    }
+}
+
+// fp32 build: sort key + the point record {x, y, z, caller index bits} as the sort payload
+__global__ void k_cell_keys_rec(GridDesc g, const float* cxyz, const int32_t* mapping, int64_t n, uint32_t* key,
+                                float4* rec, int32_t* mark) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float* p = cxyz + 3 * i;
+        int cx, cy, cz;
+        cell_of_point<float>(g, p, cx, cy, cz);
+        key[i] = (uint32_t)cell_id(g, cx, cy, cz);
+        rec[i] = make_float4(p[0], p[1], p[2], __int_as_float(mapping[i]));
+        if (mark) mark[brick_of(g, cx, cy, cz)] = 1;
+    }
 }
 
 // Radix-sort build: key = cell id (cstart index) of each compacted point, value = its
@@ -152,19 +235,6 @@ __global__ void k_cell_keys(GridDesc g, const T* cxyz, int64_t n, uint32_t* key,
         val[i] = (uint32_t)i;
         if (mark) mark[brick_of(g, cx, cy, cz)] = 1;
     }
-}
-
-// per-cell counts from the runs of the sorted keys (count[] zeroed): run starts record
-// their position, run ends turn it into the run length
-__global__ void k_run_start(const uint32_t* key, int64_t n, uint32_t* count) {
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
-         k += (int64_t)gridDim.x * blockDim.x)
-        if (k == 0 || key[k] != key[k - 1]) count[key[k]] = (uint32_t)k;
-}
-__global__ void k_run_end(const uint32_t* key, int64_t n, uint32_t* count) {
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
-         k += (int64_t)gridDim.x * blockDim.x)
-        if (k == n - 1 || key[k] != key[k + 1]) count[key[k]] = (uint32_t)(k + 1) - count[key[k]];
 }
 
 // points in cell order: w = internal j (fp64, FLANN tie order) or caller index bits (fp32)
@@ -293,9 +363,13 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     uint32_t* count = nullptr;
     uint32_t* rank = nullptr;  // sort input values (point index)
     uint32_t* skey = nullptr;  // sort input keys (cell id)
-    if ((rc = dmalloc(ctx, &rank, n + 1)) || (rc = dmalloc(ctx, &skey, n + 1))) {
+    if ((is_f64 && (rc = dmalloc(ctx, &rank, n + 1))) || (rc = dmalloc(ctx, &skey, n + 1))) {
         dfree(ctx, rank);
         dfree(ctx, cxyz);
+        return fail(rc);
+    }
+    if ((rc = dmalloc(ctx, (typename Real<T>::V4**)&ix->pts, n + 1))) {
+        dfree(ctx, rank); dfree(ctx, skey); dfree(ctx, cxyz);
         return fail(rc);
     }
     for (int attempt = 0; attempt < 3; attempt++) {
@@ -331,60 +405,80 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             ncells = (int64_t)nslots * 64;
         }
         if ((rc = dmalloc(ctx, &count, ncells + 1))) break;
-        PCP_HIP(ctx, hipMemsetAsync(count, 0, (size_t)(ncells + 1) * sizeof(uint32_t), st));
-        // ---- stable radix sort of (cell id, point) pairs, then per-cell counts from the runs
+        // ---- stable radix sort by cell id.  fp32: the payload is the point record itself, so
+        // the sort output is the cell-ordered point array (no gather).  fp64: the payload is the
+        // internal j (FLANN tie order), gathered below.
         uint32_t* key1 = nullptr;
         uint32_t* val1 = nullptr;
+        using V4 = typename Real<T>::V4;
         if (n > 0) {
-            if ((rc = dmalloc(ctx, &key1, n)) || (rc = dmalloc(ctx, &val1, n))) {
-                dfree(ctx, key1);
-                break;
-            }
-            hipLaunchKernelGGL(k_cell_keys<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, skey, rank,
-                               g.dense ? ix->brick : nullptr);
+            if ((rc = dmalloc(ctx, &key1, n))) break;
+            if (is_f64 && (rc = dmalloc(ctx, &val1, n))) { dfree(ctx, key1); break; }
+            float4* rec0 = nullptr;
+            if (!is_f64 && (rc = dmalloc(ctx, &rec0, n))) { dfree(ctx, key1); break; }
             unsigned bits = 1;
             while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)ncells) bits++;
             size_t tmp_bytes = 0;
-            PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u, bits, st));
             void* tmp = nullptr;
-            if ((rc = dmalloc(ctx, (char**)&tmp, tmp_bytes))) { dfree(ctx, key1); dfree(ctx, val1); break; }
-            PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u, bits, st));
+            if (is_f64) {
+                hipLaunchKernelGGL(k_cell_keys<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, skey, rank,
+                                   g.dense ? ix->brick : nullptr);
+                PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u,
+                                                       bits, st));
+                if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
+                    PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u,
+                                                           bits, st));
+            } else {
+                hipLaunchKernelGGL(k_cell_keys_rec, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const float*)cxyz,
+                                   (const int32_t*)ix->mapping, n, skey, rec0, g.dense ? ix->brick : nullptr);
+                PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, rec0, (float4*)ix->pts,
+                                                       (size_t)n, 0u, bits, st));
+                if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
+                    PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, rec0, (float4*)ix->pts,
+                                                           (size_t)n, 0u, bits, st));
+            }
             dfree(ctx, tmp);
-            hipLaunchKernelGGL(k_run_start, dim3(grid_for(n, kB)), dim3(kB), 0, st, (const uint32_t*)key1, n, count);
-            hipLaunchKernelGGL(k_run_end, dim3(grid_for(n, kB)), dim3(kB), 0, st, (const uint32_t*)key1, n, count);
+            dfree(ctx, rec0);
+            if (rc) { dfree(ctx, key1); dfree(ctx, val1); break; }
         }
         if (g.dense)
             hipLaunchKernelGGL(k_brick_flag, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks);
+        // ---- chunk boundaries of the sorted keys (+ the number of non-empty cells)
+        const int64_t nchunk = (ncells + 1 + kChunk - 1) / kChunk;
+        uint32_t* lo = nullptr;
+        unsigned long long* d_ne = nullptr;
+        if ((rc = dmalloc(ctx, &lo, nchunk + 1)) || (rc = dmalloc(ctx, &d_ne, 1))) {
+            dfree(ctx, lo); dfree(ctx, key1); dfree(ctx, val1);
+            break;
+        }
+        PCP_HIP(ctx, hipMemsetAsync(d_ne, 0, sizeof(unsigned long long), st));
+        hipLaunchKernelGGL(k_chunk_lo, dim3(grid_for(n + 1, kB, 1024)), dim3(kB), 0, st, (const uint32_t*)key1, n,
+                           nchunk, lo, d_ne);
         if (auto_h && attempt < 2 && n > 0) {
-            unsigned long long* d_ne;
-            if ((rc = dmalloc(ctx, &d_ne, 1))) { dfree(ctx, key1); dfree(ctx, val1); break; }
-            PCP_HIP(ctx, hipMemsetAsync(d_ne, 0, sizeof(unsigned long long), st));
-            hipLaunchKernelGGL(k_nonempty, dim3(grid_for(ncells, kB, 4096)), dim3(kB), 0, st, count, ncells, d_ne);
             unsigned long long ne = 0;
             hipMemcpyAsync(&ne, d_ne, sizeof(ne), hipMemcpyDeviceToHost, st);
             hipStreamSynchronize(st);
-            dfree(ctx, d_ne);
             double occ = (double)n / std::max(1.0, (double)ne);
             bool redo = false;
             if (occ > 12.0) { h *= std::sqrt(4.0 / occ); redo = true; }   // surface-like data
             else if (occ < 1.5) { h *= std::cbrt(4.0 / occ); redo = true; }  // sparser than assumed
-            if (redo) { dfree(ctx, key1); dfree(ctx, val1); continue; }
+            if (redo) { dfree(ctx, lo); dfree(ctx, d_ne); dfree(ctx, key1); dfree(ctx, val1); continue; }
         }
-        // ---- cell starts + points in cell order
-        rc = scan_u32_inplace(ctx, count, ncells + 1, nullptr);
-        if (rc) { dfree(ctx, key1); dfree(ctx, val1); break; }
+        // ---- cell starts straight from the sorted keys (no count array, no scan)
+        hipLaunchKernelGGL(k_cell_starts, dim3((unsigned)nchunk), dim3(kB), 0, st, (const uint32_t*)key1,
+                           (const uint32_t*)lo, ncells + 1, count);
+        dfree(ctx, lo);
+        dfree(ctx, d_ne);
         g.cstart = count;
         ix->g = g;
         ix->cstart = count;
         count = nullptr;
-        using V4 = typename Real<T>::V4;
-        if ((rc = dmalloc(ctx, (V4**)&ix->pts, n + 1)) || (rc = dmalloc(ctx, &ix->sorted_j, n + 1))) {
-            dfree(ctx, key1); dfree(ctx, val1);
-            break;
+        if (is_f64) {
+            if ((rc = dmalloc(ctx, &ix->sorted_j, n + 1))) { dfree(ctx, key1); dfree(ctx, val1); break; }
+            if (n > 0)
+                hipLaunchKernelGGL(k_gather<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, cxyz, (const uint32_t*)val1,
+                                   (const int32_t*)ix->mapping, n, (V4*)ix->pts, ix->sorted_j, is_f64);
         }
-        if (n > 0)
-            hipLaunchKernelGGL(k_gather<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, cxyz, (const uint32_t*)val1,
-                               (const int32_t*)ix->mapping, n, (V4*)ix->pts, ix->sorted_j, is_f64);
         dfree(ctx, key1);
         dfree(ctx, val1);
         if (is_f64) {
@@ -407,14 +501,6 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
 }
 
 }  // namespace
-
-// Brick-ordered (4x4x4-cell bricks, x-fastest brick order) index: used to give ICP query
-// sets a spatially compact order (a chunk of consecutive queries spans a few bricks).
-int index_build_f32_bricks(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size,
-                           pcp_index** out) {
-    if (stride == 0) stride = 3 * sizeof(float);
-    return build_impl<float>(ctx, xyz, stride, n, nullptr, cell_size, 0, out, true);
-}
 
 }  // namespace pcp
 

@@ -13,6 +13,8 @@
 #include <cstring>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "grid.hpp"
 
 struct pcp_icp {
@@ -571,6 +573,40 @@ __global__ void __launch_bounds__(256) k_sum_partials(const double* part, int nb
     }
 }
 
+// ---- query order (pcp_icp_create): queries sorted once by target-grid cell in brick-major
+// order (4x4x4-cell bricks; stable, so input order inside a cell), carried as float4
+// {x, y, z, bits(index)}
+// through the radix sort; non-finite queries get key 64 * nbricks (after every cell) and
+// are dropped.
+__global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_t n, uint32_t* key, float4* rec) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float* p = q + (size_t)i * stride_f;
+        const float x = p[0], y = p[1], z = p[2];
+        const bool fin = isfinite(x) && isfinite(y) && isfinite(z);
+        uint32_t k = (uint32_t)(g.nbricks * 64);  // past every cell: non-finite queries sort last
+        if (fin) {
+            const int cx = clampi(cell_i<float>(g, x, 0), 0, g.n[0] - 1);
+            const int cy = clampi(cell_i<float>(g, y, 1), 0, g.n[1] - 1);
+            const int cz = clampi(cell_i<float>(g, z, 2), 0, g.n[2] - 1);
+            k = (uint32_t)(brick_of(g, cx, cy, cz) * 64 + local_of(cx, cy, cz));  // brick-major cell order
+        }
+        key[i] = k;
+        rec[i] = make_float4(x, y, z, __int_as_float((int)i));
+    }
+}
+
+// number of finite queries = first position of the sentinel key in the sorted keys
+// (a single-address atomic per wave costs ~9 ms at 50M queries; this costs nothing)
+__global__ void k_first_at_least(const uint32_t* sorted, int64_t n, uint32_t key, unsigned long long* out) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (sorted[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    *out = (unsigned long long)lo;
+}
+
 // ------------------------------------------------------------------ host 3x3 solve
 // One-sided Jacobi SVD of a 3x3 matrix: A = U diag(s) V^T (columns of U, V).
 void svd3(const double Ain[9], double U[9], double s[3], double V[9]) {
@@ -763,17 +799,61 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     if (target->is_f64) return pcp::set_error(ctx, PCP_ERR_ARG, "ICP target must be an fp32 index");
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     *out = nullptr;
-    // spatially sort the query set once (same grid machinery), keep its sorted points
-    pcp_index* qi = nullptr;
-    PCP_TRY(pcp::index_build_f32_bricks(ctx, q, q_stride, nq, target->g.h, &qi));
+    if (q_stride == 0) q_stride = 3 * sizeof(float);
+    if (q_stride % sizeof(float)) return pcp::set_error(ctx, PCP_ERR_ARG, "query stride must be whole floats");
+    if (nq >= ((int64_t)1 << 31)) return pcp::set_error(ctx, PCP_ERR_ARG, "ICP supports < 2^31 queries");
+    if (target->g.nbricks * 64 >= ((int64_t)1 << 32))
+        return pcp::set_error(ctx, PCP_ERR_UNSUPPORTED, "ICP target grid too large for 32-bit cell keys");
+    // sort the query set once by target-grid brick (stable radix sort, record as payload)
+    hipStream_t st = ctx->stream;
+    float4* qs = nullptr;
+    int64_t nfin = 0;
+    {
+        uint32_t *k0 = nullptr, *k1 = nullptr;
+        float4* r0 = nullptr;
+        unsigned long long* d_cnt = nullptr;
+        void* tmp = nullptr;
+        int rc = pcp::dmalloc(ctx, &k0, nq);
+        if (!rc) rc = pcp::dmalloc(ctx, &k1, nq);
+        if (!rc) rc = pcp::dmalloc(ctx, &r0, nq);
+        if (!rc) rc = pcp::dmalloc(ctx, &qs, nq + 1);
+        if (!rc) rc = pcp::dmalloc(ctx, &d_cnt, 1);
+        if (!rc && hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long), st) != hipSuccess)
+            rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
+        if (!rc && nq > 0) {
+            hipLaunchKernelGGL(pcp::k_query_keys, dim3(pcp::grid_for(nq, 256)), dim3(256), 0, st, target->g, q,
+                               q_stride / sizeof(float), nq, k0, r0);
+            unsigned bits = 1;  // keys are in [0, 64 * nbricks]
+            while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)target->g.nbricks * 64) bits++;
+            size_t tb = 0;
+            hipError_t e = rocprim::radix_sort_pairs(nullptr, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
+            if (e == hipSuccess && !(rc = pcp::dmalloc(ctx, (char**)&tmp, tb)))
+                e = rocprim::radix_sort_pairs(tmp, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
+            if (!rc && e == hipSuccess)
+                hipLaunchKernelGGL(pcp::k_first_at_least, dim3(1), dim3(1), 0, st, k1, nq,
+                                   (uint32_t)(target->g.nbricks * 64), d_cnt);
+            unsigned long long hc = 0;
+            if (!rc && e == hipSuccess) e = hipMemcpyAsync(&hc, d_cnt, sizeof(hc), hipMemcpyDeviceToHost, st);
+            if (!rc && e == hipSuccess) e = hipStreamSynchronize(st);
+            if (!rc && e != hipSuccess) rc = pcp::hip_fail(ctx, e, "query sort", __FILE__, __LINE__);
+            nfin = (int64_t)hc;
+        }
+        pcp::dfree(ctx, k0);
+        pcp::dfree(ctx, k1);
+        pcp::dfree(ctx, r0);
+        pcp::dfree(ctx, d_cnt);
+        pcp::dfree(ctx, tmp);
+        if (rc) {
+            pcp::dfree(ctx, qs);
+            return rc;
+        }
+    }
     pcp_icp* icp = new pcp_icp();
     icp->ctx = ctx;
     icp->target = target;
-    icp->nq = qi->n;
+    icp->nq = nfin;
     icp->nq_in = nq;
-    icp->q = (float4*)qi->pts;
-    qi->pts = nullptr;
-    pcp_index_destroy(qi);
+    icp->q = qs;
     int dev_cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
