@@ -444,32 +444,24 @@ __global__ void k_fb_compact(const int32_t* fb, const uint32_t* cnt, const uint3
     for (uint32_t k = threadIdx.x & 63; k < n; k += 64) out[o + k] = fb[seg * seg_cap + k];
 }
 
-// fixed-order reduction of nb partial rows of 24 doubles -> out[24]
-__global__ void __launch_bounds__(256) k_reduce_partials(const double* part, int nb, double* out,
-                                                         const uint32_t* fbc, int nfb) {
-    __shared__ double s[256];
-    for (int k = 0; k < kAcc; k++) {
-        double v = 0.0;
-        for (int b = threadIdx.x; b < nb; b += 256) v += part[(int64_t)b * kAcc + k];
-        s[threadIdx.x] = v;
-        __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[k] = s[0];
-        __syncthreads();
-    }
-    // slot 23 (unused by the solve): fallback queries of this iteration
-    double f = 0.0;
-    for (int b = threadIdx.x; b < nfb; b += 256) f += (double)fbc[b];
-    s[threadIdx.x] = f;
+// fixed-order reduction of nb partial rows of 24 doubles -> out[24]: thread t sums column
+// t % 24 over the rows b = t / 24 (mod 32) -- coalesced row reads, no barrier per column --
+// then 24 threads add the 32 group sums in order.  Slot 23 (unused by the solve) carries the
+// number of fallback queries of the iteration (*fb_total, or 0 without a fallback list).
+constexpr int kRedGroups = 32;
+__global__ void __launch_bounds__(kAcc * kRedGroups) k_reduce_partials(const double* part, int nb, double* out,
+                                                                       const uint32_t* fb_total) {
+    __shared__ double s[kRedGroups][kAcc];
+    const int k = threadIdx.x % kAcc, grp = threadIdx.x / kAcc;
+    double v = 0.0;
+    for (int b = grp; b < nb; b += kRedGroups) v += part[(int64_t)b * kAcc + k];
+    s[grp][k] = v;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
-        __syncthreads();
+    if (threadIdx.x < kAcc) {
+        double t = 0.0;
+        for (int j = 0; j < kRedGroups; j++) t += s[j][threadIdx.x];
+        out[threadIdx.x] = threadIdx.x == kAcc - 1 ? (fb_total ? (double)*fb_total : 0.0) : t;
     }
-    if (threadIdx.x == 0) out[kAcc - 1] = s[0];
 }
 
 // sorted-order winners -> caller (original query) order
@@ -585,10 +577,12 @@ __global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_
         const bool fin = isfinite(x) && isfinite(y) && isfinite(z);
         uint32_t k = (uint32_t)(g.nbricks * 64);  // past every cell: non-finite queries sort last
         if (fin) {
-            const int cx = clampi(cell_i<float>(g, x, 0), 0, g.n[0] - 1);
-            const int cy = clampi(cell_i<float>(g, y, 1), 0, g.n[1] - 1);
-            const int cz = clampi(cell_i<float>(g, z, 2), 0, g.n[2] - 1);
-            k = (uint32_t)(brick_of(g, cx, cy, cz) * 64 + local_of(cx, cy, cz));  // brick-major cell order
+            // dual cell = the octant block origin floor(f - 1/2) the main pass will use: lanes
+            // with the same block scan the same target rows, so their loads coalesce
+            const int cx = clampi((int)floorf(cell_f<float>(g, x, 0) - 0.5f), 0, g.n[0] - 1);
+            const int cy = clampi((int)floorf(cell_f<float>(g, y, 1) - 0.5f), 0, g.n[1] - 1);
+            const int cz = clampi((int)floorf(cell_f<float>(g, z, 2) - 0.5f), 0, g.n[2] - 1);
+            k = (uint32_t)(brick_of(g, cx, cy, cz) * 64 + local_of(cx, cy, cz));  // brick-major block order
         }
         key[i] = k;
         rec[i] = make_float4(x, y, z, __int_as_float((int)i));
@@ -734,9 +728,9 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
                        icp->partials + (int64_t)icp->nb_fast * kAcc, (const int32_t*)icp->fbc,
                        (const uint32_t*)(icp->fb_off + a.nseg));
     PCP_HIP(ctx, hipEventRecord(icp->ev1, ctx->stream));
-    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(256), 0, ctx->stream, icp->partials,
-                       icp->nb_fast + icp->nb_ring, acc_dev, (const uint32_t*)icp->fb_count,
-                       a.g.dense ? (int)a.nseg : 0);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kAcc * kRedGroups), 0, ctx->stream, icp->partials,
+                       icp->nb_fast + icp->nb_ring, acc_dev,
+                       a.g.dense ? (const uint32_t*)(icp->fb_off + a.nseg) : nullptr);
     if (corr_idx) {
         if (icp->nq_in > icp->nq)  // non-finite queries were dropped at create time
             hipLaunchKernelGGL(k_fill_corr, dim3(grid_for(icp->nq_in, 256)), dim3(256), 0, ctx->stream, corr_idx,
