@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cell", type=float, default=0.1)
     ap.add_argument("--cpu-n", type=int, default=2_000_000, help="CPU baseline sample size")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--host-loop", action="store_true", help="host solve per iteration (one round trip each)")
     return ap.parse_args()
 
 
@@ -100,27 +101,43 @@ def main():
     def one_step(timed):
         index = ops.GridIndex(ctx, tgt, cell_size=args.cell)
         icp = ops.ICP(index, q)
-        T = np.eye(4)
-        err = -1.0
-        for _ in range(args.iters):
-            acc = icp.step(T, args.rmax)
-            ms, nl = icp.last_kernel_ms()
+        if args.host_loop:  # reference-style loop: host solve, one round trip per iteration
+            T = np.eye(4)
+            err = -1.0
+            for _ in range(args.iters):
+                acc = icp.step(T, args.rmax)
+                ms, nl = icp.last_kernel_ms()
+                if timed:
+                    kernel["ms"] += ms
+                    kernel["launches"] += nl
+                    kernel["fallback"] = kernel.get("fallback", 0) + icp.last_fallback()
+                if world > 1:
+                    acc_buf.copy_(acc)
+                    dist.all_reduce(acc_buf)
+                    a = acc_buf.cpu().numpy()
+                else:
+                    a = acc.cpu().numpy()
+                rc, dT = ops.icp_solve(a)
+                if rc != 0:
+                    err = -1.0
+                    break
+                err = math.sqrt(a[22] / a[0])
+                T = dT @ T
+        else:  # device-resident loop: pose, solve and all-reduce stay on the GPU stream
+            T_dev, stats = icp.new_pose()
+            for _ in range(args.iters):
+                acc = icp.step_dev(T_dev, args.rmax)
+                if world > 1:
+                    dist.all_reduce(acc)
+                icp.solve_dev(acc, T_dev, stats)
+            ms, nl = icp.kernel_ms()  # waits for the step
+            st = stats.cpu().numpy()
             if timed:
                 kernel["ms"] += ms
                 kernel["launches"] += nl
-                kernel["fallback"] = kernel.get("fallback", 0) + icp.last_fallback()
-            if world > 1:
-                acc_buf.copy_(acc)
-                dist.all_reduce(acc_buf)
-                a = acc_buf.cpu().numpy()
-            else:
-                a = acc.cpu().numpy()
-            rc, dT = ops.icp_solve(a)
-            if rc != 0:
-                err = -1.0
-                break
-            err = math.sqrt(a[22] / a[0])
-            T = dT @ T
+                kernel["fallback"] = kernel.get("fallback", 0) + st[2]
+            T = T_dev.cpu().numpy().reshape(4, 4)
+            err = float(st[1]) if st[0] == 0 and st[3] == args.iters else -1.0
         result["T"], result["err"], result["nq"] = T, err, icp.q.shape[0]
         icp.close()
         index.close()

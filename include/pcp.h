@@ -213,6 +213,21 @@ int pcp_icp_run(pcp_ctx* ctx, pcp_icp* icp, double T_inout[16], float rmax, int 
 /* Device time (ms) of the last pcp_icp_step/pcp_icp_run correspondence kernels
  * (sum over iterations) and the number of launches it covers, from hipEvents. */
 int pcp_icp_last_kernel_ms(const pcp_icp* icp, double* ms, int* launches);
+/* Device-resident iteration (no host round trip per iteration; multi-GPU callers insert
+ * their all-reduce of acc_dev between the two calls on the same stream).  T_dev: 16 doubles
+ * row-major in device memory.  pcp_icp_step_dev = pcp_icp_step for the pose in T_dev.
+ * pcp_icp_solve_dev: Kabsch/Umeyama solve of acc_dev on the device and T_dev <- dT * T_dev;
+ * stats_dev (4 doubles, zeroed by the caller) = [status (0 ok, -1 failed: T frozen), rms of
+ * the last solved step, running sum of fallback queries, iterations solved].
+ * pcp_icp_run_dev = iters x (step_dev + solve_dev), no convergence test (get_rot_icp with a
+ * fixed iteration count; point_cloud_helper.cpp:75-166). */
+int pcp_icp_step_dev(pcp_ctx* ctx, pcp_icp* icp, const double* T_dev, float rmax, double* acc_dev);
+int pcp_icp_solve_dev(pcp_ctx* ctx, const double* acc_dev, int do_scale, double* T_dev, double* stats_dev);
+int pcp_icp_run_dev(pcp_ctx* ctx, pcp_icp* icp, double* T_dev, float rmax, int iters, int do_scale,
+                    double* stats_dev);
+/* Device ms of the correspondence kernels of every pcp_icp_step_dev / pcp_icp_run_dev launch
+ * since the previous call (waits for them), and how many launches that was; resets. */
+int pcp_icp_kernel_ms(pcp_ctx* ctx, pcp_icp* icp, double* ms, int* launches);
 /* Queries of the last pcp_icp_step that needed the exact ring-search fallback (the fast
  * octant pass could not certify their nearest neighbour). */
 int pcp_icp_last_fallback(const pcp_icp* icp, int64_t* n);

@@ -34,6 +34,9 @@ struct pcp_icp {
     double* acc = nullptr;        // 24 (scratch for pcp_icp_run)
     int nb_fast = 0, nb_ring = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
+    float* pose_dev = nullptr;    // 12 floats (R row-major, t) for the device-resident loop
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-launch timing events (device loop)
+    size_t ntev = 0;              // pairs recorded since the last pcp_icp_kernel_ms
     int dbg = 0;                  // PCP_ICP_ABLATE flags (profiling only)
     double last_ms = 0.0;
     int last_launches = 0;
@@ -70,7 +73,18 @@ struct IcpArgs {
     int64_t nseg;       // fallback segments (= waves of the octant kernel)
     int ring_all;       // ring kernel: process every query (sparse grid) instead of the list
     int dbg;            // ablation flags (PCP_ICP_ABLATE, profiling builds of the bench only)
+    const float* pose;  // device pose (R row-major, t) overriding R/t, or null
 };
+
+// the pose as the kernels use it: from the device copy when the loop is device-resident
+__device__ __forceinline__ void load_pose(IcpArgs& a) {
+    if (a.pose) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) a.R[k] = a.pose[k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) a.t[k] = a.pose[9 + k];
+    }
+}
 
 // Ablation switches for profiling (env PCP_ICP_ABLATE); results are wrong when any is set.
 constexpr int kDbgNoScan = 1, kDbgNoAccum = 4, kDbgNoFallback = 8;
@@ -287,6 +301,7 @@ __device__ __forceinline__ void write_wave_partials(double (*s_acc)[kAcc], doubl
 }
 
 __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a) {
+    load_pose(a);
     constexpr int kW = kIcpBlock / 64;
     __shared__ double s_acc[kW][kAcc];
     const GridDesc& g = a.g;
@@ -372,6 +387,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
 // take 64-entry chunks grid-stride and accumulate like the octant pass.
 __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_ring(IcpArgs a, double* partials,
                                                                         const int32_t* list, const uint32_t* list_n) {
+    load_pose(a);
     constexpr int kW = kIcpBlock / 64;
     __shared__ double s_acc[kW][kAcc];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -603,9 +619,10 @@ __global__ void k_first_at_least(const uint32_t* sorted, int64_t n, uint32_t key
 
 // ------------------------------------------------------------------ host 3x3 solve
 // One-sided Jacobi SVD of a 3x3 matrix: A = U diag(s) V^T (columns of U, V).
-void svd3(const double Ain[9], double U[9], double s[3], double V[9]) {
+// (host and device: the device-resident loop solves on the GPU with the same code)
+__host__ __device__ void svd3(const double Ain[9], double U[9], double s[3], double V[9]) {
     double A[9];
-    std::memcpy(A, Ain, sizeof(A));
+    for (int i = 0; i < 9; i++) A[i] = Ain[i];
     for (int i = 0; i < 9; i++) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; sweep++) {
         double off = 0.0;
@@ -617,13 +634,13 @@ void svd3(const double Ain[9], double U[9], double s[3], double V[9]) {
                     be += A[3 * r + q] * A[3 * r + q];
                     ga += A[3 * r + p] * A[3 * r + q];
                 }
-                if (ga == 0.0 || std::fabs(ga) <= 1e-300) continue;
-                double conv = std::fabs(ga) / std::sqrt(al * be);
+                if (ga == 0.0 || fabs(ga) <= 1e-300) continue;
+                double conv = fabs(ga) / sqrt(al * be);
                 if (!(conv > 1e-15)) continue;
-                off = std::fmax(off, conv);
+                off = fmax(off, conv);
                 double zeta = (be - al) / (2.0 * ga);
-                double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
-                double c = 1.0 / std::sqrt(1.0 + t * t), sn = c * t;
+                double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
                 for (int r = 0; r < 3; r++) {
                     double ap = A[3 * r + p], aq = A[3 * r + q];
                     A[3 * r + p] = c * ap - sn * aq;
@@ -638,19 +655,19 @@ void svd3(const double Ain[9], double U[9], double s[3], double V[9]) {
     for (int c = 0; c < 3; c++) {
         double n = 0;
         for (int r = 0; r < 3; r++) n += A[3 * r + c] * A[3 * r + c];
-        s[c] = std::sqrt(n);
+        s[c] = sqrt(n);
     }
     // order singular values descending (permute U/V columns consistently)
     int ord[3] = {0, 1, 2};
     for (int i = 0; i < 3; i++)
         for (int j = i + 1; j < 3; j++)
-            if (s[ord[j]] > s[ord[i]]) std::swap(ord[i], ord[j]);
+            if (s[ord[j]] > s[ord[i]]) { const int tmp = ord[i]; ord[i] = ord[j]; ord[j] = tmp; }
     double A2[9], V2[9], s2[3];
     for (int c = 0; c < 3; c++) {
         s2[c] = s[ord[c]];
         for (int r = 0; r < 3; r++) { A2[3 * r + c] = A[3 * r + ord[c]]; V2[3 * r + c] = V[3 * r + ord[c]]; }
     }
-    std::memcpy(V, V2, sizeof(V2));
+    for (int i = 0; i < 9; i++) V[i] = V2[i];
     for (int c = 0; c < 3; c++) s[c] = s2[c];
     const double tiny = 1e-14 * (s[0] > 0 ? s[0] : 1.0);
     for (int c = 0; c < 3; c++)
@@ -659,10 +676,10 @@ void svd3(const double Ain[9], double U[9], double s[3], double V[9]) {
     if (!(s[2] > tiny)) {
         double u0[3] = {U[0], U[3], U[6]}, u1[3] = {U[1], U[4], U[7]};
         if (!(s[1] > tiny)) {  // rank 1: any unit vector orthogonal to u0
-            double a[3] = {std::fabs(u0[0]) < 0.9 ? 1.0 : 0.0, std::fabs(u0[0]) < 0.9 ? 0.0 : 1.0, 0.0};
+            double a[3] = {fabs(u0[0]) < 0.9 ? 1.0 : 0.0, fabs(u0[0]) < 0.9 ? 0.0 : 1.0, 0.0};
             double d = a[0] * u0[0] + a[1] * u0[1] + a[2] * u0[2];
             for (int r = 0; r < 3; r++) u1[r] = a[r] - d * u0[r];
-            double nn = std::sqrt(u1[0] * u1[0] + u1[1] * u1[1] + u1[2] * u1[2]);
+            double nn = sqrt(u1[0] * u1[0] + u1[1] * u1[1] + u1[2] * u1[2]);
             for (int r = 0; r < 3; r++) { u1[r] /= nn; U[3 * r + 1] = u1[r]; }
         }
         double u2[3] = {u0[1] * u1[2] - u0[2] * u1[1], u0[2] * u1[0] - u0[0] * u1[2], u0[0] * u1[1] - u0[1] * u1[0]};
@@ -670,15 +687,49 @@ void svd3(const double Ain[9], double U[9], double s[3], double V[9]) {
     }
 }
 
-double det3(const double M[9]) {
+__host__ __device__ double det3(const double M[9]) {
     return M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) +
            M[2] * (M[3] * M[7] - M[4] * M[6]);
 }
 
 }  // namespace
 
+// device pose for the kernels: R, t of T (row-major 4x4 doubles) cast to fp32 as on the host
+__global__ void k_pose_from_T(const double* T, float* pose) {
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) pose[3 * r + c] = (float)T[4 * r + c];
+        pose[9 + r] = (float)T[4 * r + 3];
+    }
+}
+
+__host__ __device__ int icp_solve(const double acc[24], int do_scale, double dT[16]);
+
+// One thread: solve the 3x3 problem of acc, T <- dT * T (device pose), stats as in pcp.h
+// (the host loop of pcp_icp_run, minus the convergence test).  A failed solve latches
+// stats[0] = -1 and freezes T.
+__global__ void k_icp_solve_dev(const double* acc, int do_scale, double* T, double* stats) {
+    if (stats[0] < 0) return;
+    double a[24], dT[16], Tn[16];
+    for (int k = 0; k < 24; k++) a[k] = acc[k];
+    stats[2] += a[23];
+    if (icp_solve(a, do_scale, dT) != PCP_OK) {
+        stats[0] = -1.0;
+        return;
+    }
+    stats[1] = sqrt(a[22] / a[0]);
+    stats[3] += 1.0;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            double v = 0;
+            for (int k = 0; k < 4; k++) v += dT[4 * i + k] * T[4 * k + j];
+            Tn[4 * i + j] = v;
+        }
+    for (int k = 0; k < 16; k++) T[k] = Tn[k];
+}
+
+// T (host) or T_dev (device pose, read by k_pose_from_T) -- exactly one is non-null
 int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, int32_t* corr_idx,
-               float* corr_d2) {
+               float* corr_d2, const double* T_dev = nullptr) {
     pcp_ctx* ctx = icp->ctx;
     const pcp_index* tg = icp->target;
     IcpArgs a;
@@ -687,9 +738,17 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.q = icp->q;
     a.nq = icp->nq;
     a.nchunks = (icp->nq + kIcpBlock - 1) / kIcpBlock;
-    for (int r = 0; r < 3; r++) {
-        for (int c = 0; c < 3; c++) a.R[3 * r + c] = (float)T[4 * r + c];
-        a.t[r] = (float)T[4 * r + 3];
+    a.pose = nullptr;
+    if (T_dev) {
+        hipLaunchKernelGGL(k_pose_from_T, dim3(1), dim3(1), 0, ctx->stream, T_dev, icp->pose_dev);
+        a.pose = icp->pose_dev;
+        for (int k = 0; k < 9; k++) a.R[k] = 0.f;
+        for (int k = 0; k < 3; k++) a.t[k] = 0.f;
+    } else {
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) a.R[3 * r + c] = (float)T[4 * r + c];
+            a.t[r] = (float)T[4 * r + 3];
+        }
     }
     a.r2 = rmax * rmax;
     const int nmax = std::max(a.g.n[0], std::max(a.g.n[1], a.g.n[2]));
@@ -709,7 +768,22 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.ring_all = a.g.dense ? 0 : 1;
     a.dbg = icp->dbg;
     PCP_HIP(ctx, hipMemsetAsync(icp->fb_count, 0, (size_t)a.nseg * sizeof(uint32_t), ctx->stream));
-    PCP_HIP(ctx, hipEventRecord(icp->ev0, ctx->stream));
+    hipEvent_t e0 = icp->ev0, e1 = icp->ev1;
+    if (T_dev) {  // device-resident loop: one event pair per launch, read by pcp_icp_kernel_ms
+        if (icp->ntev == icp->tev.size()) {
+            std::pair<hipEvent_t, hipEvent_t> pr{nullptr, nullptr};
+            PCP_HIP(ctx, hipEventCreate(&pr.first));
+            if (hipEventCreate(&pr.second) != hipSuccess) {
+                (void)hipEventDestroy(pr.first);
+                return set_error(ctx, PCP_ERR_HIP, "hipEventCreate");
+            }
+            icp->tev.push_back(pr);
+        }
+        e0 = icp->tev[icp->ntev].first;
+        e1 = icp->tev[icp->ntev].second;
+        icp->ntev++;
+    }
+    PCP_HIP(ctx, hipEventRecord(e0, ctx->stream));
     if (a.g.dense) {
         hipLaunchKernelGGL(k_icp_octant, dim3(icp->nb_fast), dim3(kIcpBlock), 0, ctx->stream, a);
     } else {
@@ -727,7 +801,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, ctx->stream, a,
                        icp->partials + (int64_t)icp->nb_fast * kAcc, (const int32_t*)icp->fbc,
                        (const uint32_t*)(icp->fb_off + a.nseg));
-    PCP_HIP(ctx, hipEventRecord(icp->ev1, ctx->stream));
+    PCP_HIP(ctx, hipEventRecord(e1, ctx->stream));
     hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kAcc * kRedGroups), 0, ctx->stream, icp->partials,
                        icp->nb_fast + icp->nb_ring, acc_dev,
                        a.g.dense ? (const uint32_t*)(icp->fb_off + a.nseg) : nullptr);
@@ -743,7 +817,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     return PCP_OK;
 }
 
-int icp_solve(const double acc[24], int do_scale, double dT[16]) {
+__host__ __device__ int icp_solve(const double acc[24], int do_scale, double dT[16]) {
     const double n = acc[0];
     if (!(n >= 3.0)) return PCP_ERR_ICP;
     double qm[3], pm[3], S[9];
@@ -860,6 +934,7 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     icp->fb_seg = ((nchunks64 + nwaves - 1) / nwaves) * 64;
     int rc = pcp::dmalloc(ctx, &icp->partials, (size_t)(icp->nb_fast + icp->nb_ring) * pcp::kAcc);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->acc, pcp::kAcc);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_dev, 12);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->win, icp->nq + 1);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->wd2, icp->nq + 1);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fb, (size_t)nwaves * icp->fb_seg + 1);
@@ -890,9 +965,14 @@ int pcp_icp_destroy(pcp_icp* icp) {
     pcp::dfree(icp->ctx, icp->fb_count);
     pcp::dfree(icp->ctx, icp->fb_off);
     pcp::dfree(icp->ctx, icp->fbc);
-    if (icp->ev0) hipEventDestroy(icp->ev0);
-    if (icp->ev1) hipEventDestroy(icp->ev1);
-    if (icp->ev_mid) hipEventDestroy(icp->ev_mid);
+    pcp::dfree(icp->ctx, icp->pose_dev);
+    if (icp->ev0) (void)hipEventDestroy(icp->ev0);
+    if (icp->ev1) (void)hipEventDestroy(icp->ev1);
+    if (icp->ev_mid) (void)hipEventDestroy(icp->ev_mid);
+    for (auto& pr : icp->tev) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
     delete icp;
     return PCP_OK;
 }
@@ -1012,6 +1092,51 @@ int pcp_icp_run(pcp_ctx* ctx, pcp_icp* icp, double T[16], float rmax, int iters,
     icp->last_launches = launches;
     if (err) *err = (float)e;
     return e < 0 ? PCP_ERR_ICP : PCP_OK;
+}
+
+int pcp_icp_step_dev(pcp_ctx* ctx, pcp_icp* icp, const double* T_dev, float rmax, double* acc_dev) {
+    if (!ctx || !icp || !T_dev || !acc_dev || !(rmax >= 0.f)) return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    icp->ctx = ctx;
+    return pcp::icp_launch(icp, nullptr, rmax, acc_dev, nullptr, nullptr, T_dev);
+}
+
+int pcp_icp_solve_dev(pcp_ctx* ctx, const double* acc_dev, int do_scale, double* T_dev, double* stats_dev) {
+    if (!ctx || !acc_dev || !T_dev || !stats_dev) return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(pcp::k_icp_solve_dev, dim3(1), dim3(1), 0, ctx->stream, acc_dev, do_scale, T_dev, stats_dev);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_icp_run_dev(pcp_ctx* ctx, pcp_icp* icp, double* T_dev, float rmax, int iters, int do_scale,
+                    double* stats_dev) {
+    if (!ctx || !icp || !T_dev || !stats_dev || iters < 0 || !(rmax >= 0.f)) return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    icp->ctx = ctx;
+    for (int it = 0; it < iters; it++) {
+        PCP_TRY(pcp::icp_launch(icp, nullptr, rmax, icp->acc, nullptr, nullptr, T_dev));
+        hipLaunchKernelGGL(pcp::k_icp_solve_dev, dim3(1), dim3(1), 0, ctx->stream, (const double*)icp->acc, do_scale,
+                           T_dev, stats_dev);
+    }
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_icp_kernel_ms(pcp_ctx* ctx, pcp_icp* icp, double* ms, int* launches) {
+    if (!ctx || !icp) return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    double tot = 0.0;
+    for (size_t i = 0; i < icp->ntev; i++) {
+        PCP_HIP(ctx, hipEventSynchronize(icp->tev[i].second));
+        float m = 0.f;
+        PCP_HIP(ctx, hipEventElapsedTime(&m, icp->tev[i].first, icp->tev[i].second));
+        tot += m;
+    }
+    if (ms) *ms = tot;
+    if (launches) *launches = (int)icp->ntev;
+    icp->ntev = 0;
+    return PCP_OK;
 }
 
 int pcp_icp_last_fallback(const pcp_icp* icp, int64_t* n) {

@@ -282,6 +282,33 @@ class ICP:
             ctx.check(rc)
         return float(err.value), np.array(T[:]).reshape(4, 4)
 
+    # ---- device-resident loop: the pose stays in HBM, no host round trip per iteration
+    def new_pose(self, T0=None):
+        """(T_dev, stats_dev): a device pose (16 fp64, row-major) and zeroed stats (4 fp64)."""
+        T = torch.as_tensor(np.eye(4) if T0 is None else np.asarray(T0, dtype=np.float64), dtype=torch.float64)
+        return T.reshape(16).to(self.ctx.device).contiguous(), torch.zeros(4, dtype=torch.float64,
+                                                                        device=self.ctx.device)
+
+    def step_dev(self, T_dev, rmax):
+        ctx = self.ctx
+        ctx.check(ctx.lib.pcp_icp_step_dev(ctx.h, self.h, _ptr(T_dev), float(rmax), _ptr(self.acc)))
+        return self.acc
+
+    def solve_dev(self, acc, T_dev, stats, do_scale=False):
+        ctx = self.ctx
+        ctx.check(ctx.lib.pcp_icp_solve_dev(ctx.h, _ptr(acc), int(do_scale), _ptr(T_dev), _ptr(stats)))
+
+    def run_dev(self, T_dev, stats, rmax, iters, do_scale=False):
+        ctx = self.ctx
+        ctx.check(ctx.lib.pcp_icp_run_dev(ctx.h, self.h, _ptr(T_dev), float(rmax), int(iters), int(do_scale),
+                                          _ptr(stats)))
+
+    def kernel_ms(self):
+        """(ms, launches) of the device-loop correspondence kernels since the last call."""
+        ms, n = C.c_double(), C.c_int()
+        self.ctx.check(self.ctx.lib.pcp_icp_kernel_ms(self.ctx.h, self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
     def keys(self, T, rmax, target_offset=0):
         """Target-sharded mode: per-query int64 keys (fp32 d2 bits << 32 | global target
         index, INT64_MAX = none) in the original query order."""

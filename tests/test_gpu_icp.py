@@ -105,6 +105,47 @@ def test_icp_run_matches_oracle(ctx):
     assert np.abs(T - eT).max() < 1e-5
 
 
+def test_device_loop_matches_oracle_and_host_loop(ctx):
+    # pcp_icp_run_dev / step_dev + solve_dev: pose, solve and stats stay in device memory
+    from pointcloudprocess_amd import ops, synth
+    T_true = synth.rigid()
+    tgt, q = _pair(300_000, 21, T_true)
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+    icp = ops.ICP(index, q.to(ctx.device))
+    T_dev, stats = icp.new_pose()
+    icp.run_dev(T_dev, stats, 0.25, 20)
+    ms, nl = icp.kernel_ms()
+    assert nl == 20 and ms > 0
+    st = stats.cpu().numpy()
+    assert st[0] == 0 and st[3] == 20
+    T = T_dev.cpu().numpy().reshape(4, 4)
+    eerr, eT = ora.icp(tgt.numpy(), q.numpy(), np.eye(4), 0.25, 20)
+    assert abs(st[1] - eerr) < 1e-5
+    assert np.abs(T - eT).max() < 1e-5
+    # the same iterations through step_dev + solve_dev equal run_dev exactly
+    T2, st2 = icp.new_pose()
+    for _ in range(20):
+        icp.solve_dev(icp.step_dev(T2, 0.25), T2, st2)
+    assert torch.equal(T2, T_dev) and torch.equal(st2, stats)
+    # and the host loop (host solve): same arithmetic, but a last-bit difference of the fp64
+    # solve can flip the fp32 cast of the pose and with it a few correspondences
+    herr, hT = icp.run(np.eye(4), 0.25, 20)
+    assert np.abs(hT - T).max() < 1e-6 and abs(herr - st[1]) < 1e-6
+
+
+def test_device_loop_failure_latches(ctx):
+    from pointcloudprocess_amd import ops
+    tgt = torch.rand((1000, 3)) * 10
+    q = torch.rand((100, 3)) * 10 + 1000.0  # no correspondences: the solve fails
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.5)
+    icp = ops.ICP(index, q.to(ctx.device))
+    T_dev, stats = icp.new_pose()
+    icp.run_dev(T_dev, stats, 0.5, 3)
+    st = stats.cpu().numpy()
+    assert st[0] == -1 and st[3] == 0
+    assert np.array_equal(T_dev.cpu().numpy().reshape(4, 4), np.eye(4))
+
+
 def test_sparse_grid_matches_oracle(ctx):
     # two clusters 5 km apart with 5 cm cells: the dense cell table would exceed its budget,
     # so the index uses 4x4x4 bricks and the ICP runs the general box search for every query
