@@ -4,7 +4,8 @@
 Workload (BASELINE.json metric "Mcorrespondences/s + ICP iter/s, 50M-vs-50M fp32"):
 config C4 -- a point_cloud_closure / get_rot_icp registration: build the fp32 grid index of
 a 50M-point target, sort the 50M-point query set, then 20 ICP iterations (fused
-transform + exact 1-NN within rmax + 24 accumulators per iteration, host Kabsch solve).
+transform + exact 1-NN within rmax + 24 accumulators per iteration, Kabsch solve on the
+device; the pose never leaves HBM during the 20 iterations).
 One "step" = one such full registration; inputs (fp32 xyz) are resident in HBM before the
 timed region.  N GPUs: each rank registers its own 50M-vs-50M tile of a larger scene
 (co-partitioned target/query, weak scaling); the only collective is the all-reduce of the
@@ -13,6 +14,8 @@ timed region.  N GPUs: each rank registers its own 50M-vs-50M tile of a larger s
   python bench.py [--gpus N] [--steps K] [--warmup W] [--n 50000000] [--iters 20]
 """
 import argparse
+import glob
+import hashlib
 import json
 import math
 import os
@@ -31,6 +34,31 @@ from pointcloudprocess_amd import ops, synth  # noqa: E402
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_CORR = 32         # 12 query + 12 target + 8 (idx, d2)
 METRIC = "Mcorrespondences/s + ICP iter/s, 50M-vs-50M fp32 @ 1/2/4/8 MI355X"
+
+
+def pmc_traffic():
+    """HBM bytes per ICP iteration (k_icp_octant + k_icp_ring, FETCH_SIZE x2 + WRITE_SIZE) from
+    the newest profiles/*/pmc_traffic.json measured on THIS icp.hip (sha1 match), else None.
+    Made by: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) of
+    `bench.py --steps 1 --warmup 0 --no-cpu`, summarised by tools/pmc_summary.py."""
+    src = os.path.join(ROOT, "pointcloudprocess_amd", "csrc", "icp.hip")
+    sha = hashlib.sha1(open(src, "rb").read()).hexdigest()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), key=os.path.getmtime,
+                    reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("icp_hip_sha1") != sha:
+            continue
+        tot = 0.0
+        for k in ("k_icp_octant", "k_icp_ring"):
+            e = d["kernels"].get(k)
+            if e is None:
+                return None
+            tot += e["fetch_bytes_avg"] + (e["write_bytes_avg"] or 0.0)
+        return tot, os.path.relpath(f, ROOT)
+    return None
 
 
 def parse():
@@ -162,6 +190,7 @@ def main():
     corr_total = n * world * args.iters * args.steps
     value = corr_total / dt / 1e6
     k_avg_ms = kernel["ms"] / max(kernel["launches"], 1)
+    traffic = pmc_traffic()
     achieved = BYTES_PER_CORR * n / (k_avg_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes / launch
     if rank == 0:
         T_err = float(np.abs(result["T"] - T_true).max())
@@ -194,7 +223,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": round(traffic[0] / (k_avg_ms * 1e-3) / 1e9, 2) if traffic else None,
+                "traffic_bytes_per_launch": round(traffic[0]) if traffic else None,
+                "traffic_source": traffic[1] if traffic else None,
                 "kernel_avg_ms": round(k_avg_ms, 4),
                 "bytes_per_unit": BYTES_PER_CORR,
                 "units_per_launch": n,

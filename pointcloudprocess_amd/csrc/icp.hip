@@ -68,6 +68,7 @@ struct IcpArgs {
     float* wd2;
     int32_t* fb;
     uint32_t* fb_count;
+    uint32_t* fb_off;   // nseg + 1: the counts again, scanned in place after the pass
     int64_t fb_seg;
     int nb_fast;
     int64_t nseg;       // fallback segments (= waves of the octant kernel)
@@ -377,7 +378,11 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
 #endif
         chunk_accumulate(acc_ok, qx, qy, qz, b, s_acc[wid], lane);
     }
-    if (lane == 0) a.fb_count[gw] = fbn;
+    if (lane == 0) {  // every wave of the grid writes its count: no zeroing pass needed
+        a.fb_count[gw] = fbn;
+        a.fb_off[gw] = fbn;  // scanned in place into the segment offsets
+        if (gw == 0) a.fb_off[a.nseg] = 0u;
+    }
     write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
 }
 
@@ -465,12 +470,20 @@ __global__ void k_fb_compact(const int32_t* fb, const uint32_t* cnt, const uint3
 // then 24 threads add the 32 group sums in order.  Slot 23 (unused by the solve) carries the
 // number of fallback queries of the iteration (*fb_total, or 0 without a fallback list).
 constexpr int kRedGroups = 32;
-__global__ void __launch_bounds__(kAcc * kRedGroups) k_reduce_partials(const double* part, int nb, double* out,
-                                                                       const uint32_t* fb_total) {
+__global__ void __launch_bounds__(kAcc * kRedGroups) k_reduce_partials(const double* __restrict__ part, int nb,
+                                                                       double* out, const uint32_t* fb_total) {
     __shared__ double s[kRedGroups][kAcc];
     const int k = threadIdx.x % kAcc, grp = threadIdx.x / kAcc;
     double v = 0.0;
-    for (int b = grp; b < nb; b += kRedGroups) v += part[(int64_t)b * kAcc + k];
+    int b = grp;
+    for (; b + 7 * kRedGroups < nb; b += 8 * kRedGroups) {  // 8 loads in flight, summed in order
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) x[u] = part[(int64_t)(b + u * kRedGroups) * kAcc + k];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v += x[u];
+    }
+    for (; b < nb; b += kRedGroups) v += part[(int64_t)b * kAcc + k];
     s[grp][k] = v;
     __syncthreads();
     if (threadIdx.x < kAcc) {
@@ -762,12 +775,12 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.wd2 = icp->wd2;
     a.fb = icp->fb;
     a.fb_count = icp->fb_count;
+    a.fb_off = icp->fb_off;
     a.fb_seg = icp->fb_seg;
     a.nb_fast = icp->nb_fast;
     a.nseg = (int64_t)icp->nb_fast * (kIcpBlock / 64);
     a.ring_all = a.g.dense ? 0 : 1;
     a.dbg = icp->dbg;
-    PCP_HIP(ctx, hipMemsetAsync(icp->fb_count, 0, (size_t)a.nseg * sizeof(uint32_t), ctx->stream));
     hipEvent_t e0 = icp->ev0, e1 = icp->ev1;
     if (T_dev) {  // device-resident loop: one event pair per launch, read by pcp_icp_kernel_ms
         if (icp->ntev == icp->tev.size()) {
@@ -791,9 +804,6 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     }
     if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_mid, ctx->stream));
     if (a.g.dense) {  // compact the per-wave fallback segments into one list
-        PCP_HIP(ctx, hipMemcpyAsync(icp->fb_off, icp->fb_count, (size_t)a.nseg * sizeof(uint32_t),
-                                    hipMemcpyDeviceToDevice, ctx->stream));
-        PCP_HIP(ctx, hipMemsetAsync(icp->fb_off + a.nseg, 0, sizeof(uint32_t), ctx->stream));
         PCP_TRY(scan_u32_inplace(ctx, icp->fb_off, a.nseg + 1, nullptr));
         hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)((a.nseg + 3) / 4)), dim3(256), 0, ctx->stream, icp->fb,
                            (const uint32_t*)icp->fb_count, (const uint32_t*)icp->fb_off, a.nseg, a.fb_seg, icp->fbc);
