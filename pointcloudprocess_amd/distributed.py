@@ -19,6 +19,12 @@ An *engine* supplies the local compute:
     step(T, rmax) -> acc            (24 float64, torch tensor on the engine's device)
     keys(T, rmax, offset) -> keys   (int64 torch tensor, one per query)
     accumulate_keys(T, keys, lo, hi) -> acc
+and, for the device-resident loop (run_copartitioned_dev: the pose and the solve stay on
+the device, the all-reduce is enqueued on the same stream, no host round trip per
+iteration):
+    new_pose(T0) -> (T_dev, stats)  (16 + 4 float64 tensors on the engine's device)
+    step_dev(T_dev, rmax) -> acc
+    solve_dev(acc, T_dev, stats, do_scale)
 GpuEngine is the libpcp implementation; tests/oracle_engine.py restates it on the CPU.
 """
 import math
@@ -61,6 +67,19 @@ def run_copartitioned(engine, T0, rmax, iters, do_scale=False):
     return err, T
 
 
+def run_copartitioned_dev(engine, T0, rmax, iters, do_scale=False):
+    """run_copartitioned with the pose, solve and all-reduce kept on the device stream (the
+    bench's loop); one host sync at the end.  Returns (err, T) -- identical on every rank."""
+    T_dev, stats = engine.new_pose(T0)
+    for _ in range(iters):
+        acc = engine.step_dev(T_dev, rmax)
+        _allreduce(acc, dist.ReduceOp.SUM)
+        engine.solve_dev(acc, T_dev, stats, do_scale)
+    st = stats.cpu().numpy()
+    T = T_dev.cpu().numpy().reshape(4, 4)
+    return (float(st[1]) if st[0] == 0 and st[3] == iters else -1.0), T
+
+
 def run_target_sharded(engine, T0, rmax, iters, lo, hi, do_scale=False):
     """ICP with the target sharded over ranks ([lo, hi) = this rank's global target range)."""
     T = np.array(T0, dtype=np.float64)
@@ -94,6 +113,15 @@ class GpuEngine:
 
     def keys(self, T, rmax, offset):
         return self.icp.keys(T, rmax, offset)
+
+    def new_pose(self, T0):
+        return self.icp.new_pose(T0)
+
+    def step_dev(self, T_dev, rmax):
+        return self.icp.step_dev(T_dev, rmax)
+
+    def solve_dev(self, acc, T_dev, stats, do_scale=False):
+        self.icp.solve_dev(acc, T_dev, stats, do_scale)
 
     def accumulate_keys(self, T, keys, lo, hi):
         return self.icp.accumulate_keys(T, keys, lo, hi, self.target)

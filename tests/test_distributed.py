@@ -38,14 +38,15 @@ def _worker(rank, world, port, mode, out):
     from oracle_engine import OracleEngine
     from pointcloudprocess_amd import distributed as D
     tgt, q, _ = _data()
-    if mode == "copartitioned":
+    if mode in ("copartitioned", "copartitioned_dev"):
         # x-slabs of the query set; the target tile carries a 1 m halo (>> rmax + motion)
         cut = 0.0
         lo_x, hi_x = (-np.inf, cut) if rank == 0 else (cut, np.inf)
         qm = (q[:, 0] >= lo_x) & (q[:, 0] < hi_x)
         tm = (tgt[:, 0] >= lo_x - 1.0) & (tgt[:, 0] < hi_x + 1.0)
         eng = OracleEngine(tgt[tm], q[qm])
-        err, T = D.run_copartitioned(eng, np.eye(4), 0.25, 8)
+        run = D.run_copartitioned if mode == "copartitioned" else D.run_copartitioned_dev
+        err, T = run(eng, np.eye(4), 0.25, 8)
     else:
         lo, hi = D.shard_range(len(tgt), world, rank)
         eng = OracleEngine(tgt[lo:hi], q)
@@ -54,7 +55,7 @@ def _worker(rank, world, port, mode, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["copartitioned", "target_sharded"])
+@pytest.mark.parametrize("mode", ["copartitioned", "copartitioned_dev", "target_sharded"])
 def test_two_ranks_match_single_process(mode):
     import oracle_ctypes as ora
     tgt, q, T_true = _data()
