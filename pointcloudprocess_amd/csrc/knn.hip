@@ -29,15 +29,30 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
     return 1e-9 + 8e-16 * (double)nmax;
 }
 
+// Candidates of a cell are loaded PCP_KNN_BATCH (or 2 for the wide top-k) at a time before
+// they are pushed, so the loads of a batch are in flight together instead of one dependent
+// round trip per candidate.  Push order is unchanged (and irrelevant: (d2, j) order).
+#ifndef PCP_KNN_BATCH
+#define PCP_KNN_BATCH 4
+#endif
 template <int K>
 struct KnnVisitor {
+    static constexpr int U = K <= 16 ? PCP_KNN_BATCH : 2;
     const double4* pts;
     double qx, qy, qz;
     TopK<K> top;
     // pruning radius^2 (1e-12 covers the rounding of the cell-box bound and of d2)
     __device__ double bound() const { return top.kth() * (1.0 + 1e-12); }
     __device__ void visit(uint32_t s, uint32_t e) {
-        for (uint32_t t = s; t < e; t++) {
+        uint32_t t = s;
+        for (; t + U <= e; t += U) {
+            double4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) p[u] = pts[t + u];
+#pragma unroll
+            for (int u = 0; u < U; u++) top.push(l2_simple(qx, qy, qz, p[u]), (int)p[u].w);
+        }
+        for (; t < e; t++) {
             const double4 p = pts[t];
             top.push(l2_simple(qx, qy, qz, p), (int)p.w);
         }
@@ -110,7 +125,13 @@ struct CountVisitor {
     uint32_t cnt;
     __device__ double bound() const { return b; }
     __device__ void visit(uint32_t s, uint32_t e) {
-        for (uint32_t t = s; t < e; t++) cnt += l2_simple(qx, qy, qz, pts[t]) < r2 ? 1u : 0u;
+        uint32_t t = s;
+        for (; t + 4 <= e; t += 4) {
+            const double4 p0 = pts[t], p1 = pts[t + 1], p2 = pts[t + 2], p3 = pts[t + 3];
+            cnt += (l2_simple(qx, qy, qz, p0) < r2 ? 1u : 0u) + (l2_simple(qx, qy, qz, p1) < r2 ? 1u : 0u) +
+                   (l2_simple(qx, qy, qz, p2) < r2 ? 1u : 0u) + (l2_simple(qx, qy, qz, p3) < r2 ? 1u : 0u);
+        }
+        for (; t < e; t++) cnt += l2_simple(qx, qy, qz, pts[t]) < r2 ? 1u : 0u;
     }
 };
 
@@ -143,15 +164,30 @@ struct FillVisitor {
     bool append;
     __device__ double bound() const { return b; }
     __device__ void visit(uint32_t s, uint32_t e) {
+        if (append) {  // batched loads; entries appended in visiting order
+            uint32_t t = s;
+            for (; t + 4 <= e; t += 4) {
+                double4 p[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) p[u] = pts[t + u];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const double d = l2_simple(qx, qy, qz, p[u]);
+                    if (d < r2 && filled < m) { rd[filled] = d; ri[filled] = (int)p[u].w; filled++; }
+                }
+            }
+            for (; t < e; t++) {
+                const double4 p = pts[t];
+                const double d = l2_simple(qx, qy, qz, p);
+                if (d < r2 && filled < m) { rd[filled] = d; ri[filled] = (int)p.w; filled++; }
+            }
+            return;
+        }
         for (uint32_t t = s; t < e; t++) {
             const double4 p = pts[t];
             const double d = l2_simple(qx, qy, qz, p);
             if (!(d < r2)) continue;
             const int j = (int)p.w;
-            if (append) {
-                if (filled < m) { rd[filled] = d; ri[filled] = j; filled++; }
-                continue;
-            }
             int64_t pos;
             if (filled < m) pos = filled++;
             else if (lex_less(d, j, rd[m - 1], ri[m - 1])) pos = m - 1;
