@@ -231,6 +231,8 @@ int pcp_icp_kernel_ms(pcp_ctx* ctx, pcp_icp* icp, double* ms, int* launches);
 /* Queries of the last pcp_icp_step that needed the exact ring-search fallback (the fast
  * octant pass could not certify their nearest neighbour). */
 int pcp_icp_last_fallback(const pcp_icp* icp, int64_t* n);
+/* Queries of the last pcp_icp_step that the verify pass could not settle (searched). */
+int pcp_icp_last_searched(const pcp_icp* icp, int64_t* n);
 
 /* PointCloudHelper::get_rot_icp (point_cloud_helper.cpp:75-166) on AoS48 clouds:
  * joint centroid, float cast, ICP(query = temp -> target = src), un-centring

@@ -209,6 +209,11 @@ __global__ void __launch_bounds__(256) k_cell_starts(const uint32_t* __restrict_
 }
 
 // fp32 build: sort key + the point record {x, y, z, caller index bits} as the sort payload
+// the fp32 index's pts[n]: +inf coordinates, index INT_MAX -- a gather target that never wins
+__global__ void k_far_sentinel(float4* pts, int64_t n) {
+    pts[n] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(0x7fffffff));
+}
+
 __global__ void k_cell_keys_rec(GridDesc g, const float* cxyz, const int32_t* mapping, int64_t n, uint32_t* key,
                                 float4* rec, int32_t* mark) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -440,6 +445,8 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             dfree(ctx, tmp);
             dfree(ctx, rec0);
             if (rc) { dfree(ctx, key1); dfree(ctx, val1); break; }
+            if (!is_f64)  // pts[n]: a point at infinity (d2 = inf from any finite query) for gathers
+                hipLaunchKernelGGL(k_far_sentinel, dim3(1), dim3(1), 0, st, (float4*)ix->pts, n);
         }
         if (g.dense)
             hipLaunchKernelGGL(k_brick_flag, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks);

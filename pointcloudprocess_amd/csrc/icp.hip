@@ -23,24 +23,38 @@ struct pcp_icp {
     int64_t nq = 0;               // finite queries
     int64_t nq_in = 0;            // queries passed to pcp_icp_create
     float4* q = nullptr;          // sorted queries {x,y,z,bits(original index)}
-    int32_t* win = nullptr;       // per sorted query: winning target index (-1 = rejected)
-    float* wd2 = nullptr;         // per sorted query: winning d2 (+inf = rejected)
+    uint4* cand = nullptr;        // per sorted query: sorted-target positions of its kCache nearest targets
+                                  // at its last search (~0u = empty slot); the winner is always among them
+    uint32_t* dlb = nullptr;      // per sorted query: (float bits of D) & ~0xff | s, where s = the launch
+                                  // (mod 256) of its last search and D a lower bound (m) on the distance
+                                  // from the query, at that launch's pose, to every target NOT in cand
+    float* pose_hist = nullptr;   // 256 x 12 floats: the pose of launch t at slot t & 255
+    int64_t launches = 0;         // correspondence launches so far (the first has nothing to verify)
+    bool last_verified = false;   // the last launch ran the verify pass
+    int32_t* sv = nullptr;        // verify pass: per-wave segments of uncertified queries (sv_seg each)
+    uint32_t* sv_count = nullptr;
+    uint32_t* sv_off = nullptr;
+    int32_t* svc = nullptr;       // compacted search list
+    int64_t sv_seg = 0;
+    int nb_ver = 0;
     int32_t* fb = nullptr;        // fallback lists: one segment of fb_seg entries per octant WG
     uint32_t* fb_count = nullptr; // per octant wave: entries in its segment
     uint32_t* fb_off = nullptr;   // exclusive scan of fb_count (+ total)
     int32_t* fbc = nullptr;       // compacted fallback list
     int64_t fb_seg = 0;
-    double* partials = nullptr;   // (nb_fast + nb_ring) * 24
+    double* partials = nullptr;   // (nb_ver + nb_fast + nb_ring) * 24
     double* acc = nullptr;        // 24 (scratch for pcp_icp_run)
     int nb_fast = 0, nb_ring = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
-    float* pose_dev = nullptr;    // 12 floats (R row-major, t) for the device-resident loop
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr, ev_ver = nullptr;
+    float* pose_dev = nullptr;    // 24 floats: this launch's pose (R row-major, t), then the previous one
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-launch timing events (device loop)
     size_t ntev = 0;              // pairs recorded since the last pcp_icp_kernel_ms
     int dbg = 0;                  // PCP_ICP_ABLATE flags (profiling only)
+    unsigned long long* dbgcnt = nullptr;  // kDbgCount: [candidates, rows, queries]
     double last_ms = 0.0;
     int last_launches = 0;
     uint32_t last_fallback = 0;
+    uint32_t last_searched = 0;   // queries the verify pass could not certify (searched)
 };
 
 namespace pcp {
@@ -49,6 +63,13 @@ namespace {
 constexpr int kIcpBlock = 256;
 #ifndef PCP_OCT_WAVES
 #define PCP_OCT_WAVES 8
+#endif
+#ifndef PCP_VER_WAVES   // tier-1 verify (per-lane accumulators: ~100 VGPRs)
+#define PCP_VER_WAVES 4
+#endif
+
+#ifndef PCP_RING_WAVES
+#define PCP_RING_WAVES 8
 #endif
 constexpr int kAcc = 24;
 
@@ -59,13 +80,22 @@ struct IcpArgs {
     int64_t nq;
     int64_t nchunks;
     float R[9], t[3];
+    float Rp[9], tq[3]; // the previous launch's pose (verify pass)
     float r2;
     float cert2;        // certified radius^2 of the 2x2x2 octant search
     float rho;          // octant half-width in cell units (0.5 - margin)
     float mc;           // cell-unit margin for pruning
     double* partials;
-    int32_t* win;
-    float* wd2;
+    uint4* cand;
+    uint32_t* dlb;
+    const float* pose_hist;
+    uint32_t launch;    // this launch's index (mod 2^32)
+    uint32_t ntp;       // target points (tp[ntp] is the far sentinel)
+    int32_t* sv;        // verify pass output segments (sv_seg entries per wave)
+    uint32_t* sv_count;
+    uint32_t* sv_off;
+    int64_t sv_seg;
+    int64_t nseg_v;     // verify-pass waves
     int32_t* fb;
     uint32_t* fb_count;
     uint32_t* fb_off;   // nseg + 1: the counts again, scanned in place after the pass
@@ -74,7 +104,8 @@ struct IcpArgs {
     int64_t nseg;       // fallback segments (= waves of the octant kernel)
     int ring_all;       // ring kernel: process every query (sparse grid) instead of the list
     int dbg;            // ablation flags (PCP_ICP_ABLATE, profiling builds of the bench only)
-    const float* pose;  // device pose (R row-major, t) overriding R/t, or null
+    const float* pose;  // device poses (current, previous: 24 floats) overriding R/t, Rp/tq, or null
+    unsigned long long* dbgcnt;  // kDbgCount counters, or null
 };
 
 // the pose as the kernels use it: from the device copy when the loop is device-resident
@@ -86,15 +117,27 @@ __device__ __forceinline__ void load_pose(IcpArgs& a) {
         for (int k = 0; k < 3; k++) a.t[k] = a.pose[9 + k];
     }
 }
+__device__ __forceinline__ void load_prev_pose(IcpArgs& a) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) a.Rp[k] = a.pose[12 + k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) a.tq[k] = a.pose[21 + k];
+}
 
 // Ablation switches for profiling (env PCP_ICP_ABLATE); results are wrong when any is set.
-constexpr int kDbgNoScan = 1, kDbgNoAccum = 4, kDbgNoFallback = 8;
+constexpr int kDbgNoScan = 1, kDbgNoAccum = 4, kDbgNoFallback = 8, kDbgCount = 16, kDbgNoVerify = 64;
 
 __device__ __forceinline__ void xform(const IcpArgs& a, const float4 q, float& x, float& y, float& z) {
     // q' = R q + t: x' = fmaf(R02,z,fmaf(R01,y,fmaf(R00,x,t0)))
     x = __fmaf_rn(a.R[2], q.z, __fmaf_rn(a.R[1], q.y, __fmaf_rn(a.R[0], q.x, a.t[0])));
     y = __fmaf_rn(a.R[5], q.z, __fmaf_rn(a.R[4], q.y, __fmaf_rn(a.R[3], q.x, a.t[1])));
     z = __fmaf_rn(a.R[8], q.z, __fmaf_rn(a.R[7], q.y, __fmaf_rn(a.R[6], q.x, a.t[2])));
+}
+// the same expression under the previous launch's pose
+__device__ __forceinline__ void xform_prev(const IcpArgs& a, const float4 q, float& x, float& y, float& z) {
+    x = __fmaf_rn(a.Rp[2], q.z, __fmaf_rn(a.Rp[1], q.y, __fmaf_rn(a.Rp[0], q.x, a.tq[0])));
+    y = __fmaf_rn(a.Rp[5], q.z, __fmaf_rn(a.Rp[4], q.y, __fmaf_rn(a.Rp[3], q.x, a.tq[1])));
+    z = __fmaf_rn(a.Rp[8], q.z, __fmaf_rn(a.Rp[7], q.y, __fmaf_rn(a.Rp[6], q.x, a.tq[2])));
 }
 
 // running 1-NN: best d2, its target index (tie order) and its position in the scanned array
@@ -104,14 +147,20 @@ __device__ __forceinline__ void xform(const IcpArgs& a, const float4 q, float& x
 #ifndef PCP_TRACK_BEST
 #define PCP_TRACK_BEST 0
 #endif
+// the contract's fp32 d2: fmaf(dz,dz,fmaf(dy,dy,dx*dx))
+__device__ __forceinline__ float icp_d2(float qx, float qy, float qz, const float4 p) {
+    const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+    return __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx));
+}
+
 struct Best {
     float bd;
     int bj;
     uint32_t bk;
     float px, py, pz;  // filled by fetch() once the scan is over (or tracked, PCP_TRACK_BEST)
+    uint32_t dbg_len = 0;  // kDbgCount: candidates scanned
     __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t k) {
-        const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
-        const float d2 = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx));
+        const float d2 = icp_d2(qx, qy, qz, p);
         const int id = __float_as_int(p.w);
         // "<=" on the index: re-visiting the current winner (a provisional bound) refreshes bk
         const bool take = d2 < bd || (d2 == bd && id <= bj);
@@ -144,6 +193,7 @@ struct Best {
                                               float qx, float qy, float qz) {
         static_assert(NR == 3 || NR == 4, "3 or 4 rows");
         const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = NR == 4 ? c3 + rn[NR - 1] : c3;
+        dbg_len = L;
         auto addr = [&](uint32_t v) {
             return v < c1 ? rs[0] + v
                           : (v < c2 ? rs[1] + (v - c1) : ((NR == 3 || v < c3) ? rs[2] + (v - c2) : rs[NR - 1] + (v - c3)));
@@ -301,7 +351,295 @@ __device__ __forceinline__ void write_wave_partials(double (*s_acc)[kAcc], doubl
     }
 }
 
-__global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a) {
+// Per-lane accumulation: each lane sums its accepted pairs in fp32, centred on the
+// (transformed) first query of the wave's current stretch of chunks, into 23 registers; every
+// kFlush chunks (and at the end) the wave reduces them with DPP adds and lane 0 un-centres the
+// totals in fp64 into the wave's LDS accumulators.  A stretch is at most kFlush * 64
+// consecutive sorted queries (a few metres), so the centred fp32 products stay small.
+constexpr int kFlush = 32;
+struct LaneAcc {
+    float v[kAcc - 1];  // n, A(3), B(3), AB(9), AA(6), D  (centred on c)
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int k = 0; k < kAcc - 1; k++) v[k] = 0.f;
+    }
+    __device__ __forceinline__ void add(float qx, float qy, float qz, float px, float py, float pz, float d2,
+                                        float cx, float cy, float cz) {
+        const float x[3] = {qx - cx, qy - cy, qz - cz}, p[3] = {px - cx, py - cy, pz - cz};
+        v[0] += 1.f;
+#pragma unroll
+        for (int k = 0; k < 3; k++) { v[1 + k] += x[k]; v[4 + k] += p[k]; }
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) v[7 + 3 * r + k] = __fmaf_rn(x[r], p[k], v[7 + 3 * r + k]);
+        v[16] = __fmaf_rn(x[0], x[0], v[16]);
+        v[17] = __fmaf_rn(x[0], x[1], v[17]);
+        v[18] = __fmaf_rn(x[0], x[2], v[18]);
+        v[19] = __fmaf_rn(x[1], x[1], v[19]);
+        v[20] = __fmaf_rn(x[1], x[2], v[20]);
+        v[21] = __fmaf_rn(x[2], x[2], v[21]);
+        v[22] += d2;
+    }
+    // whole wave (full EXEC): totals -> S (fp64, un-centred by lane 0).  Not inlined: it runs once
+    // per kFlush chunks, and its fp64 temporaries would otherwise raise the loop's register count.
+    __device__ __attribute__((noinline)) void flush(double* S, int lane, float cx, float cy, float cz) {
+        float t[kAcc - 1];
+#pragma unroll
+        for (int k = 0; k < kAcc - 1; k++) t[k] = wave_sum_f32(v[k]);
+        if (lane == 0) {
+            const double n = t[0], C[3] = {cx, cy, cz}, A[3] = {t[1], t[2], t[3]}, B[3] = {t[4], t[5], t[6]};
+            S[0] += n;
+            for (int k = 0; k < 3; k++) { S[1 + k] += A[k] + n * C[k]; S[4 + k] += B[k] + n * C[k]; }
+            for (int r = 0; r < 3; r++)
+                for (int k = 0; k < 3; k++)
+                    S[7 + 3 * r + k] += (double)t[7 + 3 * r + k] + A[r] * C[k] + C[r] * B[k] + n * C[r] * C[k];
+            const int ir[6] = {0, 0, 0, 1, 1, 2}, ik[6] = {0, 1, 2, 1, 2, 2};
+            for (int m = 0; m < 6; m++)
+                S[16 + m] += (double)t[16 + m] + A[ir[m]] * C[ik[m]] + C[ir[m]] * A[ik[m]] + n * C[ir[m]] * C[ik[m]];
+            S[22] += t[22];
+        }
+        zero();
+    }
+};
+
+// ---- candidate cache (a Verlet-style neighbour list per query)
+// The search that last settled query i left cand[i] = the positions of its kCache nearest
+// targets (or fewer) and D = dlb[i], a lower bound on the distance from the query, at the
+// previous launch's pose q_s, to every target point NOT in cand[i].  With q_t the query at the
+// current pose and Delta = |q_t - q_s|, every uncached point p has |q_t - p| >= D - Delta
+// (triangle inequality).  So if the nearest cached point is closer than D - Delta (with
+// relative margins far above the fp32 rounding of d2), it is the exact 1-NN under the
+// contract -- the same (d2, index) winner an exhaustive search returns, cached ties included
+// -- and the query is settled without a search; the bound moves to D - Delta.
+constexpr int kCache = 4;
+
+// the cached candidates' winner under the current pose, by (d2, target index)
+struct CacheBest {
+    float bd = INFINITY;
+    int bj = 0x7fffffff;
+    uint32_t bk = ~0u;
+    float4 P = make_float4(0.f, 0.f, 0.f, 0.f);
+};
+__device__ __forceinline__ CacheBest cache_best(const float4* tp, const uint4 cd, float qx, float qy, float qz) {
+    const uint32_t c[kCache] = {cd.x, cd.y, cd.z, cd.w};
+    float4 p[kCache];
+#pragma unroll
+    for (int s = 0; s < kCache; s++) p[s] = c[s] != ~0u ? tp[c[s]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    CacheBest r;
+#pragma unroll
+    for (int s = 0; s < kCache; s++) {
+        if (c[s] == ~0u) continue;
+        const float d2 = icp_d2(qx, qy, qz, p[s]);
+        const int id = __float_as_int(p[s].w);
+        if (d2 < r.bd || (d2 == r.bd && id < r.bj)) {
+            r.bd = d2;
+            r.bj = id;
+            r.bk = c[s];
+            r.P = p[s];
+        }
+    }
+    return r;
+}
+
+// dlb word: D rounded down to 15 mantissa bits (still a lower bound), launch index in the low byte
+constexpr int kHist = 256;     // pose history slots (launch & 255)
+constexpr uint32_t kMaxAge = 128;  // older caches are searched again (so the slot is never reused)
+__device__ __forceinline__ uint32_t pack_dlb(float D, uint32_t launch) {
+    return (__float_as_uint(fmaxf(D, 0.f)) & ~0xffu) | (launch & 0xffu);
+}
+// 16-byte record of a table by element index (32-bit byte offset: tables < 4 GB)
+template <typename V>
+__device__ __forceinline__ V ld16(const V* base, uint32_t idx) {
+    return *(const V*)((const char*)base + (size_t)(idx * 16u));
+}
+
+// ---- verify pass (every query, every launch after the first)
+// Settles a query from its cache (above): q_s is recomputed exactly from the pose of the
+// launch s that searched it (pose history in LDS), so the bound is |q_t - q_s| (not a sum of
+// steps) and nothing is written for a settled query.  "No correspondence" is settled the same
+// way when the nearest cached point is beyond rmax.  Everything else goes to the search list
+// (per-wave segments, compacted afterwards).  Wave w owns the contiguous chunk range
+// [w*nch/nwaves, (w+1)*nch/nwaves) of the sorted queries; accumulation is per lane (fp32,
+// centred on the stretch's first query).
+__global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs a) {
+    __shared__ float4 s_pose[kHist][3];
+    constexpr int kW = kIcpBlock / 64;
+    __shared__ double s_acc[kW][kAcc];
+    for (int k = threadIdx.x; k < kHist * 3; k += blockDim.x)
+        s_pose[k / 3][k % 3] = ((const float4*)a.pose_hist)[k];
+    load_pose(a);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * kW + wid;
+    const int64_t nwaves = (int64_t)gridDim.x * kW;
+    const int64_t nch = (a.nq + 63) / 64;
+    const int64_t cb = gw * nch / nwaves, ce = (gw + 1) * nch / nwaves;
+    if (lane < kAcc) s_acc[wid][lane] = 0.0;
+    __syncthreads();
+    uint32_t svn = 0;
+    LaneAcc acc;
+    acc.zero();
+    const float r2m = a.r2 * 1.0003f;
+    // software pipeline: the query, cache and bound words two chunks ahead, the cached points'
+    // gathers one chunk ahead (this chunk's were issued during the previous one)
+    const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+    auto raw = [&](int64_t c, float4& q, uint4& cd, uint32_t& D) {
+        const int64_t i = c * 64 + lane;
+        if (c < ce && i < a.nq) {
+            q = a.q[i];
+            cd = a.cand[i];
+            D = a.dlb[i];
+        } else {
+            q = make_float4(0.f, 0.f, 0.f, 0.f);
+            cd = none;
+            D = 0u;
+        }
+    };
+    auto gather = [&](const uint4 cd, float4& p0, float4& p1, float4& p2, float4& p3) {
+        // an empty slot reads the far sentinel tp[ntp]: d2 = inf
+        p0 = ld16(a.tp, min(cd.x, a.ntp));
+        p1 = ld16(a.tp, min(cd.y, a.ntp));
+        p2 = ld16(a.tp, min(cd.z, a.ntp));
+        p3 = ld16(a.tp, min(cd.w, a.ntp));
+    };
+    float4 q1, q2;
+    uint4 c1_, c2_;
+    uint32_t D1, D2;
+    float4 g0, g1, g2, g3;
+    raw(cb, q1, c1_, D1);
+    raw(cb + 1, q2, c2_, D2);
+    gather(c1_, g0, g1, g2, g3);
+    for (int64_t c0 = cb; c0 < ce; c0 += kFlush) {  // stretches of kFlush chunks
+        const int64_t c1 = min(c0 + (int64_t)kFlush, ce);
+        // centre: the stretch's first query under the current pose (wave-uniform)
+        float ccx, ccy, ccz;
+        xform(a, a.q[c0 * 64], ccx, ccy, ccz);
+        ccx = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccx)));
+        ccy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccy)));
+        ccz = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccz)));
+        for (int64_t c = c0; c < c1; c++) {
+            const int64_t i = c * 64 + lane;
+            const bool valid = i < a.nq;
+            const float4 qq = q1;
+            const uint32_t Dw = valid ? D1 : 0u;
+            const float4 p0 = g0, p1 = g1, p2 = g2, p3 = g3;
+            // issue chunk c+1's gathers and chunk c+2's words before using chunk c's
+            gather(c2_, g0, g1, g2, g3);
+            q1 = q2;
+            c1_ = c2_;
+            D1 = D2;
+            raw(c + 2, q2, c2_, D2);
+            float qx, qy, qz;
+            xform(a, qq, qx, qy, qz);
+            // winner among the cached points by (d2, target index); an empty slot never wins
+            float m = INFINITY, px = 0.f, py = 0.f, pz = 0.f;
+            int mj = 0x7fffffff;
+            auto take = [&](const float4 p) {
+                const float e = icp_d2(qx, qy, qz, p);
+                const int id = __float_as_int(p.w);
+                const bool t = e < m || (e == m && id < mj);
+                m = t ? e : m;
+                mj = t ? id : mj;
+                px = t ? p.x : px;
+                py = t ? p.y : py;
+                pz = t ? p.z : pz;
+            };
+            take(p0);
+            take(p1);
+            take(p2);
+            take(p3);
+            // the query at the pose of its last search
+            const uint32_t sl = Dw & 0xffu;
+            const float4 A = s_pose[sl][0], B = s_pose[sl][1], C = s_pose[sl][2];
+            const float ex = qx - __fmaf_rn(A.z, qq.z, __fmaf_rn(A.y, qq.y, __fmaf_rn(A.x, qq.x, C.y)));
+            const float ey = qy - __fmaf_rn(B.y, qq.z, __fmaf_rn(B.x, qq.y, __fmaf_rn(A.w, qq.x, C.z)));
+            const float ez = qz - __fmaf_rn(C.x, qq.z, __fmaf_rn(B.w, qq.y, __fmaf_rn(B.z, qq.x, C.w)));
+            const float delta = sqrtf(__fmaf_rn(ez, ez, __fmaf_rn(ey, ey, ex * ex))) * 1.00001f + 1e-7f;
+            const float lb = __uint_as_float(Dw & ~0xffu) * 0.99998f - delta;  // every uncached point is >= lb
+            // the nearest cached point is the exact 1-NN (it beats lb), or nothing is within rmax
+            const float thr = fminf(m * 1.0003f, r2m);
+            bool ok = valid && ((a.launch - Dw) & 0xffu) < kMaxAge && lb > 0.f && thr + 1e-12f < lb * lb;
+            ok = ok && !(a.dbg & kDbgNoVerify);
+            const bool srch = valid && !ok;
+            const uint64_t msk = __ballot(srch);
+            if (srch) {
+                const uint32_t pos = svn + __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+                a.sv[gw * a.sv_seg + pos] = (int32_t)i;
+            }
+            svn += (uint32_t)__popcll(msk);
+            if (ok && m <= a.r2 && !(a.dbg & kDbgNoAccum)) acc.add(qx, qy, qz, px, py, pz, m, ccx, ccy, ccz);
+        }
+        acc.flush(s_acc[wid], lane, ccx, ccy, ccz);
+    }
+    if (lane == 0) {
+        a.sv_count[gw] = svn;
+        a.sv_off[gw] = svn;  // scanned in place into the segment offsets
+        if (gw == 0) a.sv_off[a.nseg_v] = 0u;
+    }
+    write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
+}
+
+// running kCache(=4)-NN of the search pass: d0 <= d1 <= d2 <= d3 with positions p0..p3, and
+// d4 = the 5th smallest d2 scanned (every uncached scanned point is >= d4).  Equal d2 values
+// keep scan order.  ~16 VALU ops per candidate beyond the d2 (med3 insertion network).
+struct Top4 {
+    float d0 = INFINITY, d1 = INFINITY, d2 = INFINITY, d3 = INFINITY, d4 = INFINITY;
+    uint32_t p0 = ~0u, p1 = ~0u, p2 = ~0u, p3 = ~0u;
+    __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t k) {
+        const float x = icp_d2(qx, qy, qz, p);
+        const bool c0 = x < d0, c1 = x < d1, c2 = x < d2, c3 = x < d3;
+        d4 = __builtin_amdgcn_fmed3f(d3, d4, x);
+        p3 = c2 ? p2 : (c3 ? k : p3);
+        d3 = __builtin_amdgcn_fmed3f(d2, d3, x);
+        p2 = c1 ? p1 : (c2 ? k : p2);
+        d2 = __builtin_amdgcn_fmed3f(d1, d2, x);
+        p1 = c0 ? p0 : (c1 ? k : p1);
+        d1 = __builtin_amdgcn_fmed3f(d0, d1, x);
+        p0 = c0 ? k : p0;
+        d0 = fminf(d0, x);
+    }
+    // rows [rs[r], rs[r] + rn[r]) scanned as one concatenated list, U loads in flight;
+    // branch-free addressing: k = v + off(v), off from 3 compares against the row prefixes
+    __device__ __forceinline__ void scan4(const float4* pts, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
+                                          float qx, float qy, float qz) {
+        const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
+        const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
+        auto addr = [&](uint32_t v) {
+            uint32_t o = v < c3 ? o2 : o3;
+            o = v < c2 ? o1 : o;
+            o = v < c1 ? o0 : o;
+            return v + o;
+        };
+        constexpr int U = PCP_SCAN_UNROLL;
+        uint32_t v = 0;
+        for (; v + U <= L; v += U) {
+            uint32_t k[U];
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) k[u] = addr(v + u);
+#pragma unroll
+            for (int u = 0; u < U; u++) p[u] = pts[k[u]];
+#pragma unroll
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, p[u], k[u]);
+        }
+        for (; v < L; v++) {
+            const uint32_t k = addr(v);
+            consider(qx, qy, qz, pts[k], k);
+        }
+    }
+};
+
+// ---- search pass (the verify pass's list; every query at the first launch)
+// One query per lane, 64-query chunks grid-stride over the list.  Each query scans its whole
+// 2x2x2 "octant" block of cells (the four x-rows [floor(f - 1/2), +1]) keeping its 4 nearest.
+// The octant holds every target within m = the query's distance to its faces (>= 1/2 cell,
+// less the margin).  The nearest is the exact 1-NN when d0 <= m^2 and d0 < d4 (every point
+// tied with it is cached, and the cache order by index decides); "nothing within rmax" is
+// certified when rmax <= m.  The cache is refreshed either way (D = min(d4, m) bounds every
+// uncached point); unsettled queries go to the fallback list.
+__global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a, const int32_t* list,
+                                                                          const uint32_t* list_n) {
     load_pose(a);
     constexpr int kW = kIcpBlock / 64;
     __shared__ double s_acc[kW][kAcc];
@@ -309,39 +647,38 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;  // global wave id = fallback segment
     const int64_t nwaves = (int64_t)gridDim.x * kW;
-    const int64_t nch = (a.nq + 63) / 64;
+    const int64_t n = list ? (int64_t)*list_n : a.nq;
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
     uint32_t fbn = 0;  // wave-uniform count of this wave's fallback entries
-
+    int64_t in_ = 0;
     float4 qn = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (gw < nch && gw * 64 + lane < a.nq) qn = a.q[gw * 64 + lane];
-    for (int64_t c = gw; c < nch; c += nwaves) {
-        const int64_t i = c * 64 + lane;
-        const bool valid = i < a.nq;
+    if (gw * 64 + lane < n) {
+        in_ = list ? (int64_t)list[gw * 64 + lane] : gw * 64 + lane;
+        qn = a.q[in_];
+    }
+    for (int64_t c = gw; c * 64 < n; c += nwaves) {
+        const int64_t j = c * 64 + lane;
+        const bool valid = j < n;
+        const int64_t i = in_;
         const float4 qraw = qn;
-        if (c + nwaves < nch && i + 64 * nwaves < a.nq) qn = a.q[i + 64 * nwaves];  // prefetch
-        Best b{a.r2, 0x7fffffff, ~0u, 0.f, 0.f, 0.f};
+        if (j + 64 * nwaves < n) {  // prefetch the next chunk's query
+            in_ = list ? (int64_t)list[j + 64 * nwaves] : j + 64 * nwaves;
+            qn = a.q[in_];
+        }
+        Top4 b;
         float qx = 0.f, qy = 0.f, qz = 0.f;
-        int bx = 0, by = 0, bz = 0;
-        float cert2 = a.cert2;
+        bool settled = false, found = false;
+        uint32_t win = ~0u;
         if (valid) {
             xform(a, qraw, qx, qy, qz);
             const float fx = cell_f<float>(g, qx, 0), fy = cell_f<float>(g, qy, 1), fz = cell_f<float>(g, qz, 2);
-            bx = (int)floorf(fx - a.rho);
-            by = (int)floorf(fy - a.rho);
-            bz = (int)floorf(fz - a.rho);
-            // this query's certified radius: its distance to the nearest face of the 2x2x2
-            // block (>= 0.5 cell, the worst case a.cert2 is built from), less the margin
+            const int bx = (int)floorf(fx - a.rho), by = (int)floorf(fy - a.rho), bz = (int)floorf(fz - a.rho);
+            // this query's certified radius (cells): its distance to the nearest face of the
+            // 2x2x2 block (>= 0.5 cell), less the margin
             const float m = fminf(fminf(fminf(fx - (float)bx, (float)(bx + 2) - fx),
                                         fminf(fy - (float)by, (float)(by + 2) - fy)),
                                   fminf(fz - (float)bz, (float)(bz + 2) - fz)) - a.mc;
-            const float rr = m * g.hf;
-            cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
-        }
-        if (valid && !(a.dbg & kDbgNoScan)) {
-            // the 4 x-rows of the octant: all 8 row bounds are loaded at once, then the rows
-            // are scanned as one concatenated candidate list with 4 loads in flight, so a
-            // chunk costs ~1 + L/4 memory round trips instead of 4 x (1 + len/4)
+            // the 4 x-rows of the octant: all 8 row bounds at once
             const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
             uint32_t rs[4], rn[4];
 #pragma unroll
@@ -354,17 +691,35 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             }
 #pragma unroll
             for (int r = 0; r < 4; r++) rn[r] -= rs[r];
-            b.scan_rows(a.tp, rs, rn, qx, qy, qz);
+            if (!(a.dbg & kDbgNoScan)) b.scan4(a.tp, rs, rn, qx, qy, qz);
+            if (a.dbg & kDbgCount) {
+                atomicAdd(a.dbgcnt, (unsigned long long)(rn[0] + rn[1] + rn[2] + rn[3]));
+                atomicAdd(a.dbgcnt + 2, 1ull);
+            }
+            const float rr = m * g.hf;
+            const float cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
+            found = b.d0 <= a.r2;
+            settled = (found ? (b.d0 < b.d4 && b.d0 <= cert2) : a.r2 <= cert2) || (a.dbg & kDbgNoFallback);
+            // the winner among the cached ties by target index (rare: only when d1 == d0)
+            win = b.p0;
+            if (found && b.d1 == b.d0) {
+                int wj = __float_as_int(a.tp[b.p0].w);
+                const uint32_t ps[3] = {b.p1, b.p2, b.p3};
+                const float ds[3] = {b.d1, b.d2, b.d3};
+#pragma unroll
+                for (int s2 = 0; s2 < 3; s2++) {
+                    if (ds[s2] != b.d0) break;
+                    const int id = __float_as_int(a.tp[ps[s2]].w);
+                    if (id < wj) { wj = id; win = ps[s2]; }
+                }
+            }
+            // the cache: the 4 nearest; D bounds every uncached point
+            const float D = fminf(sqrtf(b.d4), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f;
+            a.cand[i] = make_uint4(b.p0, b.p1, b.p2, b.p3);
+            a.dlb[i] = pack_dlb(D, a.launch);
         }
-        // ---- epilogue: results, fallback list, accumulators
-        const bool found = b.bj != 0x7fffffff;
-        const bool done = valid && ((found && b.bd <= cert2) || (!found && a.r2 <= cert2) ||
-                                    (a.dbg & kDbgNoFallback));
-        if (valid) {  // provisional for fallback queries (an upper bound), final otherwise
-            a.win[i] = found ? b.bj : -1;
-            a.wd2[i] = found ? b.bd : INFINITY;
-        }
-        const bool fb = valid && !done;
+        // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
+        const bool fb = valid && !settled;
         const uint64_t fbm = __ballot(fb);
         if (fb) {
             const uint32_t pos = fbn + __builtin_amdgcn_mbcnt_hi((uint32_t)(fbm >> 32),
@@ -372,11 +727,10 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             a.fb[gw * a.fb_seg + pos] = (int32_t)i;
         }
         fbn += (uint32_t)__popcll(fbm);
-        const bool acc_ok = done && found && !(a.dbg & kDbgNoAccum);
-#if !PCP_TRACK_BEST
-        if (acc_ok) b.fetch(a.tp);
-#endif
-        chunk_accumulate(acc_ok, qx, qy, qz, b, s_acc[wid], lane);
+        const bool acc_ok = valid && settled && found && !(a.dbg & kDbgNoAccum);
+        Best w{b.d0, 0, win, 0.f, 0.f, 0.f};
+        if (acc_ok) w.fetch(a.tp);
+        chunk_accumulate(acc_ok, qx, qy, qz, w, s_acc[wid], lane);
     }
     if (lane == 0) {  // every wave of the grid writes its count: no zeroing pass needed
         a.fb_count[gw] = fbn;
@@ -390,7 +744,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
 // octant pass's provisional winner when it has one.  Queries come from the compacted
 // fallback list (or are all queries when ring_all is set, i.e. on a sparse grid); waves
 // take 64-entry chunks grid-stride and accumulate like the octant pass.
-__global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_ring(IcpArgs a, double* partials,
+__global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs a, double* partials,
                                                                         const int32_t* list, const uint32_t* list_n) {
     load_pose(a);
     constexpr int kW = kIcpBlock / 64;
@@ -408,9 +762,13 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_ring(IcpArgs a
         if (valid) {
             i = a.ring_all ? j : list[j];
             xform(a, a.q[i], qx, qy, qz);
-            if (!a.ring_all && a.win[i] >= 0) {  // provisional octant winner: a valid upper bound
-                b.bd = a.wd2[i];
-                b.bj = a.win[i];
+            {  // provisional: the cache's best (refreshed by the search pass), an upper bound
+                const CacheBest cbst = cache_best(a.tp, a.cand[i], qx, qy, qz);
+                if (cbst.bd <= b.bd) {
+                    b.bd = cbst.bd;
+                    b.bj = cbst.bj;
+                    b.bk = cbst.bk;
+                }
             }
             bool done = false;
             if (!a.ring_all) {
@@ -446,8 +804,8 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_ring(IcpArgs a
             }
             if (!done) box_search(a.g, a.tp, qx, qy, qz, a.mc, b);
             const bool ok = b.bj != 0x7fffffff;
-            a.win[i] = ok ? b.bj : -1;
-            a.wd2[i] = ok ? b.bd : INFINITY;
+            a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, ~0u);
+            a.dlb[i] = pack_dlb(0.f, a.launch);  // no bound kept: the next launch searches it again
         }
         const bool acc_ok = valid && b.bj != 0x7fffffff && !(a.dbg & kDbgNoAccum);
         if (acc_ok) b.fetch(a.tp);
@@ -493,14 +851,20 @@ __global__ void __launch_bounds__(kAcc * kRedGroups) k_reduce_partials(const dou
     }
 }
 
-// sorted-order winners -> caller (original query) order
-__global__ void k_scatter_corr(const float4* q, const int32_t* win, const float* wd2, int64_t n,
-                               int32_t* idx, float* d2) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+// sorted-order winners -> caller (original query) order; d2 recomputed from the winner's
+// position under the same pose (the same fp32 expression, so bit-identical)
+__global__ void k_scatter_corr(IcpArgs a, int32_t* idx, float* d2) {
+    load_pose(a);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.nq;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const int oq = __float_as_int(q[i].w);
-        idx[oq] = win[i];
-        d2[oq] = wd2[i];
+        const float4 qq = a.q[i];
+        const int oq = __float_as_int(qq.w);
+        float x, y, z;
+        xform(a, qq, x, y, z);
+        const CacheBest w = cache_best(a.tp, a.cand[i], x, y, z);  // the settled winner is cached
+        const bool ok = w.bd <= a.r2;
+        idx[oq] = ok ? w.bj : -1;
+        d2[oq] = ok ? w.bd : INFINITY;
     }
 }
 
@@ -522,13 +886,16 @@ __global__ void k_fill_keys(uint64_t* keys, int64_t n) {
         keys[i] = kNoKey;
 }
 
-__global__ void k_make_keys(const float4* q, const int32_t* win, const float* wd2, int64_t n, uint32_t offset,
-                            uint64_t* keys) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int oq = __float_as_int(q[i].w);
-        const int w = win[i];
-        keys[oq] = w < 0 ? kNoKey
-                         : (((uint64_t)__float_as_uint(wd2[i]) << 32) | (uint64_t)(uint32_t)((uint32_t)w + offset));
+__global__ void k_make_keys(IcpArgs a, uint32_t offset, uint64_t* keys) {
+    load_pose(a);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.nq; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 qq = a.q[i];
+        const int oq = __float_as_int(qq.w);
+        float x, y, z;
+        xform(a, qq, x, y, z);
+        const CacheBest w = cache_best(a.tp, a.cand[i], x, y, z);
+        keys[oq] = w.bd <= a.r2 ? (((uint64_t)__float_as_uint(w.bd) << 32) | (uint64_t)(uint32_t)((uint32_t)w.bj + offset))
+                                : kNoKey;
     }
 }
 
@@ -611,7 +978,11 @@ __global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_
             const int cx = clampi((int)floorf(cell_f<float>(g, x, 0) - 0.5f), 0, g.n[0] - 1);
             const int cy = clampi((int)floorf(cell_f<float>(g, y, 1) - 0.5f), 0, g.n[1] - 1);
             const int cz = clampi((int)floorf(cell_f<float>(g, z, 2) - 0.5f), 0, g.n[2] - 1);
+#if PCP_QORDER_ROWMAJOR
+            k = (uint32_t)dense_id(g, cx, cy, cz);  // the target's row-major cell order
+#else
             k = (uint32_t)(brick_of(g, cx, cy, cz) * 64 + local_of(cx, cy, cz));  // brick-major block order
+#endif
         }
         key[i] = k;
         rec[i] = make_float4(x, y, z, __int_as_float((int)i));
@@ -707,12 +1078,19 @@ __host__ __device__ double det3(const double M[9]) {
 
 }  // namespace
 
-// device pose for the kernels: R, t of T (row-major 4x4 doubles) cast to fp32 as on the host
-__global__ void k_pose_from_T(const double* T, float* pose) {
+// device poses for the kernels: pose[12..23] <- pose[0..11] (the previous launch's), then
+// pose[0..11] <- R, t of T_dev (row-major 4x4 doubles cast to fp32, as on the host) or of the
+// host-cast Rh/th when T_dev is null
+struct HostPose {
+    float R[9], t[3];
+};
+__global__ void k_pose_set(const double* T, HostPose hp, float* pose, float* hist) {
+    for (int k = 0; k < 12; k++) pose[12 + k] = pose[k];
     for (int r = 0; r < 3; r++) {
-        for (int c = 0; c < 3; c++) pose[3 * r + c] = (float)T[4 * r + c];
-        pose[9 + r] = (float)T[4 * r + 3];
+        for (int c = 0; c < 3; c++) pose[3 * r + c] = T ? (float)T[4 * r + c] : hp.R[3 * r + c];
+        pose[9 + r] = T ? (float)T[4 * r + 3] : hp.t[r];
     }
+    for (int k = 0; k < 12; k++) hist[k] = pose[k];
 }
 
 __host__ __device__ int icp_solve(const double acc[24], int do_scale, double dT[16]);
@@ -742,27 +1120,27 @@ __global__ void k_icp_solve_dev(const double* acc, int do_scale, double* T, doub
 
 // T (host) or T_dev (device pose, read by k_pose_from_T) -- exactly one is non-null
 int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, int32_t* corr_idx,
-               float* corr_d2, const double* T_dev = nullptr) {
+               float* corr_d2, const double* T_dev = nullptr, IcpArgs* args_out = nullptr) {
     pcp_ctx* ctx = icp->ctx;
     const pcp_index* tg = icp->target;
-    IcpArgs a;
+    IcpArgs a{};
     a.g = tg->g;
     a.tp = (const float4*)tg->pts;
     a.q = icp->q;
     a.nq = icp->nq;
     a.nchunks = (icp->nq + kIcpBlock - 1) / kIcpBlock;
-    a.pose = nullptr;
-    if (T_dev) {
-        hipLaunchKernelGGL(k_pose_from_T, dim3(1), dim3(1), 0, ctx->stream, T_dev, icp->pose_dev);
-        a.pose = icp->pose_dev;
-        for (int k = 0; k < 9; k++) a.R[k] = 0.f;
-        for (int k = 0; k < 3; k++) a.t[k] = 0.f;
-    } else {
+    HostPose hp{};
+    if (!T_dev) {
         for (int r = 0; r < 3; r++) {
-            for (int c = 0; c < 3; c++) a.R[3 * r + c] = (float)T[4 * r + c];
-            a.t[r] = (float)T[4 * r + 3];
+            for (int c = 0; c < 3; c++) hp.R[3 * r + c] = (float)T[4 * r + c];
+            hp.t[r] = (float)T[4 * r + 3];
         }
     }
+    hipLaunchKernelGGL(k_pose_set, dim3(1), dim3(1), 0, ctx->stream, T_dev, hp, icp->pose_dev,
+                       icp->pose_hist + (icp->launches & (kHist - 1)) * 12);
+    a.pose = icp->pose_dev;  // every kernel reads the pose (and the previous one) from HBM
+    for (int k = 0; k < 9; k++) a.R[k] = hp.R[k];
+    for (int k = 0; k < 3; k++) a.t[k] = hp.t[k];
     a.r2 = rmax * rmax;
     const int nmax = std::max(a.g.n[0], std::max(a.g.n[1], a.g.n[2]));
     a.mc = 1e-5f + 8e-7f * (float)nmax;  // >> fp32 rounding of the cell coordinates
@@ -770,9 +1148,16 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     // exact radius of the octant block: (0.5 - mc) cells, shrunk for fp32 d2 rounding
     const double rr = (0.5 - (double)a.mc) * a.g.h;
     a.cert2 = (float)(rr * rr * (1.0 - 1e-5));
-    a.partials = icp->partials;
-    a.win = icp->win;
-    a.wd2 = icp->wd2;
+    a.cand = icp->cand;
+    a.dlb = icp->dlb;
+    a.pose_hist = icp->pose_hist;
+    a.launch = (uint32_t)icp->launches;
+    a.ntp = (uint32_t)tg->n;
+    a.sv = icp->sv;
+    a.sv_count = icp->sv_count;
+    a.sv_off = icp->sv_off;
+    a.sv_seg = icp->sv_seg;
+    a.nseg_v = (int64_t)icp->nb_ver * (kIcpBlock / 64);
     a.fb = icp->fb;
     a.fb_count = icp->fb_count;
     a.fb_off = icp->fb_off;
@@ -781,6 +1166,10 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.nseg = (int64_t)icp->nb_fast * (kIcpBlock / 64);
     a.ring_all = a.g.dense ? 0 : 1;
     a.dbg = icp->dbg;
+    a.dbgcnt = icp->dbgcnt;
+    double* part_v = icp->partials;
+    double* part_o = part_v + (int64_t)icp->nb_ver * kAcc;
+    double* part_r = part_o + (int64_t)icp->nb_fast * kAcc;
     hipEvent_t e0 = icp->ev0, e1 = icp->ev1;
     if (T_dev) {  // device-resident loop: one event pair per launch, read by pcp_icp_kernel_ms
         if (icp->ntev == icp->tev.size()) {
@@ -796,11 +1185,31 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
         e1 = icp->tev[icp->ntev].second;
         icp->ntev++;
     }
+    if (icp->dbgcnt) PCP_HIP(ctx, hipMemsetAsync(icp->dbgcnt, 0, 16 * sizeof(unsigned long long), ctx->stream));
     PCP_HIP(ctx, hipEventRecord(e0, ctx->stream));
+    const bool verify = a.g.dense && icp->launches > 0;  // the first launch has nothing cached
+    icp->last_verified = verify;
     if (a.g.dense) {
-        hipLaunchKernelGGL(k_icp_octant, dim3(icp->nb_fast), dim3(kIcpBlock), 0, ctx->stream, a);
+        // 1. settle what the candidate caches can; the rest -> search list
+        if (verify) {
+            a.partials = part_v;
+            hipLaunchKernelGGL(k_icp_verify, dim3(icp->nb_ver), dim3(kIcpBlock), 0, ctx->stream, a);
+            PCP_TRY(scan_u32_inplace(ctx, icp->sv_off, a.nseg_v + 1, nullptr));
+            hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)((a.nseg_v + 3) / 4)), dim3(256), 0, ctx->stream,
+                               icp->sv, (const uint32_t*)icp->sv_count, (const uint32_t*)icp->sv_off, a.nseg_v,
+                               a.sv_seg, icp->svc);
+        } else {
+            PCP_HIP(ctx, hipMemsetAsync(part_v, 0, (size_t)icp->nb_ver * kAcc * sizeof(double), ctx->stream));
+        }
+        if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_ver, ctx->stream));
+        // 2. octant search of the list (every query at the first launch); unsettled -> fallback list
+        a.partials = part_o;
+        hipLaunchKernelGGL(k_icp_octant, dim3(icp->nb_fast), dim3(kIcpBlock), 0, ctx->stream, a,
+                           verify ? (const int32_t*)icp->svc : nullptr,
+                           verify ? (const uint32_t*)(icp->sv_off + a.nseg_v) : nullptr);
     } else {
-        PCP_HIP(ctx, hipMemsetAsync(icp->partials, 0, (size_t)icp->nb_fast * kAcc * sizeof(double), ctx->stream));
+        PCP_HIP(ctx, hipMemsetAsync(part_v, 0, (size_t)(icp->nb_ver + icp->nb_fast) * kAcc * sizeof(double),
+                                    ctx->stream));
     }
     if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_mid, ctx->stream));
     if (a.g.dense) {  // compact the per-wave fallback segments into one list
@@ -808,21 +1217,24 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
         hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)((a.nseg + 3) / 4)), dim3(256), 0, ctx->stream, icp->fb,
                            (const uint32_t*)icp->fb_count, (const uint32_t*)icp->fb_off, a.nseg, a.fb_seg, icp->fbc);
     }
-    hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, ctx->stream, a,
-                       icp->partials + (int64_t)icp->nb_fast * kAcc, (const int32_t*)icp->fbc,
-                       (const uint32_t*)(icp->fb_off + a.nseg));
+    // 3. exact fallback (or every query on a sparse grid)
+    a.partials = part_r;
+    hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, ctx->stream, a, part_r,
+                       (const int32_t*)icp->fbc, (const uint32_t*)(icp->fb_off + a.nseg));
     PCP_HIP(ctx, hipEventRecord(e1, ctx->stream));
     hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kAcc * kRedGroups), 0, ctx->stream, icp->partials,
-                       icp->nb_fast + icp->nb_ring, acc_dev,
+                       icp->nb_ver + icp->nb_fast + icp->nb_ring, acc_dev,
                        a.g.dense ? (const uint32_t*)(icp->fb_off + a.nseg) : nullptr);
     if (corr_idx) {
         if (icp->nq_in > icp->nq)  // non-finite queries were dropped at create time
             hipLaunchKernelGGL(k_fill_corr, dim3(grid_for(icp->nq_in, 256)), dim3(256), 0, ctx->stream, corr_idx,
                                corr_d2, icp->nq_in);
         if (icp->nq > 0)
-            hipLaunchKernelGGL(k_scatter_corr, dim3(grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, icp->q,
-                               icp->win, icp->wd2, icp->nq, corr_idx, corr_d2);
+            hipLaunchKernelGGL(k_scatter_corr, dim3(grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, a,
+                               corr_idx, corr_d2);
     }
+    if (args_out) *args_out = a;
+    icp->launches++;
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }
@@ -937,24 +1349,40 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
         dev_cus = prop.multiProcessorCount;
     const int64_t want = (icp->nq + pcp::kIcpBlock - 1) / pcp::kIcpBlock;
-    icp->nb_fast = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * 8));
-    icp->nb_ring = icp->nb_fast;
+    icp->nb_fast = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_OCT_WAVES));
+    icp->nb_ring = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_RING_WAVES));
     const int64_t nwaves = (int64_t)icp->nb_fast * (pcp::kIcpBlock / 64);
     const int64_t nchunks64 = (icp->nq + 63) / 64;
     icp->fb_seg = ((nchunks64 + nwaves - 1) / nwaves) * 64;
-    int rc = pcp::dmalloc(ctx, &icp->partials, (size_t)(icp->nb_fast + icp->nb_ring) * pcp::kAcc);
+    icp->nb_ver = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_VER_WAVES));
+    const int64_t nwaves_v = (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64);
+    icp->sv_seg = ((nchunks64 + nwaves_v - 1) / nwaves_v) * 64;  // contiguous ranges: <= this per wave
+    int rc = pcp::dmalloc(ctx, &icp->partials, (size_t)(icp->nb_ver + icp->nb_fast + icp->nb_ring) * pcp::kAcc);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->acc, pcp::kAcc);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_dev, 12);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->win, icp->nq + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->wd2, icp->nq + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_dev, 24);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->cand, icp->nq + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->dlb, icp->nq + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_hist, pcp::kHist * 12);
+    if (!rc && (hipMemsetAsync(icp->cand, 0xff, (size_t)(icp->nq + 1) * sizeof(uint4), ctx->stream) != hipSuccess ||
+
+                hipMemsetAsync(icp->dlb, 0, (size_t)(icp->nq + 1) * sizeof(uint32_t), ctx->stream) != hipSuccess ||
+                hipMemsetAsync(icp->pose_hist, 0, pcp::kHist * 12 * sizeof(float), ctx->stream) != hipSuccess ||
+                hipMemsetAsync(icp->pose_dev, 0, 24 * sizeof(float), ctx->stream) != hipSuccess))
+        rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv, (size_t)nwaves_v * icp->sv_seg + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_count, (size_t)nwaves_v);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_off, (size_t)nwaves_v + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->svc, icp->nq + 1);
+
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fb, (size_t)nwaves * icp->fb_seg + 1);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_count, (size_t)nwaves);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_off, (size_t)nwaves + 1);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fbc, icp->nq + 1);
     if (!rc && (hipEventCreate(&icp->ev0) != hipSuccess || hipEventCreate(&icp->ev1) != hipSuccess ||
-                hipEventCreate(&icp->ev_mid) != hipSuccess))
+                hipEventCreate(&icp->ev_mid) != hipSuccess || hipEventCreate(&icp->ev_ver) != hipSuccess))
         rc = pcp::set_error(ctx, PCP_ERR_HIP, "hipEventCreate failed");
     if (const char* ab = std::getenv("PCP_ICP_ABLATE")) icp->dbg = std::atoi(ab);
+    if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgcnt, 16);
     if (rc) {
         pcp_icp_destroy(icp);
         return rc;
@@ -969,8 +1397,15 @@ int pcp_icp_destroy(pcp_icp* icp) {
     pcp::dfree(icp->ctx, icp->q);
     pcp::dfree(icp->ctx, icp->partials);
     pcp::dfree(icp->ctx, icp->acc);
-    pcp::dfree(icp->ctx, icp->win);
-    pcp::dfree(icp->ctx, icp->wd2);
+    pcp::dfree(icp->ctx, icp->cand);
+    pcp::dfree(icp->ctx, icp->dlb);
+    pcp::dfree(icp->ctx, icp->pose_hist);
+    pcp::dfree(icp->ctx, icp->sv);
+    pcp::dfree(icp->ctx, icp->sv_count);
+    pcp::dfree(icp->ctx, icp->sv_off);
+    pcp::dfree(icp->ctx, icp->svc);
+
+    pcp::dfree(icp->ctx, icp->dbgcnt);
     pcp::dfree(icp->ctx, icp->fb);
     pcp::dfree(icp->ctx, icp->fb_count);
     pcp::dfree(icp->ctx, icp->fb_off);
@@ -979,6 +1414,7 @@ int pcp_icp_destroy(pcp_icp* icp) {
     if (icp->ev0) (void)hipEventDestroy(icp->ev0);
     if (icp->ev1) (void)hipEventDestroy(icp->ev1);
     if (icp->ev_mid) (void)hipEventDestroy(icp->ev_mid);
+    if (icp->ev_ver) (void)hipEventDestroy(icp->ev_ver);
     for (auto& pr : icp->tev) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -995,17 +1431,33 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
     PCP_TRY(pcp::icp_launch(icp, T, rmax, acc_dev, corr_idx, corr_d2));
     double fbn = 0.0;
     PCP_HIP(ctx, hipMemcpyAsync(&fbn, acc_dev + 23, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    uint32_t nsv = (uint32_t)icp->nq;  // sparse grid / first launch: every query is searched
+    if (icp->last_verified)
+        PCP_HIP(ctx, hipMemcpyAsync(&nsv, icp->sv_off + (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64), sizeof(nsv),
+                                    hipMemcpyDeviceToHost, ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     icp->last_fallback = (uint32_t)fbn;
+    icp->last_searched = nsv;
     float ms = 0.f;
     PCP_HIP(ctx, hipEventElapsedTime(&ms, icp->ev0, icp->ev1));
     icp->last_ms = ms;
     icp->last_launches = 1;
     if (icp->dbg) {
-        float m1 = 0.f;
+        float m1 = 0.f, mv = 0.f;
         (void)hipEventElapsedTime(&m1, icp->ev0, icp->ev_mid);
-        std::fprintf(stderr, "[pcp icp dbg=%d] octant %.4f ms  fallback %.4f ms  n_fallback %u\n", icp->dbg, m1,
-                     ms - m1, icp->last_fallback);
+        (void)hipEventElapsedTime(&mv, icp->ev0, icp->ev_ver);
+        std::fprintf(stderr, "[pcp icp dbg=%d] verify %.4f ms  octant %.4f ms  fallback %.4f ms  searched %u  "
+                     "n_fallback %u\n", icp->dbg, mv, m1 - mv, ms - m1, nsv, icp->last_fallback);
+        if (icp->dbgcnt) {
+            unsigned long long c[16];
+            PCP_HIP(ctx, hipMemcpy(c, icp->dbgcnt, sizeof(c), hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "[pcp icp dbg] octant candidates/query %.2f  rows/query %.2f  wave max/chunk %.2f\n",
+                         (double)c[0] / (double)(c[2] ? c[2] : 1), (double)c[1] / (double)(c[2] ? c[2] : 1),
+                         (double)c[3] * 64.0 / (double)(c[2] ? c[2] : 1));
+            std::fprintf(stderr, "[pcp icp dbg] L histogram (bins of 4):");
+            for (int k = 4; k < 16; k++) std::fprintf(stderr, " %.3f", (double)c[k] / (double)(c[2] ? c[2] : 1));
+            std::fprintf(stderr, "\n");
+        }
     }
     return PCP_OK;
 }
@@ -1019,16 +1471,16 @@ int pcp_icp_keys(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, int
     icp->ctx = ctx;
     const int saved = icp->dbg;
     icp->dbg |= pcp::kDbgNoAccum;  // correspondences only
-    const int rc = pcp::icp_launch(icp, T, rmax, icp->acc, nullptr, nullptr);
+    pcp::IcpArgs a{};
+    const int rc = pcp::icp_launch(icp, T, rmax, icp->acc, nullptr, nullptr, nullptr, &a);
     icp->dbg = saved;
     PCP_TRY(rc);
     if (icp->nq_in > icp->nq)
         hipLaunchKernelGGL(pcp::k_fill_keys, dim3(pcp::grid_for(icp->nq_in, 256)), dim3(256), 0, ctx->stream, keys_dev,
                            icp->nq_in);
     if (icp->nq > 0)
-        hipLaunchKernelGGL(pcp::k_make_keys, dim3(pcp::grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, icp->q,
-                           (const int32_t*)icp->win, (const float*)icp->wd2, icp->nq, (uint32_t)target_offset,
-                           keys_dev);
+        hipLaunchKernelGGL(pcp::k_make_keys, dim3(pcp::grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, a,
+                           (uint32_t)target_offset, keys_dev);
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }
@@ -1152,6 +1604,12 @@ int pcp_icp_kernel_ms(pcp_ctx* ctx, pcp_icp* icp, double* ms, int* launches) {
 int pcp_icp_last_fallback(const pcp_icp* icp, int64_t* n) {
     if (!icp || !n) return PCP_ERR_ARG;
     *n = icp->last_fallback;
+    return PCP_OK;
+}
+
+int pcp_icp_last_searched(const pcp_icp* icp, int64_t* n) {
+    if (!icp || !n) return PCP_ERR_ARG;
+    *n = icp->last_searched;
     return PCP_OK;
 }
 

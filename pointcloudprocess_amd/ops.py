@@ -331,6 +331,12 @@ class ICP:
         self.ctx.check(self.ctx.lib.pcp_icp_last_kernel_ms(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def last_searched(self):
+        """Queries of the last step the verify pass could not settle (they were searched)."""
+        n = C.c_int64()
+        self.ctx.check(self.ctx.lib.pcp_icp_last_searched(self.h, C.byref(n)))
+        return n.value
+
     def last_fallback(self):
         n = C.c_int64()
         self.ctx.check(self.ctx.lib.pcp_icp_last_fallback(self.h, C.byref(n)))

@@ -58,6 +58,48 @@ def test_correspondence_bit_exact(ctx, cell):
         assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * scale)
 
 
+def test_verify_pass_exact_over_registration(ctx):
+    # The verify pass settles a query from its previous winner and lower bound (triangle
+    # inequality); it must return exactly what an exhaustive search returns, at every
+    # iteration of a registration, on a repeated pose, and after a jump back to the start.
+    from pointcloudprocess_amd import ops, synth
+    T_true = synth.rigid()
+    tgt, q = _pair(200_000, 31, T_true)
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+    icp = ops.ICP(index, q.to(ctx.device))
+    oi = ora.F32Index(tgt.numpy())
+    T = np.eye(4)
+    searched = []
+    poses = []
+    for it in range(12):
+        acc, ci, cd = icp.step(T, 0.25, corr=True)
+        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+        ei, ed = oi.correspond(q.numpy(), R, t, 0.25)
+        gi = ci.cpu().numpy()
+        assert np.array_equal(gi, ei), f"iter {it}: {(gi != ei).sum()} mismatching correspondences"
+        assert np.array_equal(cd.cpu().numpy()[ei >= 0], ed[ei >= 0])
+        searched.append(icp.last_searched())
+        poses.append(T)
+        rc, dT = ops.icp_solve(acc.cpu().numpy())
+        assert rc == 0
+        T = dT @ T
+    assert searched[0] == q.shape[0]            # nothing to verify at the first launch
+    assert searched[-1] < 0.75 * q.shape[0], searched  # settled ones skip the search
+    # the same pose again: every settled query verifies (zero motion)
+    _, ci, _ = icp.step(poses[-1], 0.25, corr=True)
+    R, t = poses[-1][:3, :3].astype(np.float32), poses[-1][:3, 3].astype(np.float32)
+    ei, _ = oi.correspond(q.numpy(), R, t, 0.25)
+    assert np.array_equal(ci.cpu().numpy(), ei)
+    # a jump back to the identity: the bounds no longer hold for most queries
+    _, ci, _ = icp.step(np.eye(4), 0.25, corr=True)
+    ei, _ = oi.correspond(q.numpy(), np.eye(3, dtype=np.float32), np.zeros(3, np.float32), 0.25)
+    assert np.array_equal(ci.cpu().numpy(), ei)
+    # a smaller rmax than the bounds were made with
+    _, ci, _ = icp.step(poses[-1], 0.02, corr=True)
+    ei, _ = oi.correspond(q.numpy(), R, t, 0.02)
+    assert np.array_equal(ci.cpu().numpy(), ei)
+
+
 def test_ties_lattice(ctx):
     from pointcloudprocess_amd import ops
     # integer lattice target + half-integer queries: every query has 8 equidistant targets
@@ -66,9 +108,10 @@ def test_ties_lattice(ctx):
     q = (tgt[:500] + 0.5).astype(np.float32)
     index = ops.GridIndex(ctx, torch.from_numpy(tgt).to(ctx.device), cell_size=1.0)
     icp = ops.ICP(index, torch.from_numpy(q).to(ctx.device))
-    _, ci, cd = icp.step(np.eye(4), 1.0, corr=True)
     ei, ed = ora.F32Index(tgt).correspond(q, np.eye(3), np.zeros(3), 1.0)
-    assert np.array_equal(ci.cpu().numpy(), ei)
+    for _ in range(2):  # the second launch starts from the first one's winners and bounds
+        _, ci, cd = icp.step(np.eye(4), 1.0, corr=True)
+        assert np.array_equal(ci.cpu().numpy(), ei)
 
 
 def test_far_queries_rejected_and_failure(ctx):
@@ -122,11 +165,19 @@ def test_device_loop_matches_oracle_and_host_loop(ctx):
     eerr, eT = ora.icp(tgt.numpy(), q.numpy(), np.eye(4), 0.25, 20)
     assert abs(st[1] - eerr) < 1e-5
     assert np.abs(T - eT).max() < 1e-5
-    # the same iterations through step_dev + solve_dev equal run_dev exactly
-    T2, st2 = icp.new_pose()
+    # the same iterations through step_dev + solve_dev equal run_dev exactly on a fresh engine
+    # (the accumulators' summation order follows which pass -- verify, search or fallback --
+    # settled each query, and that depends on the engine's carried winners and bounds)
+    icp2 = ops.ICP(index, q.to(ctx.device))
+    T2, st2 = icp2.new_pose()
     for _ in range(20):
-        icp.solve_dev(icp.step_dev(T2, 0.25), T2, st2)
+        icp2.solve_dev(icp2.step_dev(T2, 0.25), T2, st2)
     assert torch.equal(T2, T_dev) and torch.equal(st2, stats)
+    icp2.close()
+    # a warm engine (carried state) gives the same correspondences: poses equal to rounding
+    T3, st3 = icp.new_pose()
+    icp.run_dev(T3, st3, 0.25, 20)
+    assert (T3 - T_dev).abs().max().item() < 1e-7 and st3[3].item() == 20
     # and the host loop (host solve): same arithmetic, but a last-bit difference of the fp64
     # solve can flip the fp32 cast of the pose and with it a few correspondences
     herr, hT = icp.run(np.eye(4), 0.25, 20)

@@ -1,0 +1,7 @@
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/${TAG:-r13d}; mkdir -p $O
+for ab in ${ABL:-32 36 37 33}; do
+PCP_ICP_ABLATE=$ab timeout -k 10 200 python3 tools/icp_micro.py --reps 1 > $O/micro_$ab.log 2>&1
+done
+echo done

@@ -1,5 +1,6 @@
 """Micro-benchmark of one ICP correspondence iteration (profiling aid, not part of the
-product).  Builds the C4 workload once, then times pcp_icp_step at a few poses; set
+product).  Builds the C4 workload once, then times a host-loop registration (pcp_icp_step +
+host solve per iteration) from the identity; set
 PCP_ICP_ABLATE=<flags> to time ablated kernels (results are then meaningless)."""
 import argparse
 import os
@@ -16,7 +17,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=50_000_000)
 ap.add_argument("--cell", type=float, default=0.1)
 ap.add_argument("--rmax", type=float, default=0.25)
-ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--iters", type=int, default=20)
 args = ap.parse_args()
 
 ctx = ops.Context(0)
@@ -28,8 +30,18 @@ index = ops.GridIndex(ctx, tgt, cell_size=args.cell)
 icp = ops.ICP(index, q)
 torch.cuda.synchronize()
 print(f"build+sort {1e3 * (time.perf_counter() - t0):.1f} ms  cells {ctx.lib.pcp_index_cells(index.h)}", flush=True)
-for name, T in (("identity", np.eye(4)), ("truth", T_true)):
-    for r in range(args.reps):
-        icp.step(T, args.rmax)
+ap2 = None
+for rep in range(args.reps):
+    T = np.eye(4)
+    tot = 0.0
+    for it in range(args.iters):
+        acc = icp.step(T, args.rmax)
         ms, _ = icp.last_kernel_ms()
-        print(f"{name} rep{r}: {ms:.4f} ms  fallback {icp.last_fallback()}", flush=True)
+        tot += ms
+        rc, dT = ops.icp_solve(acc.cpu().numpy())
+        print(f"rep{rep} iter{it}: {ms:.4f} ms  fallback {icp.last_fallback()}", flush=True)
+        if rc != 0:
+            break
+        T = dT @ T
+    print(f"rep{rep}: {tot:.3f} ms over {args.iters} iterations ({tot / args.iters:.4f} ms/iter)  "
+          f"|T-T_true| {np.abs(T - T_true).max():.2e}", flush=True)
