@@ -37,8 +37,9 @@ METRIC = "Mcorrespondences/s + ICP iter/s, 50M-vs-50M fp32 @ 1/2/4/8 MI355X"
 
 
 def pmc_traffic():
-    """HBM bytes per ICP iteration (k_icp_octant + k_icp_ring, FETCH_SIZE x2 + WRITE_SIZE) from
-    the newest profiles/*/pmc_traffic.json measured on THIS icp.hip (sha1 match), else None.
+    """HBM bytes per ICP iteration (k_icp_verify + k_icp_octant + k_icp_ring, FETCH_SIZE x2 +
+    WRITE_SIZE, summed over the profiled launches / iterations) from the newest
+    profiles/*/pmc_traffic.json measured on THIS icp.hip (sha1 match), else None.
     Made by: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) of
     `bench.py --steps 1 --warmup 0 --no-cpu`, summarised by tools/pmc_summary.py."""
     src = os.path.join(ROOT, "pointcloudprocess_amd", "csrc", "icp.hip")
@@ -51,13 +52,16 @@ def pmc_traffic():
             continue
         if d.get("icp_hip_sha1") != sha:
             continue
+        ks = d["kernels"]
+        if "k_icp_octant" not in ks:
+            return None
+        iters = ks["k_icp_octant"]["launches"]
         tot = 0.0
-        for k in ("k_icp_octant", "k_icp_ring"):
-            e = d["kernels"].get(k)
-            if e is None:
-                return None
-            tot += e["fetch_bytes_avg"] + (e["write_bytes_avg"] or 0.0)
-        return tot, os.path.relpath(f, ROOT)
+        for k in ("k_icp_verify", "k_icp_octant", "k_icp_ring"):
+            e = ks.get(k)
+            if e is not None:
+                tot += e["launches"] * (e["fetch_bytes_avg"] + (e["write_bytes_avg"] or 0.0))
+        return tot / iters, os.path.relpath(f, ROOT)
     return None
 
 
@@ -229,7 +233,8 @@ def main():
                 "kernel_avg_ms": round(k_avg_ms, 4),
                 "bytes_per_unit": BYTES_PER_CORR,
                 "units_per_launch": n,
-                "launch_includes": "k_icp_octant + k_icp_ring (fallback) per iteration",
+                "launch_includes": "per iteration: k_icp_verify (candidate caches) + k_icp_octant (search "
+                                   "list) + k_icp_ring (fallback) with their list compactions",
                 "fallback_frac": round(kernel.get("fallback", 0) / max(1, n * kernel["launches"]), 5),
             },
             "cpu_baseline": None if args.no_cpu else cpu_baseline(args, T_true),

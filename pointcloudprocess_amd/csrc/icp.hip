@@ -412,7 +412,12 @@ struct LaneAcc {
 // relative margins far above the fp32 rounding of d2), it is the exact 1-NN under the
 // contract -- the same (d2, index) winner an exhaustive search returns, cached ties included
 // -- and the query is settled without a search; the bound moves to D - Delta.
-constexpr int kCache = 4;
+#ifndef PCP_CACHE3
+#define PCP_CACHE3 1
+#endif
+// kCache = 3: cand = {3 positions, dlb word} (one 16-byte record per query); 4: cand = 4 positions
+// and a separate dlb array
+constexpr int kCache = PCP_CACHE3 ? 3 : 4;
 
 // the cached candidates' winner under the current pose, by (d2, target index)
 struct CacheBest {
@@ -422,7 +427,7 @@ struct CacheBest {
     float4 P = make_float4(0.f, 0.f, 0.f, 0.f);
 };
 __device__ __forceinline__ CacheBest cache_best(const float4* tp, const uint4 cd, float qx, float qy, float qz) {
-    const uint32_t c[kCache] = {cd.x, cd.y, cd.z, cd.w};
+    const uint32_t c[4] = {cd.x, cd.y, cd.z, cd.w};  // with kCache = 3, .w is the dlb word
     float4 p[kCache];
 #pragma unroll
     for (int s = 0; s < kCache; s++) p[s] = c[s] != ~0u ? tp[c[s]] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -488,7 +493,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
         if (c < ce && i < a.nq) {
             q = a.q[i];
             cd = a.cand[i];
-            D = a.dlb[i];
+            D = PCP_CACHE3 ? cd.w : a.dlb[i];
         } else {
             q = make_float4(0.f, 0.f, 0.f, 0.f);
             cd = none;
@@ -500,7 +505,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
         p0 = ld16(a.tp, min(cd.x, a.ntp));
         p1 = ld16(a.tp, min(cd.y, a.ntp));
         p2 = ld16(a.tp, min(cd.z, a.ntp));
-        p3 = ld16(a.tp, min(cd.w, a.ntp));
+        p3 = PCP_CACHE3 ? ld16(a.tp, a.ntp) : ld16(a.tp, min(cd.w, a.ntp));
     };
     float4 q1, q2;
     uint4 c1_, c2_;
@@ -547,7 +552,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             take(p0);
             take(p1);
             take(p2);
-            take(p3);
+            if (!PCP_CACHE3) take(p3);
             // the query at the pose of its last search
             const uint32_t sl = Dw & 0xffu;
             const float4 A = s_pose[sl][0], B = s_pose[sl][1], C = s_pose[sl][2];
@@ -630,6 +635,50 @@ struct Top4 {
     }
 };
 
+// running 3-NN (kCache = 3): d0 <= d1 <= d2 with positions, d3 = the 4th smallest d2 scanned
+struct Top3 {
+    float d0 = INFINITY, d1 = INFINITY, d2 = INFINITY, d3 = INFINITY;
+    uint32_t p0 = ~0u, p1 = ~0u, p2 = ~0u;
+    __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t k) {
+        const float x = icp_d2(qx, qy, qz, p);
+        const bool c0 = x < d0, c1 = x < d1, c2 = x < d2;
+        d3 = __builtin_amdgcn_fmed3f(d2, d3, x);
+        p2 = c1 ? p1 : (c2 ? k : p2);
+        d2 = __builtin_amdgcn_fmed3f(d1, d2, x);
+        p1 = c0 ? p0 : (c1 ? k : p1);
+        d1 = __builtin_amdgcn_fmed3f(d0, d1, x);
+        p0 = c0 ? k : p0;
+        d0 = fminf(d0, x);
+    }
+    __device__ __forceinline__ void scan4(const float4* pts, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
+                                          float qx, float qy, float qz) {
+        const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
+        const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
+        auto addr = [&](uint32_t v) {
+            uint32_t o = v < c3 ? o2 : o3;
+            o = v < c2 ? o1 : o;
+            o = v < c1 ? o0 : o;
+            return v + o;
+        };
+        constexpr int U = PCP_SCAN_UNROLL;
+        uint32_t v = 0;
+        for (; v + U <= L; v += U) {
+            uint32_t k[U];
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) k[u] = addr(v + u);
+#pragma unroll
+            for (int u = 0; u < U; u++) p[u] = pts[k[u]];
+#pragma unroll
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, p[u], k[u]);
+        }
+        for (; v < L; v++) {
+            const uint32_t k = addr(v);
+            consider(qx, qy, qz, pts[k], k);
+        }
+    }
+};
+
 // ---- search pass (the verify pass's list; every query at the first launch)
 // One query per lane, 64-query chunks grid-stride over the list.  Each query scans its whole
 // 2x2x2 "octant" block of cells (the four x-rows [floor(f - 1/2), +1]) keeping its 4 nearest.
@@ -665,7 +714,11 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             in_ = list ? (int64_t)list[j + 64 * nwaves] : j + 64 * nwaves;
             qn = a.q[in_];
         }
+#if PCP_CACHE3
+        Top3 b;
+#else
         Top4 b;
+#endif
         float qx = 0.f, qy = 0.f, qz = 0.f;
         bool settled = false, found = false;
         uint32_t win = ~0u;
@@ -699,24 +752,38 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             const float rr = m * g.hf;
             const float cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
             found = b.d0 <= a.r2;
-            settled = (found ? (b.d0 < b.d4 && b.d0 <= cert2) : a.r2 <= cert2) || (a.dbg & kDbgNoFallback);
+#if PCP_CACHE3
+            const float dnext = b.d3;  // the first uncached d2
+#else
+            const float dnext = b.d4;
+#endif
+            settled = (found ? (b.d0 < dnext && b.d0 <= cert2) : a.r2 <= cert2) || (a.dbg & kDbgNoFallback);
             // the winner among the cached ties by target index (rare: only when d1 == d0)
             win = b.p0;
             if (found && b.d1 == b.d0) {
                 int wj = __float_as_int(a.tp[b.p0].w);
+#if PCP_CACHE3
+                const uint32_t ps[2] = {b.p1, b.p2};
+                const float ds[2] = {b.d1, b.d2};
+#else
                 const uint32_t ps[3] = {b.p1, b.p2, b.p3};
                 const float ds[3] = {b.d1, b.d2, b.d3};
+#endif
 #pragma unroll
-                for (int s2 = 0; s2 < 3; s2++) {
+                for (int s2 = 0; s2 < kCache - 1; s2++) {
                     if (ds[s2] != b.d0) break;
                     const int id = __float_as_int(a.tp[ps[s2]].w);
                     if (id < wj) { wj = id; win = ps[s2]; }
                 }
             }
             // the cache: the 4 nearest; D bounds every uncached point
-            const float D = fminf(sqrtf(b.d4), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f;
+            const float D = fminf(sqrtf(dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f;
+#if PCP_CACHE3
+            a.cand[i] = make_uint4(b.p0, b.p1, b.p2, pack_dlb(D, a.launch));
+#else
             a.cand[i] = make_uint4(b.p0, b.p1, b.p2, b.p3);
             a.dlb[i] = pack_dlb(D, a.launch);
+#endif
         }
         // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
         const bool fb = valid && !settled;
@@ -804,8 +871,13 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
             }
             if (!done) box_search(a.g, a.tp, qx, qy, qz, a.mc, b);
             const bool ok = b.bj != 0x7fffffff;
+            // no bound kept: the next launch searches it again
+#if PCP_CACHE3
+            a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, pack_dlb(0.f, a.launch));
+#else
             a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, ~0u);
-            a.dlb[i] = pack_dlb(0.f, a.launch);  // no bound kept: the next launch searches it again
+            a.dlb[i] = pack_dlb(0.f, a.launch);
+#endif
         }
         const bool acc_ok = valid && b.bj != 0x7fffffff && !(a.dbg & kDbgNoAccum);
         if (acc_ok) b.fetch(a.tp);

@@ -26,7 +26,7 @@ def per_kernel(path, counter):
 
 def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
-    keys = sys.argv[3:] or ["k_icp_octant", "k_icp_ring"]
+    keys = sys.argv[3:] or ["k_icp_verify", "k_icp_octant", "k_icp_ring"]
     f, w = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
     out = {"source": f"{fdir}, {wdir}", "fetch_correction": 2.0, "kernels": {}}
     for k in keys:
