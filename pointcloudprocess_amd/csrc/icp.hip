@@ -341,6 +341,26 @@ __device__ __forceinline__ void chunk_accumulate(bool ok, float qx, float qy, fl
     }
 }
 
+// XCD-blocked work split: workgroups are dealt round-robin over the 8 XCDs, so workgroup b
+// runs on XCD b % 8.  The 64-query chunks [0, nch) are cut into np = min(8, grid) contiguous
+// parts, one per XCD, and each part is handed out grid-stride to that XCD's waves: spatially
+// adjacent chunks then share one L2 (their cell rows and target points) instead of being
+// fetched once per XCD.
+struct XcdSplit {
+    int64_t c0, c1, w, nw;  // this wave's part [c0, c1), its index and the part's wave count
+};
+__device__ __forceinline__ XcdSplit xcd_split(int64_t nch, int kW) {
+    const int np = min(8, (int)gridDim.x);
+    const int part = (int)(blockIdx.x % np);
+    const int64_t nblk = ((int64_t)gridDim.x - part + np - 1) / np;  // workgroups of this part
+    XcdSplit x;
+    x.c0 = part * nch / np;
+    x.c1 = (part + 1) * nch / np;
+    x.w = (int64_t)(blockIdx.x / np) * kW + (threadIdx.x >> 6);
+    x.nw = nblk * kW;
+    return x;
+}
+
 __device__ __forceinline__ void write_wave_partials(double (*s_acc)[kAcc], double* out) {
     __syncthreads();
     if (threadIdx.x < kAcc) {
@@ -695,17 +715,17 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
     const GridDesc& g = a.g;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;  // global wave id = fallback segment
-    const int64_t nwaves = (int64_t)gridDim.x * kW;
     const int64_t n = list ? (int64_t)*list_n : a.nq;
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
     uint32_t fbn = 0;  // wave-uniform count of this wave's fallback entries
+    const int64_t nwaves = (int64_t)gridDim.x * kW;
     int64_t in_ = 0;
     float4 qn = make_float4(0.f, 0.f, 0.f, 0.f);
     if (gw * 64 + lane < n) {
         in_ = list ? (int64_t)list[gw * 64 + lane] : gw * 64 + lane;
         qn = a.q[in_];
     }
-    for (int64_t c = gw; c * 64 < n; c += nwaves) {
+    for (int64_t c = gw; c * 64 < n; c += nwaves) {  // grid-stride (an XCD split measured slower here)
         const int64_t j = c * 64 + lane;
         const bool valid = j < n;
         const int64_t i = in_;
@@ -777,7 +797,9 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
                 }
             }
             // the cache: the 4 nearest; D bounds every uncached point
-            const float D = fminf(sqrtf(dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f;
+            // settled: D bounds every uncached point for the verify pass.  Unsettled: the fallback
+            // pass (which overwrites the cache) gets the octant's first uncached d2 instead.
+            const float D = settled ? fminf(sqrtf(dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : dnext;
 #if PCP_CACHE3
             a.cand[i] = make_uint4(b.p0, b.p1, b.p2, pack_dlb(D, a.launch));
 #else
@@ -819,8 +841,8 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
     const int64_t n = a.ring_all ? a.nq : (int64_t)*list_n;
-    const int64_t gw = (int64_t)blockIdx.x * kW + wid, nwaves = (int64_t)gridDim.x * kW;
-    for (int64_t c = gw; c * 64 < n; c += nwaves) {
+    const XcdSplit xs = xcd_split((n + 63) / 64, kW);
+    for (int64_t c = xs.c0 + xs.w; c < xs.c1; c += xs.nw) {
         const int64_t j = c * 64 + lane;
         const bool valid = j < n;
         Best b{a.r2, 0x7fffffff, 0u, 0.f, 0.f, 0.f};
@@ -829,37 +851,59 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
         if (valid) {
             i = a.ring_all ? j : list[j];
             xform(a, a.q[i], qx, qy, qz);
-            {  // provisional: the cache's best (refreshed by the search pass), an upper bound
-                const CacheBest cbst = cache_best(a.tp, a.cand[i], qx, qy, qz);
-                if (cbst.bd <= b.bd) {
-                    b.bd = cbst.bd;
-                    b.bj = cbst.bj;
-                    b.bk = cbst.bk;
-                }
+            // provisional: the cache's best (refreshed by the search pass), an upper bound
+            const uint4 cd = a.cand[i];
+            const CacheBest cbst = cache_best(a.tp, cd, qx, qy, qz);
+            if (cbst.bd <= b.bd) {
+                b.bd = cbst.bd;
+                b.bj = cbst.bj;
+                b.bk = cbst.bk;
             }
+            // the search pass left this launch's octant message: the 4th smallest d2 of its
+            // octant.  Above the cached best, every octant point tied with that best is cached,
+            // so the cached best IS the octant's (d2, index) winner and its cells need no rescan.
+#if PCP_CACHE3
+            const uint32_t msg = cd.w;
+#else
+            const uint32_t msg = a.dlb[i];
+#endif
+            const bool skip_oct = !a.ring_all && ((msg ^ a.launch) & 0xffu) == 0u &&
+                                  __uint_as_float(msg & ~0xffu) > cbst.bd;
             bool done = false;
             if (!a.ring_all) {
-                // stage 2: the 3x3x3 cells around the query, as 3 planes of 3 x-rows scanned
-                // like the octant pass; certifies any winner within the distance to the
-                // block's faces (>= 1 cell).  Only what is left goes to the general search.
+                // stage 2: the 3x3x3 cells around the query (less the octant's when it was
+                // searched completely), rows and end cells pruned by the bound, as 3 planes of 3
+                // x-rows scanned like the octant pass; certifies any winner within the distance
+                // to the block's faces (>= 1 cell).  Only what is left goes to the general search.
                 const GridDesc& g = a.g;
                 const float fx = cell_f<float>(g, qx, 0), fy = cell_f<float>(g, qy, 1), fz = cell_f<float>(g, qz, 2);
                 const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
-                const int xa = max(cx - 1, 0), xb = min(cx + 1, g.n[0] - 1);
-                if (xa <= xb) {
-                    for (int dz = -1; dz <= 1; dz++) {
-                        const int z = cz + dz;
-                        uint32_t rs[3], rn[3];
+                const float lx = fx - (float)cx, ly = fy - (float)cy, lz = fz - (float)cz;
+                const int bxo = (int)floorf(fx - a.rho), byo = (int)floorf(fy - a.rho), bzo = (int)floorf(fz - a.rho);
+                const float inv_h2 = g.inv_hf * g.inv_hf;
+                const float gxl = sq_gap(lx, a.mc), gxr = sq_gap(1.f - lx, a.mc);
+                for (int dz = -1; dz <= 1; dz++) {
+                    const int z = cz + dz;
+                    const float lim = b.bd * 1.00002f * inv_h2;  // the bound in cells^2 (shrinks)
+                    const float gz2 = sq_gap(axis_gap<float>(z, cz, lz), a.mc);
+                    uint32_t rs[3], rn[3];
 #pragma unroll
-                        for (int r = 0; r < 3; r++) {
-                            const int y = cy - 1 + r;
-                            const bool in = y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
-                            const int64_t cc = in ? dense_id(g, xa, y, z) : 0;
-                            rs[r] = in ? g.cstart[cc] : 0u;
-                            rn[r] = in ? g.cstart[cc + (xb - xa + 1)] - rs[r] : 0u;
+                    for (int r = 0; r < 3; r++) {
+                        const int y = cy - 1 + r;
+                        const float gyz = gz2 + sq_gap(axis_gap<float>(y, cy, ly), a.mc);
+                        int xlo = max(cx - 1, 0), xhi = min(cx + 1, g.n[0] - 1);
+                        if (skip_oct && y >= byo && y <= byo + 1 && z >= bzo && z <= bzo + 1) {
+                            if (bxo == cx - 1) xlo = max(xlo, cx + 1);
+                            else xhi = min(xhi, cx - 1);
                         }
-                        b.scan_rows(a.tp, rs, rn, qx, qy, qz);
+                        if (xlo == cx - 1 && gyz + gxl > lim) xlo = cx;
+                        if (xhi == cx + 1 && gyz + gxr > lim) xhi = cx;
+                        const bool in = y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2] && gyz <= lim && xlo <= xhi;
+                        const int64_t cc = in ? dense_id(g, xlo, y, z) : 0;
+                        rs[r] = in ? g.cstart[cc] : 0u;
+                        rn[r] = in ? g.cstart[cc + (xhi - xlo + 1)] - rs[r] : 0u;
                     }
+                    b.scan_rows(a.tp, rs, rn, qx, qy, qz);
                 }
                 const float m = fminf(fminf(fminf(fx - (float)(cx - 1), (float)(cx + 2) - fx),
                                             fminf(fy - (float)(cy - 1), (float)(cy + 2) - fy)),
@@ -869,7 +913,9 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
                 const bool found = b.bj != 0x7fffffff;
                 done = (found && b.bd <= c2) || (!found && a.r2 <= c2);
             }
+            if ((a.dbg & kDbgCount) && done) atomicAdd(a.dbgcnt + 5, 1ull);
             if (!done) box_search(a.g, a.tp, qx, qy, qz, a.mc, b);
+            if ((a.dbg & kDbgCount) && b.bj != 0x7fffffff) atomicAdd(a.dbgcnt + 6, 1ull);
             const bool ok = b.bj != 0x7fffffff;
             // no bound kept: the next launch searches it again
 #if PCP_CACHE3
@@ -1526,6 +1572,8 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
             std::fprintf(stderr, "[pcp icp dbg] octant candidates/query %.2f  rows/query %.2f  wave max/chunk %.2f\n",
                          (double)c[0] / (double)(c[2] ? c[2] : 1), (double)c[1] / (double)(c[2] ? c[2] : 1),
                          (double)c[3] * 64.0 / (double)(c[2] ? c[2] : 1));
+            std::fprintf(stderr, "[pcp icp dbg] fallback: settled by the 3x3x3 stage %llu, with a correspondence %llu\n",
+                         c[5], c[6]);
             std::fprintf(stderr, "[pcp icp dbg] L histogram (bins of 4):");
             for (int k = 4; k < 16; k++) std::fprintf(stderr, " %.3f", (double)c[k] / (double)(c[2] ? c[2] : 1));
             std::fprintf(stderr, "\n");
