@@ -194,16 +194,24 @@ __global__ void __launch_bounds__(256) k_cell_starts(const uint32_t* __restrict_
     if (lane == 63) after = p1;
     __syncthreads();
     for (int w = wid + 1; w < 4; w++) after = min(after, s_wmin[w]);
-    const int64_t c = c0 + kPer * t;
+    // back through LDS, so every 16-byte store instruction of a wave covers 1 KB contiguously
+    __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kPer; j += 4) {
-        const uint4 o = make_uint4(min(v[j], after), min(v[j + 1], after), min(v[j + 2], after), min(v[j + 3], after));
-        if (c + j + 3 < ncells1) {
-            *(uint4*)&cstart[c + j] = o;
+    for (int j = 0; j < kPer; j += 4)
+        *(uint4*)&s[kPer * t + j] = make_uint4(min(v[j], after), min(v[j + 1], after), min(v[j + 2], after),
+                                               min(v[j + 3], after));
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer / 4; k++) {
+        const int e = 4 * (k * 256 + t);  // element offset in the chunk
+        const uint4 o = *(const uint4*)&s[e];
+        const int64_t c = c0 + e;
+        if (c + 3 < ncells1) {
+            *(uint4*)&cstart[c] = o;
         } else {
-            if (c + j < ncells1) cstart[c + j] = o.x;
-            if (c + j + 1 < ncells1) cstart[c + j + 1] = o.y;
-            if (c + j + 2 < ncells1) cstart[c + j + 2] = o.z;
+            if (c < ncells1) cstart[c] = o.x;
+            if (c + 1 < ncells1) cstart[c + 1] = o.y;
+            if (c + 2 < ncells1) cstart[c + 2] = o.z;
         }
     }
 }
@@ -434,8 +442,10 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
                     PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u,
                                                            bits, st));
             } else {
+                // no brick marks: the fp32 index serves ICP only, whose dense-grid searches never
+                // read brick occupancy (its brick table stays all-zero = "occupied")
                 hipLaunchKernelGGL(k_cell_keys_rec, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const float*)cxyz,
-                                   (const int32_t*)ix->mapping, n, skey, rec0, g.dense ? ix->brick : nullptr);
+                                   (const int32_t*)ix->mapping, n, skey, rec0, nullptr);
                 PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, rec0, (float4*)ix->pts,
                                                        (size_t)n, 0u, bits, st));
                 if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
@@ -448,7 +458,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             if (!is_f64)  // pts[n]: a point at infinity (d2 = inf from any finite query) for gathers
                 hipLaunchKernelGGL(k_far_sentinel, dim3(1), dim3(1), 0, st, (float4*)ix->pts, n);
         }
-        if (g.dense)
+        if (g.dense && is_f64)
             hipLaunchKernelGGL(k_brick_flag, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks);
         // ---- chunk boundaries of the sorted keys (+ the number of non-empty cells)
         const int64_t nchunk = (ncells + 1 + kChunk - 1) / kChunk;
