@@ -62,7 +62,7 @@ namespace {
 
 constexpr int kIcpBlock = 256;
 #ifndef PCP_OCT_WAVES
-#define PCP_OCT_WAVES 8
+#define PCP_OCT_WAVES 6
 #endif
 #ifndef PCP_VER_WAVES   // tier-1 verify (per-lane accumulators: ~100 VGPRs)
 #define PCP_VER_WAVES 4

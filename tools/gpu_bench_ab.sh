@@ -5,7 +5,7 @@ O=gpurun_out/${TAG:-benchab}; mkdir -p $O
 if [ -z "$NOTEST" ]; then
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
 fi
-for v in default ${VARIANTS}; do
+for v in ${ORDER:-default ${VARIANTS}}; do
   if [ $v = default ]; then export PCP_LIB=""; else export PCP_LIB=$GRAFT_REPO_ROOT/variants/$v/libpcp.so; fi
   timeout -k 10 300 python3 bench.py --no-cpu --steps ${STEPS:-3} > $O/bench_$v.json 2> $O/bench_$v.err
 done
