@@ -153,6 +153,16 @@ __device__ __forceinline__ float icp_d2(float qx, float qy, float qz, const floa
     return __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx));
 }
 
+// position of candidate v of four concatenated rows (row prefixes c1 <= c2 <= c3, per-row
+// offsets o0..o3): register selects only (an indexed form was lowered to an LDS table of
+// pointers plus a scratch load per candidate)
+__device__ __forceinline__ uint32_t cat_addr(uint32_t v, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t o0,
+                                             uint32_t o1, uint32_t o2, uint32_t o3) {
+    const uint32_t a = v < c3 ? o2 : o3;
+    const uint32_t b = v < c2 ? o1 : a;
+    return v + (v < c1 ? o0 : b);
+}
+
 struct Best {
     float bd;
     int bj;
@@ -194,10 +204,9 @@ struct Best {
         static_assert(NR == 3 || NR == 4, "3 or 4 rows");
         const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = NR == 4 ? c3 + rn[NR - 1] : c3;
         dbg_len = L;
-        auto addr = [&](uint32_t v) {
-            return v < c1 ? rs[0] + v
-                          : (v < c2 ? rs[1] + (v - c1) : ((NR == 3 || v < c3) ? rs[2] + (v - c2) : rs[NR - 1] + (v - c3)));
-        };
+        const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[NR - 1] - c3;
+        const uint32_t c3e = NR == 4 ? c3 : 0xffffffffu;  // 3 rows: never past the third
+        auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3e, o0, o1, o2, o3); };
         uint32_t v = 0;
         constexpr int U = PCP_SCAN_UNROLL;
         for (; v + U <= L; v += U) {
@@ -630,12 +639,7 @@ struct Top4 {
                                           float qx, float qy, float qz) {
         const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
         const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
-        auto addr = [&](uint32_t v) {
-            uint32_t o = v < c3 ? o2 : o3;
-            o = v < c2 ? o1 : o;
-            o = v < c1 ? o0 : o;
-            return v + o;
-        };
+        auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3, o0, o1, o2, o3); };
         constexpr int U = PCP_SCAN_UNROLL;
         uint32_t v = 0;
         for (; v + U <= L; v += U) {
@@ -674,12 +678,7 @@ struct Top3 {
                                           float qx, float qy, float qz) {
         const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
         const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
-        auto addr = [&](uint32_t v) {
-            uint32_t o = v < c3 ? o2 : o3;
-            o = v < c2 ? o1 : o;
-            o = v < c1 ? o0 : o;
-            return v + o;
-        };
+        auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3, o0, o1, o2, o3); };
         constexpr int U = PCP_SCAN_UNROLL;
         uint32_t v = 0;
         for (; v + U <= L; v += U) {
@@ -1482,11 +1481,12 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     if (!rc) rc = pcp::dmalloc(ctx, &icp->acc, pcp::kAcc);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_dev, 24);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->cand, icp->nq + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->dlb, icp->nq + 1);
+    if (!rc && !PCP_CACHE3) rc = pcp::dmalloc(ctx, &icp->dlb, icp->nq + 1);  // else packed in cand.w
     if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_hist, pcp::kHist * 12);
     if (!rc && (hipMemsetAsync(icp->cand, 0xff, (size_t)(icp->nq + 1) * sizeof(uint4), ctx->stream) != hipSuccess ||
 
-                hipMemsetAsync(icp->dlb, 0, (size_t)(icp->nq + 1) * sizeof(uint32_t), ctx->stream) != hipSuccess ||
+                (icp->dlb && hipMemsetAsync(icp->dlb, 0, (size_t)(icp->nq + 1) * sizeof(uint32_t), ctx->stream) !=
+                                 hipSuccess) ||
                 hipMemsetAsync(icp->pose_hist, 0, pcp::kHist * 12 * sizeof(float), ctx->stream) != hipSuccess ||
                 hipMemsetAsync(icp->pose_dev, 0, 24 * sizeof(float), ctx->stream) != hipSuccess))
         rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
