@@ -64,7 +64,10 @@ constexpr int kIcpBlock = 256;
 #ifndef PCP_OCT_WAVES
 #define PCP_OCT_WAVES 6
 #endif
-#ifndef PCP_VER_WAVES   // tier-1 verify (per-lane accumulators: ~100 VGPRs)
+#ifndef PCP_VER_XCD  // verify work split: 1 = XCD-blocked grid-stride, 0 = contiguous per wave
+#define PCP_VER_XCD 0
+#endif
+#ifndef PCP_VER_WAVES   // verify (per-lane accumulators: ~100 VGPRs)
 #define PCP_VER_WAVES 4
 #endif
 
@@ -505,9 +508,19 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     load_pose(a);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;
-    const int64_t nwaves = (int64_t)gridDim.x * kW;
     const int64_t nch = (a.nq + 63) / 64;
-    const int64_t cb = gw * nch / nwaves, ce = (gw + 1) * nch / nwaves;
+#if PCP_VER_XCD
+    // XCD-blocked grid-stride: the waves of one XCD sweep its eighth of the queries together,
+    // so neighbouring chunks (which share cached targets) run on one L2 at the same time
+    const XcdSplit xs = xcd_split(nch, kW);
+    const int64_t cstart_ = xs.c0 + xs.w, cstep = xs.nw;
+    const int64_t nsteps = cstart_ < xs.c1 ? (xs.c1 - cstart_ + cstep - 1) / cstep : 0;
+#else
+    // contiguous ranges: wave w owns chunks [w*nch/nwaves, (w+1)*nch/nwaves)
+    const int64_t nwaves = (int64_t)gridDim.x * kW;
+    const int64_t cstart_ = gw * nch / nwaves, cstep = 1;
+    const int64_t nsteps = (gw + 1) * nch / nwaves - cstart_;
+#endif
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
     __syncthreads();
     uint32_t svn = 0;
@@ -517,9 +530,9 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     // software pipeline: the query, cache and bound words two chunks ahead, the cached points'
     // gathers one chunk ahead (this chunk's were issued during the previous one)
     const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
-    auto raw = [&](int64_t c, float4& q, uint4& cd, uint32_t& D) {
-        const int64_t i = c * 64 + lane;
-        if (c < ce && i < a.nq) {
+    auto raw = [&](int64_t k, float4& q, uint4& cd, uint32_t& D) {
+        const int64_t i = (cstart_ + k * cstep) * 64 + lane;
+        if (k < nsteps && i < a.nq) {
             q = a.q[i];
             cd = a.cand[i];
             D = PCP_CACHE3 ? cd.w : a.dlb[i];
@@ -534,25 +547,25 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
         p0 = ld16(a.tp, min(cd.x, a.ntp));
         p1 = ld16(a.tp, min(cd.y, a.ntp));
         p2 = ld16(a.tp, min(cd.z, a.ntp));
-        p3 = PCP_CACHE3 ? ld16(a.tp, a.ntp) : ld16(a.tp, min(cd.w, a.ntp));
+        p3 = PCP_CACHE3 ? make_float4(INFINITY, INFINITY, INFINITY, 0.f) : ld16(a.tp, min(cd.w, a.ntp));
     };
     float4 q1, q2;
     uint4 c1_, c2_;
     uint32_t D1, D2;
     float4 g0, g1, g2, g3;
-    raw(cb, q1, c1_, D1);
-    raw(cb + 1, q2, c2_, D2);
+    raw(0, q1, c1_, D1);
+    raw(1, q2, c2_, D2);
     gather(c1_, g0, g1, g2, g3);
-    for (int64_t c0 = cb; c0 < ce; c0 += kFlush) {  // stretches of kFlush chunks
-        const int64_t c1 = min(c0 + (int64_t)kFlush, ce);
+    for (int64_t k0 = 0; k0 < nsteps; k0 += kFlush) {  // stretches of kFlush chunks
+        const int64_t k1 = min(k0 + (int64_t)kFlush, nsteps);
         // centre: the stretch's first query under the current pose (wave-uniform)
         float ccx, ccy, ccz;
-        xform(a, a.q[c0 * 64], ccx, ccy, ccz);
+        xform(a, a.q[(cstart_ + k0 * cstep) * 64], ccx, ccy, ccz);
         ccx = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccx)));
         ccy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccy)));
         ccz = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccz)));
-        for (int64_t c = c0; c < c1; c++) {
-            const int64_t i = c * 64 + lane;
+        for (int64_t k = k0; k < k1; k++) {
+            const int64_t i = (cstart_ + k * cstep) * 64 + lane;
             const bool valid = i < a.nq;
             const float4 qq = q1;
             const uint32_t Dw = valid ? D1 : 0u;
@@ -562,7 +575,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             q1 = q2;
             c1_ = c2_;
             D1 = D2;
-            raw(c + 2, q2, c2_, D2);
+            raw(k + 2, q2, c2_, D2);
             float qx, qy, qz;
             xform(a, qq, qx, qy, qz);
             // winner among the cached points by (d2, target index); an empty slot never wins
@@ -1476,7 +1489,15 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     icp->fb_seg = ((nchunks64 + nwaves - 1) / nwaves) * 64;
     icp->nb_ver = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_VER_WAVES));
     const int64_t nwaves_v = (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64);
+#if PCP_VER_XCD
+    {  // XCD-blocked split: a part of ceil(nch / np) chunks over floor(grid / np) * 4 waves
+        const int64_t np = std::min<int64_t>(8, icp->nb_ver);
+        const int64_t part = (nchunks64 + np - 1) / np, nw = (icp->nb_ver / np) * (pcp::kIcpBlock / 64);
+        icp->sv_seg = ((part + nw - 1) / nw) * 64;
+    }
+#else
     icp->sv_seg = ((nchunks64 + nwaves_v - 1) / nwaves_v) * 64;  // contiguous ranges: <= this per wave
+#endif
     int rc = pcp::dmalloc(ctx, &icp->partials, (size_t)(icp->nb_ver + icp->nb_fast + icp->nb_ring) * pcp::kAcc);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->acc, pcp::kAcc);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_dev, 24);
