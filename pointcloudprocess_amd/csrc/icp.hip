@@ -156,6 +156,10 @@ __device__ __forceinline__ float icp_d2(float qx, float qy, float qz, const floa
     return __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx));
 }
 
+// min / max of non-NaN floats as one v_med3_f32 (fminf/fmaxf add canonicalizing v_max ops)
+__device__ __forceinline__ float fmin_nn(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -INFINITY); }
+__device__ __forceinline__ float fmax_nn(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, INFINITY); }
+
 // position of candidate v of four concatenated rows (row prefixes c1 <= c2 <= c3, per-row
 // offsets o0..o3): register selects only (an indexed form was lowered to an LDS table of
 // pointers plus a scratch load per candidate)
@@ -676,16 +680,25 @@ struct Top4 {
 struct Top3 {
     float d0 = INFINITY, d1 = INFINITY, d2 = INFINITY, d3 = INFINITY;
     uint32_t p0 = ~0u, p1 = ~0u, p2 = ~0u;
+    // insertion as three independent compare-swaps from the bottom (flat selects: a nested
+    // select form was lowered to branches and register moves)
     __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t k) {
-        const float x = icp_d2(qx, qy, qz, p);
-        const bool c0 = x < d0, c1 = x < d1, c2 = x < d2;
-        d3 = __builtin_amdgcn_fmed3f(d2, d3, x);
-        p2 = c1 ? p1 : (c2 ? k : p2);
-        d2 = __builtin_amdgcn_fmed3f(d1, d2, x);
-        p1 = c0 ? p0 : (c1 ? k : p1);
-        d1 = __builtin_amdgcn_fmed3f(d0, d1, x);
-        p0 = c0 ? k : p0;
-        d0 = fminf(d0, x);
+        float x = icp_d2(qx, qy, qz, p);
+        uint32_t kx = k;
+        cswap(d2, p2, x, kx);
+        d3 = fmin_nn(d3, x);  // what fell out of the top 3
+        cswap(d1, p1, d2, p2);
+        cswap(d0, p0, d1, p1);
+    }
+    // (a, pa) <- the smaller of (a, pa), (b, pb) by d2; (b, pb) <- the larger (ties keep a)
+    __device__ __forceinline__ static void cswap(float& a, uint32_t& pa, float& b, uint32_t& pb) {
+        const bool t = b < a;
+        const float lo = fmin_nn(a, b), hi = fmax_nn(a, b);
+        const uint32_t ql = t ? pb : pa, qh = t ? pa : pb;
+        a = lo;
+        b = hi;
+        pa = ql;
+        pb = qh;
     }
     __device__ __forceinline__ void scan4(const float4* pts, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
                                           float qx, float qy, float qz) {
