@@ -16,6 +16,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "grid.hpp"
+#include "wave_acc.hpp"
 
 struct pcp_icp {
     pcp_ctx* ctx = nullptr;
@@ -324,8 +325,13 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
 }
 
 // Add one chunk's accepted pairs (lanes with ok) to the wave's fp64 accumulators S (LDS):
-// fp32 products centred on lane 0's query, summed across the wave with DPP adds, then
-// un-centred in fp64 by lane 0.  Every lane of the wave must call it (full EXEC).
+// fp32 products centred on lane 0's query, summed across the wave and un-centred in fp64
+// (wave_acc.hpp: reduce-scatter butterfly, one lane per accumulator; PCP_WAVE_ACC=0 keeps
+// the former 23 DPP reductions with lane 0 un-centring).  Every lane of the wave must call
+// it (full EXEC).
+#ifndef PCP_WAVE_ACC
+#define PCP_WAVE_ACC 1
+#endif
 __device__ __forceinline__ void chunk_accumulate(bool ok, float qx, float qy, float qz, const Best& b,
                                                  double* S, int lane) {
     if (!__ballot(ok)) return;
@@ -334,6 +340,12 @@ __device__ __forceinline__ void chunk_accumulate(bool ok, float qx, float qy, fl
     const float ccz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qz), 0));
     const float x0 = ok ? qx - ccx : 0.f, x1 = ok ? qy - ccy : 0.f, x2 = ok ? qz - ccz : 0.f;
     const float p0 = ok ? b.px - ccx : 0.f, p1 = ok ? b.py - ccy : 0.f, p2 = ok ? b.pz - ccz : 0.f;
+#if PCP_WAVE_ACC
+    const float v[23] = {ok ? 1.f : 0.f, x0, x1, x2, p0, p1, p2,
+                         x0 * p0, x0 * p1, x0 * p2, x1 * p0, x1 * p1, x1 * p2, x2 * p0, x2 * p1, x2 * p2,
+                         x0 * x0, x0 * x1, x0 * x2, x1 * x1, x1 * x2, x2 * x2, ok ? b.bd : 0.f};
+    wave_accumulate(v, S, lane, ccx, ccy, ccz);
+#else
     const float nn = wave_sum_f32(ok ? 1.f : 0.f);
     const float A0 = wave_sum_f32(x0), A1 = wave_sum_f32(x1), A2 = wave_sum_f32(x2);
     const float B0 = wave_sum_f32(p0), B1 = wave_sum_f32(p1), B2 = wave_sum_f32(p2);
@@ -355,6 +367,7 @@ __device__ __forceinline__ void chunk_accumulate(bool ok, float qx, float qy, fl
             S[16 + m] += (double)AA[m] + A[ir[m]] * C[ik[m]] + C[ir[m]] * A[ik[m]] + n * C[ir[m]] * C[ik[m]];
         S[22] += DD;
     }
+#endif
 }
 
 // XCD-blocked work split: workgroups are dealt round-robin over the 8 XCDs, so workgroup b
@@ -420,6 +433,9 @@ struct LaneAcc {
     // whole wave (full EXEC): totals -> S (fp64, un-centred by lane 0).  Not inlined: it runs once
     // per kFlush chunks, and its fp64 temporaries would otherwise raise the loop's register count.
     __device__ __attribute__((noinline)) void flush(double* S, int lane, float cx, float cy, float cz) {
+#if PCP_WAVE_ACC
+        wave_accumulate(v, S, lane, cx, cy, cz);
+#else
         float t[kAcc - 1];
 #pragma unroll
         for (int k = 0; k < kAcc - 1; k++) t[k] = wave_sum_f32(v[k]);
@@ -435,6 +451,7 @@ struct LaneAcc {
                 S[16 + m] += (double)t[16 + m] + A[ir[m]] * C[ik[m]] + C[ir[m]] * A[ik[m]] + n * C[ir[m]] * C[ik[m]];
             S[22] += t[22];
         }
+#endif
         zero();
     }
 };
