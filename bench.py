@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--n", type=int, default=50_000_000, help="points per cloud per GPU")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rmax", type=float, default=0.25)
-    ap.add_argument("--cell", type=float, default=0.1)
+    ap.add_argument("--cell", type=float, default=0.12, help="ICP target grid cell (m); swept 0.1-0.16, 0.12 best")
     ap.add_argument("--cpu-n", type=int, default=2_000_000, help="CPU baseline sample size")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-loop", action="store_true", help="host solve per iteration (one round trip each)")

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include "sortcfg.hpp"
 
 #include "grid.hpp"
 
@@ -446,10 +447,10 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
                 // read brick occupancy (its brick table stays all-zero = "occupied")
                 hipLaunchKernelGGL(k_cell_keys_rec, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const float*)cxyz,
                                    (const int32_t*)ix->mapping, n, skey, rec0, nullptr);
-                PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, rec0, (float4*)ix->pts,
+                PCP_HIP(ctx, rocprim::radix_sort_pairs<RecSortConfig>(nullptr, tmp_bytes, skey, key1, rec0, (float4*)ix->pts,
                                                        (size_t)n, 0u, bits, st));
                 if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
-                    PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, rec0, (float4*)ix->pts,
+                    PCP_HIP(ctx, rocprim::radix_sort_pairs<RecSortConfig>(tmp, tmp_bytes, skey, key1, rec0, (float4*)ix->pts,
                                                            (size_t)n, 0u, bits, st));
             }
             dfree(ctx, tmp);

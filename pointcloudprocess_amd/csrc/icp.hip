@@ -14,6 +14,7 @@
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include "sortcfg.hpp"
 
 #include "grid.hpp"
 #include "wave_acc.hpp"
@@ -1129,7 +1130,13 @@ __global__ void __launch_bounds__(256) k_sum_partials(const double* part, int nb
 #ifndef PCP_QKEY_LOCAL  // 0: brick order only (one radix pass less; measured 5 % slower searches)
 #define PCP_QKEY_LOCAL 1
 #endif
+#ifndef PCP_QBRICK  // edge (cells) of the query-order bricks: 4 = the index's bricks
+#define PCP_QBRICK 8
+#endif
+__host__ __device__ inline int64_t qbricks(const GridDesc& g, int a) { return (g.n[a] + PCP_QBRICK - 1) / PCP_QBRICK; }
 __host__ __device__ inline uint32_t query_key_end(const GridDesc& g) {
+    if (PCP_QBRICK != 4)
+        return (uint32_t)(qbricks(g, 0) * qbricks(g, 1) * qbricks(g, 2) * PCP_QBRICK * PCP_QBRICK * PCP_QBRICK);
     return (uint32_t)(PCP_QKEY_LOCAL ? g.nbricks * 64 : g.nbricks);
 }
 __global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_t n, uint32_t* key, float4* rec) {
@@ -1144,8 +1151,14 @@ __global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_
             const int cx = clampi((int)floorf(cell_f<float>(g, x, 0) - 0.5f), 0, g.n[0] - 1);
             const int cy = clampi((int)floorf(cell_f<float>(g, y, 1) - 0.5f), 0, g.n[1] - 1);
             const int cz = clampi((int)floorf(cell_f<float>(g, z, 2) - 0.5f), 0, g.n[2] - 1);
-            k = PCP_QKEY_LOCAL ? (uint32_t)(brick_of(g, cx, cy, cz) * 64 + local_of(cx, cy, cz))
-                               : (uint32_t)brick_of(g, cx, cy, cz);
+            if (PCP_QBRICK != 4) {
+                constexpr int B = PCP_QBRICK;
+                const int64_t b = ((int64_t)(cz / B) * qbricks(g, 1) + cy / B) * qbricks(g, 0) + cx / B;
+                k = (uint32_t)(b * B * B * B + ((cz % B) * B + cy % B) * B + cx % B);
+            } else {
+                k = PCP_QKEY_LOCAL ? (uint32_t)(brick_of(g, cx, cy, cz) * 64 + local_of(cx, cy, cz))
+                                   : (uint32_t)brick_of(g, cx, cy, cz);
+            }
         }
         key[i] = k;
         rec[i] = make_float4(x, y, z, __int_as_float((int)i));
@@ -1455,7 +1468,9 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     if (q_stride == 0) q_stride = 3 * sizeof(float);
     if (q_stride % sizeof(float)) return pcp::set_error(ctx, PCP_ERR_ARG, "query stride must be whole floats");
     if (nq >= ((int64_t)1 << 31)) return pcp::set_error(ctx, PCP_ERR_ARG, "ICP supports < 2^31 queries");
-    if (target->g.nbricks * 64 >= ((int64_t)1 << 32))
+    if (target->g.nbricks * 64 >= ((int64_t)1 << 32) ||
+        pcp::qbricks(target->g, 0) * pcp::qbricks(target->g, 1) * pcp::qbricks(target->g, 2) * PCP_QBRICK *
+                PCP_QBRICK * PCP_QBRICK >= ((int64_t)1 << 32))
         return pcp::set_error(ctx, PCP_ERR_UNSUPPORTED, "ICP target grid too large for 32-bit cell keys");
     // sort the query set once by target-grid brick (stable radix sort, record as payload)
     hipStream_t st = ctx->stream;
@@ -1479,9 +1494,9 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
             unsigned bits = 1;  // keys are in [0, query_key_end]
             while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)pcp::query_key_end(target->g)) bits++;
             size_t tb = 0;
-            hipError_t e = rocprim::radix_sort_pairs(nullptr, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
+            hipError_t e = rocprim::radix_sort_pairs<pcp::RecSortConfig>(nullptr, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
             if (e == hipSuccess && !(rc = pcp::dmalloc(ctx, (char**)&tmp, tb)))
-                e = rocprim::radix_sort_pairs(tmp, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
+                e = rocprim::radix_sort_pairs<pcp::RecSortConfig>(tmp, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
             if (!rc && e == hipSuccess)
                 hipLaunchKernelGGL(pcp::k_first_at_least, dim3(1), dim3(1), 0, st, k1, nq,
                                    pcp::query_key_end(target->g), d_cnt);
