@@ -1643,9 +1643,6 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
                          (double)c[3] * 64.0 / (double)(c[2] ? c[2] : 1));
             std::fprintf(stderr, "[pcp icp dbg] fallback: settled by the 3x3x3 stage %llu, with a correspondence %llu\n",
                          c[5], c[6]);
-            std::fprintf(stderr, "[pcp icp dbg] L histogram (bins of 4):");
-            for (int k = 4; k < 16; k++) std::fprintf(stderr, " %.3f", (double)c[k] / (double)(c[2] ? c[2] : 1));
-            std::fprintf(stderr, "\n");
         }
     }
     return PCP_OK;

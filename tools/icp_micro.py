@@ -15,7 +15,7 @@ from pointcloudprocess_amd import ops, synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=50_000_000)
-ap.add_argument("--cell", type=float, default=0.1)
+ap.add_argument("--cell", type=float, default=0.12)
 ap.add_argument("--rmax", type=float, default=0.25)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--iters", type=int, default=20)
