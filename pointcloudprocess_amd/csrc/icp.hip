@@ -742,6 +742,61 @@ struct Top3 {
     }
 };
 
+// running 3-NN on packed keys (PCP_TOPK_PACKED): key = (bits(d2') & ~255) | v, v the
+// candidate's index in the concatenated octant list (< 256), d2' the contract's d2 chain
+// started from FLT_MIN (so no key is denormal).  Positive floats order like their bits, so a
+// v_med3_u32 network on the keys keeps the 4 smallest keys -- values and list indices
+// together -- in 4 VALU ops per candidate (the compare-swap form needs 13).  The truncated
+// d2 only chooses WHICH points are cached: the winner among them is decided on the exact d2
+// afterwards, and the 4th key with its low byte cleared bounds every uncached point's d2.
+// Measured (r15f-j): exact, 7 % faster on the full first launch, but 10-20 % slower on the
+// later launches' scattered search lists (latency-bound there; 8 waves only recover parity),
+// so it is off by default.
+#ifndef PCP_TOPK_PACKED
+#define PCP_TOPK_PACKED 0
+#endif
+constexpr uint32_t kKeyMax = 0x7f7fffffu;  // FLT_MAX: above every real key
+constexpr uint32_t kMaxOctList = 256;       // list indices that fit the key's low byte
+// median of three u32 (one v_med3_u32; the float form adds canonicalizing ops on bit-cast keys)
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+struct Top3K {
+    uint32_t t0 = kKeyMax, t1 = kKeyMax, t2 = kKeyMax, t3 = kKeyMax;
+    __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t v) {
+        const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+        const float d = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, __fmaf_rn(dx, dx, 1.17549435e-38f)));
+        const uint32_t x = (__float_as_uint(d) & ~0xffu) | v;
+        t3 = umed3(t2, t3, x);
+        t2 = umed3(t1, t2, x);
+        t1 = umed3(t0, t1, x);
+        t0 = min(t0, x);
+    }
+    __device__ __forceinline__ void scan4(const float4* pts, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
+                                          float qx, float qy, float qz) {
+        const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
+        const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
+        auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3, o0, o1, o2, o3); };
+        constexpr int U = PCP_SCAN_UNROLL;
+        uint32_t v = 0;
+        for (; v + U <= L; v += U) {
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) p[u] = pts[addr(v + u)];
+#pragma unroll
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, p[u], v + u);
+        }
+        for (; v < L; v++) consider(qx, qy, qz, pts[addr(v)], v);
+    }
+    // lower bound on the d2 of every scanned point that is not among the 3 kept
+    __device__ __forceinline__ float uncached_lb() const {
+        const uint32_t k = t3;
+        return k == kKeyMax ? INFINITY : __uint_as_float(k & ~0xffu) * (1.f - 1e-6f);
+    }
+};
+
 // ---- search pass (the verify pass's list; every query at the first launch)
 // One query per lane, 64-query chunks grid-stride over the list.  Each query scans its whole
 // 2x2x2 "octant" block of cells (the four x-rows [floor(f - 1/2), +1]) keeping its 4 nearest.
@@ -777,7 +832,11 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             in_ = list ? (int64_t)list[j + 64 * nwaves] : j + 64 * nwaves;
             qn = a.q[in_];
         }
-#if PCP_CACHE3
+#if PCP_TOPK_PACKED
+        Top3K b;
+        float4 wp = make_float4(0.f, 0.f, 0.f, 0.f);  // the winner's coordinates
+        float wd = INFINITY;                           // and exact d2
+#elif PCP_CACHE3
         Top3 b;
 #else
         Top4 b;
@@ -807,6 +866,11 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             }
 #pragma unroll
             for (int r = 0; r < 4; r++) rn[r] -= rs[r];
+#if PCP_TOPK_PACKED
+            // a list too long for the key's index byte is left to the fallback pass (no message)
+            const bool big = rn[0] + rn[1] + rn[2] + rn[3] > kMaxOctList;
+            if (big) rn[0] = rn[1] = rn[2] = rn[3] = 0u;
+#endif
             if (!(a.dbg & kDbgNoScan)) b.scan4(a.tp, rs, rn, qx, qy, qz);
             if (a.dbg & kDbgCount) {
                 atomicAdd(a.dbgcnt, (unsigned long long)(rn[0] + rn[1] + rn[2] + rn[3]));
@@ -814,6 +878,38 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             }
             const float rr = m * g.hf;
             const float cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
+#if PCP_TOPK_PACKED
+            // the kept points' positions (list index -> row position) and exact (d2, index) winner
+            const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2];
+            const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
+            const uint32_t k0 = b.t0, k1 = b.t1, k2 = b.t2;
+            const uint32_t ps0 = k0 == kKeyMax ? ~0u : cat_addr(k0 & 0xffu, c1, c2, c3, o0, o1, o2, o3);
+            const uint32_t ps1 = k1 == kKeyMax ? ~0u : cat_addr(k1 & 0xffu, c1, c2, c3, o0, o1, o2, o3);
+            const uint32_t ps2 = k2 == kKeyMax ? ~0u : cat_addr(k2 & 0xffu, c1, c2, c3, o0, o1, o2, o3);
+            int wj = 0x7fffffff;
+            auto take = [&](const float4 P, uint32_t ps) {
+                const float e = icp_d2(qx, qy, qz, P);
+                const int id = __float_as_int(P.w);
+                const bool t = e < wd || (e == wd && id < wj);
+                wd = t ? e : wd;
+                wj = t ? id : wj;
+                wp = t ? P : wp;
+                win = t ? ps : win;
+            };
+            // the smallest key's point is the winner unless another kept key lies in the same or
+            // the next truncation bucket (then its exact d2 decides): one gather, rarely three
+            take(ld16(a.tp, min(ps0, a.ntp)), ps0);  // empty: the far sentinel
+            if ((k1 >> 8) - (k0 >> 8) <= 1u) take(ld16(a.tp, min(ps1, a.ntp)), ps1);
+            if ((k2 >> 8) - (k0 >> 8) <= 1u) take(ld16(a.tp, min(ps2, a.ntp)), ps2);
+            const float lbu = b.uncached_lb();  // every other scanned point: d2 >= lbu
+            found = wd <= a.r2;
+            settled = !big && (found ? (wd < lbu && wd <= cert2) : (lbu > a.r2 && a.r2 <= cert2));
+            settled = settled || (a.dbg & kDbgNoFallback);
+            // settled: D bounds every uncached point for the verify pass.  Unsettled: the
+            // fallback pass (which overwrites the cache) gets lbu as its message.
+            const float D = settled ? fminf(sqrtf(lbu), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : (big ? 0.f : lbu);
+            a.cand[i] = make_uint4(ps0, ps1, ps2, pack_dlb(D, a.launch));
+#else
             found = b.d0 <= a.r2;
 #if PCP_CACHE3
             const float dnext = b.d3;  // the first uncached d2
@@ -849,6 +945,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             a.cand[i] = make_uint4(b.p0, b.p1, b.p2, b.p3);
             a.dlb[i] = pack_dlb(D, a.launch);
 #endif
+#endif  // PCP_TOPK_PACKED
         }
         // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
         const bool fb = valid && !settled;
@@ -860,8 +957,12 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         }
         fbn += (uint32_t)__popcll(fbm);
         const bool acc_ok = valid && settled && found && !(a.dbg & kDbgNoAccum);
+#if PCP_TOPK_PACKED
+        const Best w{wd, 0, win, wp.x, wp.y, wp.z};
+#else
         Best w{b.d0, 0, win, 0.f, 0.f, 0.f};
         if (acc_ok) w.fetch(a.tp);
+#endif
         chunk_accumulate(acc_ok, qx, qy, qz, w, s_acc[wid], lane);
     }
     if (lane == 0) {  // every wave of the grid writes its count: no zeroing pass needed
