@@ -19,6 +19,11 @@ struct pcp_ctx {
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
     uint32_t bf_fallback = 0;  // queries of the last pcp_knn_bruteforce that needed the exact scan
+    // look-back scan state (scan.hip): per-tile status words tagged with the call's epoch, so
+    // no clearing pass is needed per call; [tiles] u64 status, then the tile counter and total
+    uint64_t* scan_status = nullptr;
+    int64_t scan_tiles = 0;
+    uint32_t scan_epoch = 0;
     // Caching device allocator for the library's internal buffers (index builds, ICP state,
     // per-call scratch): blocks are reused in stream order on this context's stream instead
     // of paying a synchronising hipMalloc/hipFree each time.  Objects allocated through a

@@ -136,6 +136,7 @@ int pcp_ctx_destroy(pcp_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->scan_status) (void)hipFree(ctx->scan_status);
     pcp::cache_release(ctx);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

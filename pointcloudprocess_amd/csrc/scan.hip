@@ -128,7 +128,10 @@ int64_t scan_tmp_elems(int64_t n) {
 constexpr int kLbBlock = 256;
 constexpr int kLbSeg = 4;                       // segments of 1024 elements per tile
 constexpr int kLbTile = kLbBlock * 4 * kLbSeg;  // 4096 elements
+// status word: flag (bits 62-63) | epoch (bits 32-61) | value; a word of another epoch reads as
+// "not published yet"
 constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStMask = 3ull << 62;
+constexpr uint32_t kEpochMask = 0x3fffffffu;
 
 __device__ __forceinline__ uint64_t st_load(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -138,10 +141,15 @@ __device__ __forceinline__ void st_store(uint64_t* p, uint64_t v) {
 }
 
 __global__ void __launch_bounds__(kLbBlock) k_scan_lookback(uint32_t* data, int64_t n, uint64_t* status,
-                                                            uint32_t* tile_ctr, uint32_t* total_out) {
+                                                            uint32_t* tile_ctr, uint32_t* total_out,
+                                                            uint32_t epoch) {
     __shared__ uint32_t s_tile, s_prefix;
     __shared__ uint32_t s_wsum[kLbBlock / 64][kLbSeg];
-    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    if (threadIdx.x == 0) {
+        s_tile = atomicAdd(tile_ctr, 1u);
+        // the last tile id is handed out last: reset the counter for the next call
+        if (s_tile == gridDim.x - 1) atomicExch(tile_ctr, 0u);
+    }
     __syncthreads();
     const uint32_t tile = s_tile;
     const int64_t base = (int64_t)tile * kLbTile;
@@ -181,16 +189,17 @@ __global__ void __launch_bounds__(kLbBlock) k_scan_lookback(uint32_t* data, int6
         tile_total += tot;
     }
     if (wid == 0) {
+        const uint64_t ep = (uint64_t)epoch << 32;
         uint32_t prefix = 0;
         if (tile == 0) {
-            if (lane == 0) st_store(&status[0], kStPre | tile_total);
+            if (lane == 0) st_store(&status[0], kStPre | ep | tile_total);
         } else {
-            if (lane == 0) st_store(&status[tile], kStAgg | tile_total);
+            if (lane == 0) st_store(&status[tile], kStAgg | ep | tile_total);
             int64_t top = (int64_t)tile - 1;
             while (true) {
                 const int64_t p = top - lane;
-                const uint64_t st = p >= 0 ? st_load(&status[p]) : kStPre;
-                const uint64_t flag = st & kStMask;
+                const uint64_t st = p >= 0 ? st_load(&status[p]) : kStPre | ep;
+                const uint64_t flag = (st & ~kStMask & ~0xffffffffull) == ep ? st & kStMask : 0ull;
                 const uint64_t pre = __ballot(flag == kStPre);
                 const uint64_t notready = __ballot(flag == 0);
                 const int first = pre ? __ffsll((long long)pre) - 1 : 64;
@@ -203,7 +212,7 @@ __global__ void __launch_bounds__(kLbBlock) k_scan_lookback(uint32_t* data, int6
                 if (first < 64) break;
                 top -= 64;
             }
-            if (lane == 0) st_store(&status[tile], kStPre | (prefix + tile_total));
+            if (lane == 0) st_store(&status[tile], kStPre | ep | (prefix + tile_total));
         }
         if (lane == 0) s_prefix = prefix;
     }
@@ -235,14 +244,27 @@ int scan_u32_inplace(pcp_ctx* ctx, uint32_t* data, int64_t n, uint32_t* total_ho
         return PCP_OK;
     }
     const int64_t tiles = (n + kLbTile - 1) / kLbTile;
-    // scratch: [status (tiles u64)] [tile counter, total (u32)]
-    void* tmp;
-    PCP_TRY(scratch(ctx, (size_t)tiles * sizeof(uint64_t) + 16, &tmp));
-    uint64_t* status = (uint64_t*)tmp;
-    uint32_t* ctr = (uint32_t*)(status + tiles);
-    PCP_HIP(ctx, hipMemsetAsync(tmp, 0, (size_t)tiles * sizeof(uint64_t) + 16, ctx->stream));
+    // persistent state: [status (tiles u64)] [tile counter, total (u32)], cleared once when it
+    // grows; each call tags its status words with a new epoch instead of clearing them
+    if (tiles > ctx->scan_tiles) {
+        if (ctx->scan_status) {
+            PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            PCP_HIP(ctx, hipFree(ctx->scan_status));
+            ctx->scan_status = nullptr;
+            ctx->scan_tiles = 0;
+        }
+        const int64_t want = tiles + tiles / 4 + 64;
+        PCP_HIP(ctx, hipMalloc(&ctx->scan_status, (size_t)(want + 1) * sizeof(uint64_t)));
+        PCP_HIP(ctx, hipMemsetAsync(ctx->scan_status, 0, (size_t)(want + 1) * sizeof(uint64_t), ctx->stream));
+        ctx->scan_tiles = want;
+        ctx->scan_epoch = 0;
+    }
+    ctx->scan_epoch = (ctx->scan_epoch + 1) & kEpochMask;
+    if (ctx->scan_epoch == 0) ctx->scan_epoch = 1;  // 0: the cleared state
+    uint64_t* status = ctx->scan_status;
+    uint32_t* ctr = (uint32_t*)(status + ctx->scan_tiles);
     hipLaunchKernelGGL(k_scan_lookback, dim3((unsigned)tiles), dim3(kLbBlock), 0, ctx->stream, data, n, status, ctr,
-                       ctr + 1);
+                       ctr + 1, ctx->scan_epoch);
     PCP_LAUNCH_CHECK(ctx);
     if (total_host) {
         PCP_HIP(ctx, hipMemcpyAsync(total_host, ctr + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
