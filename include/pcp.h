@@ -139,10 +139,14 @@ int pcp_knn_lod(pcp_ctx* ctx, const void* cloud_aos48_dev, int64_t n, const void
 /* PointCloudHelper::getMinMax3D(cloud, Vector4d&, Vector4d&) (point_cloud_helper.h:59-90). */
 int pcp_minmax_aos48(pcp_ctx* ctx, const void* in_dev, int64_t n, int is_dense,
                      double min_host[4], double max_host[4]);
-/* compute3DCentroid (point_cloud_helper.h:193-230).  The GPU sum is a fixed-order tree,
- * not the reference's sequential left fold. */
+/* compute3DCentroid (point_cloud_helper.h:193-230): the reference's sequential left fold,
+ * bit for bit, evaluated as a parallel scan of exact chunk transfer maps (fold.hip). */
 int pcp_centroid_aos48(pcp_ctx* ctx, const void* in_dev, int64_t n, int is_dense,
                        double c_host[4], uint32_t* count_host);
+/* compute3DCentroid of cloud_all = a ++ b (get_rot_icp, point_cloud_helper.cpp:78-83:
+ * `*cloud_all += *src; *cloud_all += *temp;` then one fold; is_dense = a && b dense). */
+int pcp_centroid_concat_aos48(pcp_ctx* ctx, const void* a_dev, int64_t na, const void* b_dev,
+                              int64_t nb, int is_dense, double c_host[4], uint32_t* count_host);
 /* transformPointCloud (point_cloud_helper.h:92-127), row-major 4x4, in == out allowed. */
 int pcp_transform_aos48(pcp_ctx* ctx, const void* in_dev, void* out_dev, int64_t n,
                         int is_dense, const double T_host[16]);
@@ -181,6 +185,10 @@ int pcp_plane_fit_segments(pcp_ctx* ctx, const double* xyz_dev, size_t stride_by
  * index (pcp_index_build_f32); the query set is sorted spatially once here. */
 int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q_dev,
                    size_t q_stride_bytes, int64_t nq, pcp_icp** out);
+/* Size limits pcp_icp_create enforces (host only, no device call): PCP_ERR_ARG for
+ * nq >= 2^31 or a negative size, PCP_ERR_CAPACITY for a target of 2^28 - 1 or more valid
+ * points (the search passes address the fp32 target with 32-bit byte offsets). */
+int pcp_icp_check_sizes(int64_t n_target, int64_t nq);
 int pcp_icp_destroy(pcp_icp* icp);
 /* One iteration at pose T (row-major 4x4 double, cast to fp32 for the kernel):
  * correspondences within rmax + the 24 accumulators ([23] = queries that
@@ -235,11 +243,14 @@ int pcp_icp_last_fallback(const pcp_icp* icp, int64_t* n);
 int pcp_icp_last_searched(const pcp_icp* icp, int64_t* n);
 
 /* PointCloudHelper::get_rot_icp (point_cloud_helper.cpp:75-166) on AoS48 clouds:
- * joint centroid, float cast, ICP(query = temp -> target = src), un-centring
- * t' = t - R c + c.  mat_rot row-major.  Returns PCP_OK and *err (< 0 on failure). */
-int pcp_get_rot_icp(pcp_ctx* ctx, const void* src_aos48_dev, int64_t ns,
-                    const void* temp_aos48_dev, int64_t nt, double mat_rot_host[16],
-                    float rmax, int iters, int do_scale, double cell_size, float* err);
+ * joint centroid (sequential fold over src ++ temp; non-finite points skipped unless both
+ * clouds are dense, as cloud_all.is_dense = src.is_dense && temp.is_dense), float cast,
+ * ICP(query = temp -> target = src), un-centring t' = t - R c + c.  mat_rot row-major.
+ * Returns PCP_OK and *err (< 0 on failure). */
+int pcp_get_rot_icp(pcp_ctx* ctx, const void* src_aos48_dev, int64_t ns, int src_is_dense,
+                    const void* temp_aos48_dev, int64_t nt, int temp_is_dense,
+                    double mat_rot_host[16], float rmax, int iters, int do_scale,
+                    double cell_size, float* err);
 
 #ifdef __cplusplus
 }

@@ -515,7 +515,16 @@ public:
                       "pcp_minmax_aos48");
         for (int a = 0; a < 4; a++) { min_pt[a] = mn[a]; max_pt[a] = mx[a]; }
     }
-    // compute3DCentroid (:193-230); GPU sum order is a fixed tree
+    // getMinMax3D(cloud, PointT&, PointT&) (:22-57): the same reduction, only x/y/z of the
+    // two points are written (the other fields keep their values)
+    template <class PointT>
+    static void getMinMax3D(const PointCloud<PointT>& cloud, PointT& min_pt, PointT& max_pt) {
+        double mn[4], mx[4];
+        getMinMax3D(cloud, mn, mx);
+        min_pt.x = mn[0]; min_pt.y = mn[1]; min_pt.z = mn[2];
+        max_pt.x = mx[0]; max_pt.y = mx[1]; max_pt.z = mx[2];
+    }
+    // compute3DCentroid (:193-230): the reference's sequential fold, bit for bit (fold.hip)
     template <class PointT, class V4>
     static unsigned int compute3DCentroid(const PointCloud<PointT>& cloud, V4& centroid) {
         if (cloud.points.empty()) return 0;
@@ -590,8 +599,9 @@ public:
         t.upload(cloud_temp->points.data(), cloud_temp->points.size() * sizeof(CloudItem));
         double Mh[16];
         float err = -1.0f;
-        const int rc = pcp_get_rot_icp(c, s.ptr(), (int64_t)cloud_src->size(), t.ptr(), (int64_t)cloud_temp->size(),
-                                       Mh, maxdist, iters, do_scale ? 1 : 0, 0.0, &err);
+        const int rc = pcp_get_rot_icp(c, s.ptr(), (int64_t)cloud_src->size(), cloud_src->is_dense ? 1 : 0, t.ptr(),
+                                       (int64_t)cloud_temp->size(), cloud_temp->is_dense ? 1 : 0, Mh, maxdist, iters,
+                                       do_scale ? 1 : 0, 0.0, &err);
         if (rc != PCP_OK) return -1.0f;
         for (int r = 0; r < 4; r++)
             for (int col = 0; col < 4; col++) mat_rot(r, col) = Mh[4 * r + col];

@@ -270,6 +270,27 @@ unsigned ora_centroid(const ora_point48* in, int n, int is_dense, double c[4]) {
     return is_dense ? (unsigned)n : cp;
 }
 
+unsigned ora_centroid_concat(const ora_point48* a, int na, const ora_point48* b, int nb, int is_dense,
+                             double c[4]) {
+    if (na + nb <= 0) return 0;
+    double s[4] = {0, 0, 0, 0};  /* one left fold over the concatenation, a first */
+    unsigned cp = 0;
+    for (int part = 0; part < 2; part++) {
+        const ora_point48* in = part ? b : a;
+        const int n = part ? nb : na;
+        for (int i = 0; i < n; i++) {
+            const ora_point48* p = &in[i];
+            if (!is_dense && !is_finite3(p->x, p->y, p->z)) continue;
+            s[0] += p->x; s[1] += p->y; s[2] += p->z; s[3] += p->w;
+            cp++;
+        }
+    }
+    s[3] = 0;
+    const double dn = is_dense ? (double)((size_t)na + (size_t)nb) : (double)cp;
+    for (int k = 0; k < 4; k++) c[k] = s[k] / dn;
+    return is_dense ? (unsigned)(na + nb) : cp;
+}
+
 /* rot * p + trans with Eigen's lazy 3x3*3x1 product ((r0*x + r1*y) + r2*z) + t. */
 static inline void xform_d(const double T[16], double x, double y, double z, double* o) {
     for (int r = 0; r < 3; r++) {
@@ -831,24 +852,42 @@ double ora_icp(const float* tgt, int nt, const float* q, int nq, double T[16], f
     return err;
 }
 
-float ora_get_rot_icp(const ora_point48* src, int ns, const ora_point48* tmp, int nt,
+float ora_get_rot_icp(const ora_point48* src, int ns, int src_dense, const ora_point48* tmp, int nt, int tmp_dense,
                       double M[16], float rmax, int iters, int do_scale, int nthreads) {
-    /* joint centroid over cloud_all = src ++ tmp (point_cloud_helper.cpp:78-83) */
+    /* joint centroid over cloud_all = src ++ tmp (point_cloud_helper.cpp:78-83): operator+=
+     * leaves cloud_all.is_dense = src.is_dense && tmp.is_dense (point_cloud.h:143-146), and
+     * compute3DCentroid then skips non-finite points (point_cloud_helper.h:213-224) */
+    const int dense = src_dense && tmp_dense;
     double s[3] = {0, 0, 0};
-    for (int i = 0; i < ns; i++) { s[0] += src[i].x; s[1] += src[i].y; s[2] += src[i].z; }
-    for (int i = 0; i < nt; i++) { s[0] += tmp[i].x; s[1] += tmp[i].y; s[2] += tmp[i].z; }
+    unsigned cp = 0;
+    for (int i = 0; i < ns; i++) {
+        if (!dense && !is_finite3(src[i].x, src[i].y, src[i].z)) continue;
+        s[0] += src[i].x; s[1] += src[i].y; s[2] += src[i].z; cp++;
+    }
+    for (int i = 0; i < nt; i++) {
+        if (!dense && !is_finite3(tmp[i].x, tmp[i].y, tmp[i].z)) continue;
+        s[0] += tmp[i].x; s[1] += tmp[i].y; s[2] += tmp[i].z; cp++;
+    }
     double c[3];
-    for (int a = 0; a < 3; a++) c[a] = s[a] / (double)(ns + nt);
+    const double dn = dense ? (double)((size_t)ns + (size_t)nt) : (double)cp;
+    for (int a = 0; a < 3; a++) c[a] = s[a] / dn;
+    /* float(p - c) vertices (:89-104); a non-finite vertex never pairs (the kd-tree of the
+     * build drops it, as the GPU index does), so only finite ones are kept here */
     float* fs = (float*)malloc((size_t)(ns > 0 ? ns : 1) * 3 * sizeof(float));
     float* ft = (float*)malloc((size_t)(nt > 0 ? nt : 1) * 3 * sizeof(float));
+    int ms = 0, mt = 0;
     for (int i = 0; i < ns; i++) {  /* :89-96 */
-        fs[3 * i] = (float)(src[i].x - c[0]); fs[3 * i + 1] = (float)(src[i].y - c[1]); fs[3 * i + 2] = (float)(src[i].z - c[2]);
+        float v[3] = {(float)(src[i].x - c[0]), (float)(src[i].y - c[1]), (float)(src[i].z - c[2])};
+        if (!(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]))) continue;
+        memcpy(fs + 3 * ms++, v, sizeof(v));
     }
     for (int i = 0; i < nt; i++) {  /* :97-103 */
-        ft[3 * i] = (float)(tmp[i].x - c[0]); ft[3 * i + 1] = (float)(tmp[i].y - c[1]); ft[3 * i + 2] = (float)(tmp[i].z - c[2]);
+        float v[3] = {(float)(tmp[i].x - c[0]), (float)(tmp[i].y - c[1]), (float)(tmp[i].z - c[2])};
+        if (!(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]))) continue;
+        memcpy(ft + 3 * mt++, v, sizeof(v));
     }
     double T[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    double err = ora_icp(fs, ns, ft, nt, T, rmax, iters, do_scale, nthreads);
+    double err = ora_icp(fs, ms, ft, mt, T, rmax, iters, do_scale, nthreads);
     memcpy(M, T, sizeof(T));        /* mat_rot(i,j) = xf2[i+4j] (:151-157) */
     for (int a = 0; a < 3; a++) {   /* t' = (t - R c) + c (:164) */
         double rc = M[4 * a] * c[0];

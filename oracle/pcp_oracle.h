@@ -75,6 +75,9 @@ void ora_getminmax3d(const ora_point48* in, int n, int is_dense, double min_p[4]
 
 /* compute3DCentroid (point_cloud_helper.h:193-230); returns count. */
 unsigned ora_centroid(const ora_point48* in, int n, int is_dense, double c[4]);
+/* compute3DCentroid of cloud_all = a ++ b (point_cloud_helper.cpp:78-83) */
+unsigned ora_centroid_concat(const ora_point48* a, int na, const ora_point48* b, int nb, int is_dense,
+                             double c[4]);
 
 /* transformPointCloud (point_cloud_helper.h:92-127). T row-major 4x4. in==out allowed. */
 void ora_transform(const ora_point48* in, ora_point48* out, int n, int is_dense, const double T[16]);
@@ -146,7 +149,7 @@ double ora_icp(const float* tgt, int nt, const float* q, int nq, double T[16], f
 
 /* PointCloudHelper::get_rot_icp front-end (point_cloud_helper.cpp:75-166): joint
  * centroid, float cast, ICP(query=temp -> target=src), un-centre t' = t - R c + c. */
-float ora_get_rot_icp(const ora_point48* src, int ns, const ora_point48* tmp, int nt,
+float ora_get_rot_icp(const ora_point48* src, int ns, int src_dense, const ora_point48* tmp, int nt, int tmp_dense,
                       double mat_rot[16], float rmax, int iters, int do_scale, int nthreads);
 
 #ifdef __cplusplus

@@ -51,11 +51,13 @@ SIGNATURES = [
     ("pcp_knn_lod", _i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp]),
     ("pcp_minmax_aos48", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _P(_f64)]),
     ("pcp_centroid_aos48", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _P(_u32)]),
+    ("pcp_centroid_concat_aos48", _i32, [_vp, _vp, _i64, _vp, _i64, _i32, _P(_f64), _P(_u32)]),
     ("pcp_transform_aos48", _i32, [_vp, _vp, _vp, _i64, _i32, _P(_f64)]),
     ("pcp_voxel_filter", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _i32, _vp, _P(_i64), _vp]),
     ("pcp_remove_duplicate", _i32, [_vp, _vp, _i64, _i32, _f32, _vp, _P(_i64)]),
     ("pcp_normals_knn", _i32, [_vp, _vp, _i32, _vp, _i64]),
     ("pcp_icp_create", _i32, [_vp, _vp, _vp, _sz, _i64, _P(_vp)]),
+    ("pcp_icp_check_sizes", _i32, [_i64, _i64]),
     ("pcp_icp_destroy", _i32, [_vp]),
     ("pcp_icp_step", _i32, [_vp, _vp, _P(_f64), _f32, _vp, _vp, _vp]),
     ("pcp_icp_keys", _i32, [_vp, _vp, _P(_f64), _f32, _i64, _vp]),
@@ -69,8 +71,8 @@ SIGNATURES = [
     ("pcp_icp_kernel_ms", _i32, [_vp, _vp, _P(_f64), _P(_i32)]),
     ("pcp_icp_last_fallback", _i32, [_vp, _P(_i64)]),
     ("pcp_icp_last_searched", _i32, [_vp, _P(_i64)]),
-    ("pcp_get_rot_icp", _i32, [_vp, _vp, _i64, _vp, _i64, _P(_f64), _f32, _i32, _i32, _f64,
-                               _P(_f32)]),
+    ("pcp_get_rot_icp", _i32, [_vp, _vp, _i64, _i32, _vp, _i64, _i32, _P(_f64), _f32, _i32, _i32,
+                               _f64, _P(_f32)]),
 ]
 
 _lib = None

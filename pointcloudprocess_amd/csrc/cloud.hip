@@ -38,10 +38,6 @@ __device__ __forceinline__ double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
     return v;
 }
-__device__ __forceinline__ double wave_add(double v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
 // V2: per-block min/max of data[0..3] over (finite unless is_dense) points.  Eigen's
 // min/max on a non-NaN running value are exact, so any reduction order gives the
@@ -70,27 +66,6 @@ __global__ __launch_bounds__(kB) void k_minmax48(const P48* in, int64_t n, int i
         double r = sm[0][threadIdx.x];
         for (int w = 1; w < kB / 64; w++) r = threadIdx.x < 4 ? fmin(r, sm[w][threadIdx.x]) : fmax(r, sm[w][threadIdx.x]);
         part[blockIdx.x * 8 + threadIdx.x] = r;
-    }
-}
-
-// I3: fixed-order tree sums (per lane sequential over a grid-stride, then a shuffle tree,
-// then blocks in index order on the host) -- deterministic for a given n.
-__global__ __launch_bounds__(kB) void k_sum48(const P48* in, int64_t n, int is_dense, double* part) {
-    double s0 = 0, s1 = 0, s2 = 0, s3 = 0, c = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const P48 p = in[i];
-        if (!is_dense && !finite3(p.x, p.y, p.z)) continue;
-        s0 += p.x; s1 += p.y; s2 += p.z; s3 += p.w; c += 1.0;
-    }
-    __shared__ double sm[kB / 64][5];
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    s0 = wave_add(s0); s1 = wave_add(s1); s2 = wave_add(s2); s3 = wave_add(s3); c = wave_add(c);
-    if (ln == 0) { sm[wv][0] = s0; sm[wv][1] = s1; sm[wv][2] = s2; sm[wv][3] = s3; sm[wv][4] = c; }
-    __syncthreads();
-    if (threadIdx.x < 5) {
-        double r = sm[0][threadIdx.x];
-        for (int w = 1; w < kB / 64; w++) r += sm[w][threadIdx.x];
-        part[blockIdx.x * 5 + threadIdx.x] = r;
     }
 }
 
@@ -274,33 +249,16 @@ int minmax_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, doub
     return PCP_OK;
 }
 
-// raw sums s[0..3] and the point count (host), fixed order
-static int sums_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, double s[5]) {
-    for (int a = 0; a < 5; a++) s[a] = 0;
-    if (n <= 0) return PCP_OK;
-    const unsigned nb = grid_for(n, kB, kRedBlocks);
-    double* part;
-    PCP_TRY(dmalloc(ctx, &part, 5 * (size_t)nb));
-    hipLaunchKernelGGL(k_sum48, dim3(nb), dim3(kB), 0, ctx->stream, (const P48*)in, n, is_dense, part);
-    std::vector<double> h(5 * nb);
-    hipError_t e = hipMemcpyAsync(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    dfree(ctx, part);
-    if (e != hipSuccess) return hip_fail(ctx, e, "centroid", __FILE__, __LINE__);
-    for (unsigned b = 0; b < nb; b++)
-        for (int a = 0; a < 5; a++) s[a] += h[5 * b + a];
-    return PCP_OK;
-}
-
 int centroid_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, double c[4], uint32_t* count) {
     if (n <= 0) {  // point_cloud_helper.h:197-198: centroid untouched, 0 returned
         if (count) *count = 0;
         return PCP_OK;
     }
-    double s[5];
-    PCP_TRY(sums_aos48_dev(ctx, in, n, is_dense, s));
-    const uint32_t cp = is_dense ? (uint32_t)n : (uint32_t)s[4];
-    const double dn = (double)cp;
+    // the reference's sequential left fold, bit for bit (point_cloud_helper.h:199-227)
+    double s[4];
+    PCP_TRY(seqfold_aos48(ctx, in, n, nullptr, 0, is_dense, s));
+    const uint32_t cp = is_dense ? (uint32_t)n : (uint32_t)s[3];
+    const double dn = is_dense ? (double)n : (double)cp;  // size() (size_t) or unsigned cp
     c[0] = s[0] / dn; c[1] = s[1] / dn; c[2] = s[2] / dn; c[3] = 0.0 / dn;
     if (count) *count = cp;
     return PCP_OK;
@@ -388,6 +346,24 @@ int pcp_centroid_aos48(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, do
     return centroid_aos48_dev(ctx, in, n, is_dense, c, count);
 }
 
+int pcp_centroid_concat_aos48(pcp_ctx* ctx, const void* a, int64_t na, const void* b, int64_t nb, int is_dense,
+                              double c[4], uint32_t* count) {
+    if (!ctx || na < 0 || nb < 0 || (na > 0 && !a) || (nb > 0 && !b) || !c)
+        return set_error(ctx, PCP_ERR_ARG, "pcp_centroid_concat_aos48: bad arguments");
+    if (na + nb == 0) {
+        if (count) *count = 0;
+        return PCP_OK;
+    }
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    double s[4];
+    PCP_TRY(seqfold_aos48(ctx, a, na, b, nb, is_dense, s));
+    const uint32_t cp = is_dense ? (uint32_t)(na + nb) : (uint32_t)s[3];
+    const double dn = is_dense ? (double)(na + nb) : (double)cp;
+    c[0] = s[0] / dn; c[1] = s[1] / dn; c[2] = s[2] / dn; c[3] = 0.0 / dn;
+    if (count) *count = cp;
+    return PCP_OK;
+}
+
 int pcp_transform_aos48(pcp_ctx* ctx, const void* in, void* out, int64_t n, int is_dense, const double T[16]) {
     if (!ctx || n < 0 || (n > 0 && (!in || !out)) || !T) return set_error(ctx, PCP_ERR_ARG, "pcp_transform_aos48: bad arguments");
     if (n == 0) return PCP_OK;
@@ -438,20 +414,22 @@ int pcp_remove_duplicate(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, 
     return rc;
 }
 
-int pcp_get_rot_icp(pcp_ctx* ctx, const void* src, int64_t ns, const void* tmp, int64_t nt, double M[16],
-                    float rmax, int iters, int do_scale, double cell_size, float* err) {
+int pcp_get_rot_icp(pcp_ctx* ctx, const void* src, int64_t ns, int src_dense, const void* tmp, int64_t nt,
+                    int tmp_dense, double M[16], float rmax, int iters, int do_scale, double cell_size, float* err) {
     if (!ctx || ns < 0 || nt < 0 || (ns > 0 && !src) || (nt > 0 && !tmp) || !M || iters < 0)
         return set_error(ctx, PCP_ERR_ARG, "pcp_get_rot_icp: bad arguments");
     if (err) *err = -1.0f;
     for (int i = 0; i < 16; i++) M[i] = (i % 5 == 0) ? 1.0 : 0.0;
     if (ns == 0 || nt == 0) return PCP_OK;  // ICP fails: err < 0 (ICP.h:26-28)
     PCP_HIP(ctx, hipSetDevice(ctx->device));
-    // joint centroid over cloud_all = src ++ temp (point_cloud_helper.cpp:78-83)
-    double a[5], b[5];
-    PCP_TRY(sums_aos48_dev(ctx, src, ns, 1, a));
-    PCP_TRY(sums_aos48_dev(ctx, tmp, nt, 1, b));
-    const double dn = (double)(ns + nt);
-    const double c[3] = {(a[0] + b[0]) / dn, (a[1] + b[1]) / dn, (a[2] + b[2]) / dn};
+    // joint centroid over cloud_all = src ++ temp (point_cloud_helper.cpp:78-83): one sequential
+    // fold over the concatenation; cloud_all.is_dense = src.is_dense && temp.is_dense
+    // (PointCloud::operator+=), so a non-dense input skips non-finite points of both
+    double s[4];
+    const int joint_dense = src_dense && tmp_dense;
+    PCP_TRY(seqfold_aos48(ctx, src, ns, tmp, nt, joint_dense, s));
+    const double dn = joint_dense ? (double)(ns + nt) : (double)(uint32_t)s[3];  // size() / unsigned cp
+    const double c[3] = {s[0] / dn, s[1] / dn, s[2] / dn};
     float* fs = nullptr;
     float* ft = nullptr;
     PCP_TRY(dmalloc(ctx, &fs, 3 * (size_t)ns));

@@ -79,6 +79,11 @@ __device__ __forceinline__ bool finite3(double x, double y, double z) {
     return isfinite(x) && isfinite(y) && isfinite(z);
 }
 
+// compute3DCentroid's sequential fp64 fold of x/y/z over the AoS48 records seg0 ++ seg1, bit-exact
+// (fold.hip); s_host[3] = number of points summed (finite ones when !is_dense).
+int seqfold_aos48(pcp_ctx* ctx, const void* p0, int64_t n0, const void* p1, int64_t n1, int is_dense,
+                  double s_host[4]);
+
 // Exclusive scan of `n` uint32 values in place (values' total must fit uint32).
 // Returns the total through *total_dev (device, optional) and *total_host (optional, syncs).
 int scan_u32_inplace(pcp_ctx* ctx, uint32_t* data, int64_t n, uint32_t* total_host);

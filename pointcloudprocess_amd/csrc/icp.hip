@@ -507,7 +507,9 @@ constexpr uint32_t kMaxAge = 128;  // older caches are searched again (so the sl
 __device__ __forceinline__ uint32_t pack_dlb(float D, uint32_t launch) {
     return (__float_as_uint(fmaxf(D, 0.f)) & ~0xffu) | (launch & 0xffu);
 }
-// 16-byte record of a table by element index (32-bit byte offset: tables < 4 GB)
+// 16-byte record of a table by element index.  The byte offset is 32-bit (so the load can use
+// the saddr + 32-bit VGPR offset form): pcp_icp_check_sizes() keeps every table this reads
+// (the fp32 target incl. its far sentinel) below 2^28 records = 4 GB.
 template <typename V>
 __device__ __forceinline__ V ld16(const V* base, uint32_t idx) {
     return *(const V*)((const char*)base + (size_t)(idx * 16u));
@@ -1560,6 +1562,14 @@ __host__ __device__ int icp_solve(const double acc[24], int do_scale, double dT[
 
 extern "C" {
 
+int pcp_icp_check_sizes(int64_t n_target, int64_t nq) {
+    if (n_target < 0 || nq < 0) return PCP_ERR_ARG;
+    if (nq >= ((int64_t)1 << 31)) return PCP_ERR_ARG;
+    // ld16(): 32-bit byte offsets into the fp32 target (n_target records + the far sentinel)
+    if (n_target + 1 >= ((int64_t)1 << 28)) return PCP_ERR_CAPACITY;
+    return PCP_OK;
+}
+
 int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t q_stride, int64_t nq,
                    pcp_icp** out) {
     if (!ctx || !target || !out || nq < 0 || (nq > 0 && !q)) return PCP_ERR_ARG;
@@ -1568,7 +1578,10 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     *out = nullptr;
     if (q_stride == 0) q_stride = 3 * sizeof(float);
     if (q_stride % sizeof(float)) return pcp::set_error(ctx, PCP_ERR_ARG, "query stride must be whole floats");
-    if (nq >= ((int64_t)1 << 31)) return pcp::set_error(ctx, PCP_ERR_ARG, "ICP supports < 2^31 queries");
+    if (int rc = pcp_icp_check_sizes(target->n, nq)) {
+        return pcp::set_error(ctx, rc, rc == PCP_ERR_CAPACITY ? "ICP target must have < 2^28 - 1 points (32-bit record offsets)"
+                                                              : "ICP supports < 2^31 queries");
+    }
     if (target->g.nbricks * 64 >= ((int64_t)1 << 32) ||
         pcp::qbricks(target->g, 0) * pcp::qbricks(target->g, 1) * pcp::qbricks(target->g, 2) * PCP_QBRICK *
                 PCP_QBRICK * PCP_QBRICK >= ((int64_t)1 << 32))

@@ -260,7 +260,12 @@ int scan_u32_inplace(pcp_ctx* ctx, uint32_t* data, int64_t n, uint32_t* total_ho
         ctx->scan_epoch = 0;
     }
     ctx->scan_epoch = (ctx->scan_epoch + 1) & kEpochMask;
-    if (ctx->scan_epoch == 0) ctx->scan_epoch = 1;  // 0: the cleared state
+    if (ctx->scan_epoch == 0) {
+        // wrapped after 2^30 - 1 calls: a status word left by an older call with fewer tiles
+        // could carry the epoch about to be reused, so clear them all once (0: the cleared state)
+        PCP_HIP(ctx, hipMemsetAsync(ctx->scan_status, 0, (size_t)ctx->scan_tiles * sizeof(uint64_t), ctx->stream));
+        ctx->scan_epoch = 1;
+    }
     uint64_t* status = ctx->scan_status;
     uint32_t* ctr = (uint32_t*)(status + ctx->scan_tiles);
     hipLaunchKernelGGL(k_scan_lookback, dim3((unsigned)tiles), dim3(kLbBlock), 0, ctx->stream, data, n, status, ctr,

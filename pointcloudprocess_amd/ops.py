@@ -209,6 +209,15 @@ def centroid(ctx, cloud, is_dense=True):
     return np.array(c[:]), cnt.value
 
 
+def centroid_concat(ctx, a, b, is_dense=True):
+    """compute3DCentroid of a ++ b (the joint centroid of get_rot_icp)."""
+    c = (C.c_double * 4)()
+    cnt = C.c_uint32()
+    ctx.check(ctx.lib.pcp_centroid_concat_aos48(ctx.h, _ptr(a), a.shape[0], _ptr(b), b.shape[0], int(is_dense),
+                                                c, C.byref(cnt)))
+    return np.array(c[:]), cnt.value
+
+
 def transform(ctx, cloud, T, is_dense=True, out=None):
     out = torch.empty_like(cloud) if out is None else out
     Tm = _lib.f64arr(np.asarray(T, dtype=np.float64).reshape(16))
@@ -358,10 +367,11 @@ def icp_solve(acc, do_scale=False):
     return rc, np.array(dT[:]).reshape(4, 4)
 
 
-def get_rot_icp(ctx, src, temp, rmax, iters=20, do_scale=False, cell_size=0.0):
+def get_rot_icp(ctx, src, temp, rmax, iters=20, do_scale=False, cell_size=0.0, src_dense=True,
+                temp_dense=True):
     M = (C.c_double * 16)()
     err = C.c_float()
-    ctx.check(ctx.lib.pcp_get_rot_icp(ctx.h, _ptr(src), src.shape[0], _ptr(temp), temp.shape[0], M,
-                                      float(rmax), int(iters), int(do_scale), float(cell_size),
-                                      C.byref(err)))
+    ctx.check(ctx.lib.pcp_get_rot_icp(ctx.h, _ptr(src), src.shape[0], int(src_dense), _ptr(temp),
+                                      temp.shape[0], int(temp_dense), M, float(rmax), int(iters),
+                                      int(do_scale), float(cell_size), C.byref(err)))
     return float(err.value), np.array(M[:]).reshape(4, 4)

@@ -137,21 +137,28 @@ static void test_cloud_helpers_vs_oracle() {
     double emn[4], emx[4];
     ora_getminmax3d((const ora_point48*)cloud->points.data(), (int)cloud->size(), 1, emn, emx);
     for (int a = 0; a < 4; a++) CHECK(mn[a] == emn[a] && mx[a] == emx[a], "minmax axis %d", a);
-    // compute3DCentroid: fixed-order tree sum vs sequential fold
+    // getMinMax3D(cloud, PointT&, PointT&) (point_cloud_helper.h:22-57): x/y/z only
+    CloudItem pmn, pmx;
+    pmn.rgba = 7u; pmx.stamp_id = 9u;
+    PointCloudHelper::getMinMax3D(*cloud, pmn, pmx);
+    CHECK(pmn.x == emn[0] && pmn.y == emn[1] && pmn.z == emn[2] && pmx.x == emx[0] && pmx.y == emx[1] &&
+              pmx.z == emx[2] && pmn.rgba == 7u && pmx.stamp_id == 9u,
+          "minmax PointT overload");
+    // compute3DCentroid: the reference's sequential fold, bit for bit
     Vec4d c;
     PointCloudHelper::compute3DCentroid(*cloud, c);
     double ec[4];
     ora_centroid((const ora_point48*)cloud->points.data(), (int)cloud->size(), 1, ec);
-    for (int a = 0; a < 3; a++) CHECK(std::fabs(c[a] - ec[a]) <= 1e-12 * std::fabs(ec[a]), "centroid %d", a);
-    // remove_duplicate: same voxel structure as the oracle given the same centroid
+    for (int a = 0; a < 4; a++) CHECK(std::memcmp(&c[a], &ec[a], sizeof(double)) == 0, "centroid %d", a);
+    // remove_duplicate: every byte equal to the oracle with its own sequential centroid
     CloudPtr rd(new Cloud(*cloud));
     PointCloudHelper::remove_duplicate(rd, 0.04f);
     std::vector<ora_point48> er(cloud->size());
-    const int m = ora_remove_duplicate_c((const ora_point48*)cloud->points.data(), (int)cloud->size(), 1, 0.04f, c.v,
-                                         er.data());
+    const int m = ora_remove_duplicate((const ora_point48*)cloud->points.data(), (int)cloud->size(), 1, 0.04f,
+                                       er.data());
     CHECK((int)rd->size() == m, "remove_duplicate %zu vs %d", rd->size(), m);
-    if ((int)rd->size() == m)
-        CHECK(std::memcmp(rd->points.data(), er.data(), m * sizeof(ora_point48)) == 0, "remove_duplicate bytes");
+    CHECK((int)rd->size() == m && std::memcmp(rd->points.data(), er.data(), m * sizeof(ora_point48)) == 0,
+          "remove_duplicate bytes");
     // VoxelGrid with anisotropic leaf, downsample_all off
     VoxelGrid<CloudItem> vg;
     vg.setInputCloud(cloud);

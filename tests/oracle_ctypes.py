@@ -48,6 +48,8 @@ def load():
     lib.ora_getminmax3d.argtypes = [vp, C.c_int, C.c_int, vp, vp]
     lib.ora_centroid.argtypes = [vp, C.c_int, C.c_int, vp]
     lib.ora_centroid.restype = C.c_uint
+    lib.ora_centroid_concat.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp]
+    lib.ora_centroid_concat.restype = C.c_uint
     lib.ora_transform.argtypes = [vp, vp, C.c_int, C.c_int, vp]
     lib.ora_voxel_filter.argtypes = [vp, C.c_int, C.c_int, C.c_double, C.c_double,
                                      C.c_double, C.c_int, vp, vp]
@@ -65,8 +67,8 @@ def load():
     lib.ora_icp.restype = C.c_double
     lib.ora_icp.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_float, C.c_int, C.c_int, C.c_int]
     lib.ora_get_rot_icp.restype = C.c_float
-    lib.ora_get_rot_icp.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_float, C.c_int,
-                                    C.c_int, C.c_int]
+    lib.ora_get_rot_icp.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.c_float,
+                                    C.c_int, C.c_int, C.c_int]
     _lib = lib
     return lib
 
@@ -162,6 +164,14 @@ def centroid(cloud, is_dense=True):
     return c
 
 
+def centroid_concat(a, b, is_dense=True):
+    lib = load()
+    c = np.zeros(4)
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    lib.ora_centroid_concat(a.ctypes.data, len(a), b.ctypes.data, len(b), int(is_dense), c.ctypes.data)
+    return c
+
+
 def minmax(cloud, is_dense=True):
     lib = load()
     mn, mx = np.zeros(4), np.zeros(4)
@@ -254,11 +264,12 @@ def icp(tgt, q, T0, rmax, iters, do_scale=False, nthreads=0):
     return err, T.reshape(4, 4)
 
 
-def get_rot_icp(src, tmp, rmax, iters, do_scale=False, nthreads=0):
+def get_rot_icp(src, tmp, rmax, iters, do_scale=False, nthreads=0, src_dense=True, tmp_dense=True):
     lib = load()
     src = np.ascontiguousarray(src)
     tmp = np.ascontiguousarray(tmp)
     M = np.zeros(16)
-    err = lib.ora_get_rot_icp(src.ctypes.data, len(src), tmp.ctypes.data, len(tmp),
-                              M.ctypes.data, float(rmax), int(iters), int(do_scale), nthreads)
+    err = lib.ora_get_rot_icp(src.ctypes.data, len(src), int(src_dense), tmp.ctypes.data, len(tmp),
+                              int(tmp_dense), M.ctypes.data, float(rmax), int(iters), int(do_scale),
+                              nthreads)
     return float(err), M.reshape(4, 4)

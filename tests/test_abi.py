@@ -62,3 +62,16 @@ def test_solve_vs_oracle():
         assert rc == 0 and erc == 0
         assert np.abs(dT - edT).max() < 1e-9
         assert np.abs(dT - T).max() < 1e-9
+
+
+def test_icp_size_guard():
+    """ld16's 32-bit record offsets (icp.hip): targets of >= 2^28 - 1 points are rejected
+    with PCP_ERR_CAPACITY instead of wrapping; queries are limited to < 2^31."""
+    from pointcloudprocess_amd import _lib
+    lib = _lib.load()
+    assert lib.pcp_icp_check_sizes(50_000_000, 50_000_000) == 0
+    assert lib.pcp_icp_check_sizes((1 << 28) - 2, 1) == 0
+    assert lib.pcp_icp_check_sizes((1 << 28) - 1, 1) == -7
+    assert lib.pcp_icp_check_sizes(1 << 30, 1) == -7
+    assert lib.pcp_icp_check_sizes(10, 1 << 31) == -1
+    assert lib.pcp_icp_check_sizes(-1, 1) == -1

@@ -207,3 +207,16 @@ def test_knn_lod_contract():
     assert idx[0] == 17
     exact = np.argsort(((xyz - q) ** 2).sum(1))[:4]
     assert set(idx.tolist()) <= set(exact.tolist()) | {-1}
+
+
+def test_near_face_cloud_needs_the_sequential_fold():
+    """Why remove_duplicate needs compute3DCentroid's exact sequential fold: on a cloud with
+    points within 1e-12 m of voxel faces, a blocked (tree-order) centroid changes the output
+    (tests/test_gpu_cloud.py::test_remove_duplicate_near_faces uses this cloud)."""
+    import test_gpu_cloud as tg
+    c = tg._near_face_cloud(200_000, 0.04, 17)
+    xyz = np.stack([c["x"], c["y"], c["z"]], 1)
+    blocked = np.append(xyz.reshape(-1, 1000, 3).sum(axis=1).sum(axis=0) / len(xyz), 0.0)
+    e = ora.remove_duplicate(c, 0.04)
+    e2 = ora.remove_duplicate_c(c, 0.04, blocked)
+    assert len(e) != len(e2) or e.tobytes() != e2.tobytes()
