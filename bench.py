@@ -1,17 +1,28 @@
 #!/usr/bin/env python3
 """Benchmark of the hot path on MI355X (contract: one JSON line from rank 0).
 
-Workload (BASELINE.json metric "Mcorrespondences/s + ICP iter/s, 50M-vs-50M fp32"):
-config C4 -- a point_cloud_closure / get_rot_icp registration: build the fp32 grid index of
-a 50M-point target, sort the 50M-point query set, then 20 ICP iterations (fused
-transform + exact 1-NN within rmax + 24 accumulators per iteration, Kabsch solve on the
-device; the pose never leaves HBM during the 20 iterations).
+Workload (BASELINE.json metric "Mcorrespondences/s + ICP iter/s, 50M-vs-50M fp32 @ 1/2/4/8
+MI355X"): config C4 -- a point_cloud_closure / get_rot_icp registration of a 50M-point query
+cloud against a 50M-point target: build the fp32 grid index of the target, sort the queries,
+then 20 ICP iterations (fused transform + exact 1-NN within rmax + 24 accumulators per
+iteration, Kabsch solve on the device; the pose never leaves HBM during the 20 iterations).
 One "step" = one such full registration; inputs (fp32 xyz) are resident in HBM before the
-timed region.  N GPUs: each rank registers its own 50M-vs-50M tile of a larger scene
-(co-partitioned target/query, weak scaling); the only collective is the all-reduce of the
-24 accumulators per iteration (RCCL over xGMI).
+timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 50000000] [--iters 20]
+N GPUs (one process per GPU; `--gpus N` without torchrun re-launches itself under
+torch.distributed.run from a parent that never touches the GPU):
+  --mode slab     (headline, STRONG scaling) the SAME 50M-vs-50M registration split into N
+                  x-slabs: a rank owns the queries of its slab and indexes the targets of the
+                  slab widened by a halo; a device guard certifies each iteration that the pose
+                  keeps the owned queries inside the halo.  Collective per iteration:
+                  all_reduce(SUM) of the 24 accumulators (RCCL over xGMI).
+  --mode sharded  the north_star layout: the target sharded by x-slab, queries replicated;
+                  per iteration ReduceScatter(MIN) of 8-byte (d2, index) keys per query, then
+                  all_reduce(SUM) of the 24 accumulators of each rank's query slice.
+  --mode weak     WEAK scaling: each rank registers its own 50M-vs-50M tile.
+At N > 1 the line also carries the two other modes under "alt_modes" (--no-alt skips them).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode slab|sharded|weak] [--n 50000000]
 """
 import argparse
 import glob
@@ -19,21 +30,49 @@ import hashlib
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from pointcloudprocess_amd import ops, synth  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_CORR = 32         # 12 query + 12 target + 8 (idx, d2)
 METRIC = "Mcorrespondences/s + ICP iter/s, 50M-vs-50M fp32 @ 1/2/4/8 MI355X"
+ICP_KERNELS = ("k_icp_verify", "k_icp_octant", "k_icp_ring")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", choices=("slab", "sharded", "weak"), default="slab")
+    ap.add_argument("--n", type=int, default=50_000_000, help="points per cloud (per GPU in weak mode)")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rmax", type=float, default=0.25)
+    ap.add_argument("--cell", type=float, default=0.12, help="ICP target grid cell (m); swept 0.1-0.16, 0.12 best")
+    ap.add_argument("--halo", type=float, default=2.0, help="slab mode: target halo (m), >= rmax + motion")
+    ap.add_argument("--cpu-n", type=int, default=2_000_000, help="CPU baseline sample (all threads)")
+    ap.add_argument("--cpu-iters1", type=int, default=3, help="CPU baseline iterations on 1 thread")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-alt", action="store_true", help="N > 1: skip the alt_modes runs")
+    return ap.parse_args()
+
+
+def launch(args):
+    """Parent of an N-GPU run: start N ranks under torch.distributed.run and exit with their
+    status.  Nothing here initialises the GPU (no HIP call before the children exist)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def pmc_traffic():
@@ -57,7 +96,7 @@ def pmc_traffic():
             return None
         iters = ks["k_icp_octant"]["launches"]
         tot = 0.0
-        for k in ("k_icp_verify", "k_icp_octant", "k_icp_ring"):
+        for k in ICP_KERNELS:
             e = ks.get(k)
             if e is not None:
                 tot += e["launches"] * (e["fetch_bytes_avg"] + (e["write_bytes_avg"] or 0.0))
@@ -65,164 +104,251 @@ def pmc_traffic():
     return None
 
 
-def parse():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=50_000_000, help="points per cloud per GPU")
-    ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--rmax", type=float, default=0.25)
-    ap.add_argument("--cell", type=float, default=0.12, help="ICP target grid cell (m); swept 0.1-0.16, 0.12 best")
-    ap.add_argument("--cpu-n", type=int, default=2_000_000, help="CPU baseline sample size")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--host-loop", action="store_true", help="host solve per iteration (one round trip each)")
-    return ap.parse_args()
+def cpu_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        out = subprocess.check_output(["lscpu"], text=True, timeout=10)
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return model, os.cpu_count(), len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(args, T_true):
-    """Oracle (C restatement, kd-tree + OpenMP) on a bounded sample of the same workload."""
+def cpu_baseline(args, T_true, synth):
+    """The oracle's ICP (C restatement: kd-tree + OpenMP correspondences, per-thread
+    accumulators) on bounded samples of the same workload, timed on this host.  The kd-tree
+    build and the 20 iterations are timed separately; `value` is the iteration rate with
+    the process's CPU share (OMP_NUM_THREADS, the threads this box allots to one GPU)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ctypes as ora  # test infrastructure: the checker / baseline only
+    import numpy as np
+    model, ncpu, naff = cpu_info()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or naff
+
     n = args.cpu_n
-    side = 200.0 * math.sqrt(n / float(args.n))  # same point density as the GPU tile
+    side = 200.0 * math.sqrt(n / float(args.n))  # same point density as the GPU cloud
     tgt, q = synth.icp_pair(n, n, 4001, 4002, T_true, extent=(side, side), device="cpu")
     tgt, q = tgt.numpy(), q.numpy()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    threads = min(threads, 16)
-    t0 = time.perf_counter()
-    err, T = ora.icp(tgt, q, np.eye(4), args.rmax, args.iters, nthreads=threads)
-    dt = time.perf_counter() - t0
+
+    def run(nthreads, iters):
+        err, T, bs, its = ora.icp_timed(tgt, q, np.eye(4), args.rmax, iters, nthreads=nthreads)
+        return n * iters / its / 1e6, bs, its
+
+    v_all, b_all, i_all = run(threads, args.iters)
+    v_1, b_1, i_1 = run(1, args.cpu_iters1)
     return {
-        "value": round(n * args.iters / dt / 1e6, 3),
+        "value": round(v_all, 3),
         "unit": "Mcorrespondences/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n}-vs-{n} pts, {args.iters} ICP iters (kd-tree build + iterations), same density "
-                  f"({side:.0f}x{side:.0f} m tile), oracle/pcp_oracle.c ora_icp, {dt:.2f} s",
+        "sample": f"{n}-vs-{n} pts (same density, {side:.0f}x{side:.0f} m tile), {args.iters} ICP "
+                  f"iters of oracle/pcp_oracle.c ora_icp_timed: iterations {i_all:.2f} s (timed, = value), kd-tree "
+                  f"build {b_all:.2f} s (not in value)",
+        "value_1core": round(v_1, 3),
+        "sample_1core": f"the same {n}-vs-{n} pts, first {args.cpu_iters1} ICP iters on 1 thread: iterations "
+                        f"{i_1:.2f} s, build {b_1:.2f} s",
+        "cores_all": threads,
+        "value_all": round(v_all, 3),
+        "nproc": ncpu,
+        "affinity_cpus": naff,
+        "cpu_model": model,
+        "threads_note": "OMP_NUM_THREADS = the CPU share of one GPU on this box (the harness allots 16 threads "
+                        "per GPU); nproc shows the whole host",
     }
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from pointcloudprocess_amd import distributed as D
+    from pointcloudprocess_amd import ops, synth
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}", file=sys.stderr)
+    # rehearsal knobs (multi-rank logic on a one-GPU box): PCP_BENCH_DEVICE pins every rank to
+    # one device, PCP_BENCH_BACKEND=gloo replaces RCCL.  The driver's runs use neither.
+    local = int(os.environ.get("PCP_BENCH_DEVICE", local))
+    backend = os.environ.get("PCP_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     ctx = ops.Context(local)
-
     T_true = synth.rigid()
     n = args.n
-    # rank tile: same density, its own seeds, shifted along x (co-partitioned weak scaling)
-    tgt, q = synth.icp_pair(n, n, 4001 + 1000 * rank, 4002 + 1000 * rank, T_true, device=dev)
-    if rank:
-        shift = torch.tensor([200.0 * rank, 0.0, 0.0], device=dev, dtype=torch.float32)
-        tgt = tgt + shift
-        q = synth.apply_inverse(synth.apply_inverse(q, np.linalg.inv(T_true)) + shift, T_true)
-    tgt = tgt.contiguous()
-    q = q.contiguous()
-    torch.cuda.synchronize()
 
-    acc_buf = torch.zeros(24, dtype=torch.float64, device=dev)
-    kernel = {"ms": 0.0, "launches": 0}
-    result = {}
+    def barrier():
+        if world > 1:
+            dist.barrier()
 
-    def one_step(timed):
-        index = ops.GridIndex(ctx, tgt, cell_size=args.cell)
-        icp = ops.ICP(index, q)
-        if args.host_loop:  # reference-style loop: host solve, one round trip per iteration
-            T = np.eye(4)
-            err = -1.0
-            for _ in range(args.iters):
-                acc = icp.step(T, args.rmax)
-                ms, nl = icp.last_kernel_ms()
-                if timed:
-                    kernel["ms"] += ms
-                    kernel["launches"] += nl
-                    kernel["fallback"] = kernel.get("fallback", 0) + icp.last_fallback()
-                if world > 1:
-                    acc_buf.copy_(acc)
-                    dist.all_reduce(acc_buf)
-                    a = acc_buf.cpu().numpy()
-                else:
-                    a = acc.cpu().numpy()
-                rc, dT = ops.icp_solve(a)
-                if rc != 0:
-                    err = -1.0
-                    break
-                err = math.sqrt(a[22] / a[0])
-                T = dT @ T
-        else:  # device-resident loop: pose, solve and all-reduce stay on the GPU stream
-            T_dev, stats = icp.new_pose()
-            for _ in range(args.iters):
-                acc = icp.step_dev(T_dev, args.rmax)
-                if world > 1:
-                    dist.all_reduce(acc)
-                icp.solve_dev(acc, T_dev, stats)
-            ms, nl = icp.kernel_ms()  # waits for the step
-            st = stats.cpu().numpy()
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def run_mode(mode, steps, warmup):
+        """Timed registrations of one mode; returns the per-mode record (rank-uniform)."""
+        kernel = {"ms": 0.0, "launches": 0, "fallback": 0.0}
+        exch = []
+        info = {"guard_ok": True}
+        if mode == "weak":  # each rank its own tile (same density, own seeds, shifted along x)
+            tgt, q = synth.icp_pair(n, n, 4001 + 1000 * rank, 4002 + 1000 * rank, T_true, device=dev)
+            if rank:
+                shift = torch.tensor([200.0 * rank, 0.0, 0.0], device=dev, dtype=torch.float32)
+                tgt = tgt + shift
+                q = synth.apply_inverse(synth.apply_inverse(q, np.linalg.inv(T_true)) + shift, T_true)
+            tile_t, tile_q = tgt.contiguous(), q.contiguous()
+            units = n * world
+            del tgt, q
+        else:  # one 50M-vs-50M registration, split across the ranks
+            tgt, q = synth.icp_pair(n, n, 4001, 4002, T_true, device=dev)
+            units = n
+            if mode == "slab":
+                xs = torch.sort(q[:, 0]).values
+                b = [-math.inf] + [float(xs[(n * r) // world].item()) for r in range(1, world)] + [math.inf]
+                del xs
+                lo, hi = b[rank], b[rank + 1]
+                qm = (q[:, 0] >= lo) & (q[:, 0] < hi)
+                tm = (tgt[:, 0] >= lo - args.halo) & (tgt[:, 0] < hi + args.halo)
+                tile_q, tile_t = q[qm].contiguous(), tgt[tm].contiguous()
+                mn, mx = tile_q.min(0).values.double().cpu().numpy(), tile_q.max(0).values.double().cpu().numpy()
+                guard = ([mn[0], mx[0], mn[1], mx[1], mn[2], mx[2]], lo - args.halo + args.rmax,
+                         hi + args.halo - args.rmax)
+                info["halo_m"] = args.halo
+                del tgt, q
+            else:  # sharded: x-sorted target, equal-count contiguous shards; queries replicated
+                tgt = tgt[torch.argsort(tgt[:, 0])].contiguous()
+                lo_i, hi_i = D.shard_range(n, world, rank)
+                tile_t, tile_q = tgt[lo_i:hi_i].contiguous(), q.contiguous()
+                tgt_all = tgt
+                del q
+        torch.cuda.synchronize()
+        result = {}
+
+        def one_step(timed):
+            st = {}
+            eng = D.GpuEngine(ctx, tile_t, tile_q, cell_size=args.cell)
+            if mode == "sharded":
+                err, T = D.run_target_sharded_dev(eng, np.eye(4), args.rmax, args.iters, lo_i, tile_q, tgt_all,
+                                                  exchange=exch if timed else None)
+                ok = True
+            else:
+                err, T, ok = D.run_slab_dev(eng, np.eye(4), args.rmax, args.iters,
+                                            guard=guard if mode == "slab" else None,
+                                            exchange=exch if timed else None, out_stats=st)
+            ms, nl = eng.icp.kernel_ms()
             if timed:
                 kernel["ms"] += ms
                 kernel["launches"] += nl
-                kernel["fallback"] = kernel.get("fallback", 0) + st[2]
-            T = T_dev.cpu().numpy().reshape(4, 4)
-            err = float(st[1]) if st[0] == 0 and st[3] == args.iters else -1.0
-        result["T"], result["err"], result["nq"] = T, err, icp.q.shape[0]
-        icp.close()
-        index.close()
+                kernel["fallback"] += st.get("fallback", 0.0)
+                info["guard_ok"] = info["guard_ok"] and ok
+            result["T"], result["err"], result["nq"] = T, err, eng.icp.q.shape[0]
+            eng.close()
 
-    for _ in range(args.warmup):
-        one_step(False)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        for _ in range(warmup):
+            one_step(False)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one_step(True)
+        torch.cuda.synchronize()
+        barrier()
+        dt = max_over_ranks(time.perf_counter() - t0)
+        exch_ms = (sum(a.elapsed_time(b) for a, b in exch) / len(exch)) if exch else 0.0
+        rec = {
+            "value": units * args.iters * steps / dt / 1e6,
+            "ms_per_step": dt / steps * 1e3,
+            "icp_iter_per_s": args.iters * steps / dt,
+            "exchange_ms_per_iter": max_over_ranks(exch_ms),
+            "guard_ok": bool(max_over_ranks(0.0 if info["guard_ok"] else 1.0) == 0.0),
+            "T": result["T"], "err": result["err"],
+            "kernel_avg_ms": kernel["ms"] / max(kernel["launches"], 1),
+            "units_per_launch": result["nq"],
+            "queries_all_ranks": sum_over_ranks(float(result["nq"])),
+            "fallback_frac": kernel["fallback"] / max(1.0, result["nq"] * kernel["launches"]),
+        }
+        rec.update({k: v for k, v in info.items() if k != "guard_ok"})
+        del tile_t, tile_q
+        torch.cuda.empty_cache()
+        return rec
 
-    corr_total = n * world * args.iters * args.steps
-    value = corr_total / dt / 1e6
-    k_avg_ms = kernel["ms"] / max(kernel["launches"], 1)
-    traffic = pmc_traffic()
-    achieved = BYTES_PER_CORR * n / (k_avg_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes / launch
+    main_rec = run_mode(args.mode, args.steps, args.warmup)
+    alt = {}
+    if world > 1 and not args.no_alt:
+        for m in ("slab", "sharded", "weak"):
+            if m != args.mode:
+                r = run_mode(m, max(1, args.steps), 1)
+                alt[m] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items() if k not in ("T",)}
+                alt[m]["T_err_vs_truth"] = float(np.abs(r["T"] - T_true).max())
+
     if rank == 0:
-        T_err = float(np.abs(result["T"] - T_true).max())
+        r = main_rec
+        traffic = pmc_traffic()
+        k_avg_ms = r["kernel_avg_ms"]
+        achieved = BYTES_PER_CORR * r["units_per_launch"] / (k_avg_ms * 1e-3) / 1e9  # algorithmic GB/s per launch
+        par = {"slab": f"x-slabs x{world}: owned queries + targets of the slab +- {args.halo} m halo per rank; "
+                       "RCCL all_reduce(SUM) of 24 fp64 accumulators per iteration",
+               "sharded": f"target sharded x{world} (x-slabs), queries replicated; RCCL ReduceScatter(MIN) of 8-B "
+                          "(d2, index) keys per query + all_reduce(SUM) of 24 fp64 per iteration",
+               "weak": f"co-partitioned tiles x{world} (each rank its own 50M-vs-50M); all_reduce(SUM) of 24 fp64"}
         line = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": round(r["value"], 3),
             "unit": "Mcorrespondences/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "ms_per_step": round(r["ms_per_step"], 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.mode == "weak" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic street scene (ground+facades+poles, seeded); query = independent "
                     "resample moved by a known rigid motion",
             "config": {"workload": "C4: 50M-vs-50M get_rot_icp/point_cloud_closure ICP, 20 iters "
                                    "(index build + query sort + iterations per step)",
-                       "points_per_gpu": n, "iters": args.iters, "rmax_m": args.rmax,
-                       "cell_m": args.cell, "parallelism": f"co-partitioned tiles x{world}, "
-                                                           "RCCL all-reduce of 24 accumulators"},
-            "icp_iter_per_s": round(args.iters * args.steps / dt, 3),
-            "icp_final_rms_m": round(result["err"], 6),
-            "icp_max_abs_T_err_vs_truth": T_err,
+                       "points_per_cloud": n, "iters": args.iters, "rmax_m": args.rmax,
+                       "cell_m": args.cell, "mode": args.mode, "parallelism": par[args.mode]},
+            "icp_iter_per_s": round(r["icp_iter_per_s"], 3),
+            "icp_final_rms_m": round(r["err"], 6),
+            "icp_max_abs_T_err_vs_truth": float(np.abs(r["T"] - T_true).max()),
+            "halo_guard_ok": r["guard_ok"],
+            "exchange_ms_per_iter": round(r["exchange_ms_per_iter"], 4),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_icp_step",
+                "kernel": "+".join(ICP_KERNELS) + " (one ICP iteration; aggregate of the three passes and "
+                                                  "their list compactions)",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -232,18 +358,20 @@ def main():
                 "traffic_source": traffic[1] if traffic else None,
                 "kernel_avg_ms": round(k_avg_ms, 4),
                 "bytes_per_unit": BYTES_PER_CORR,
-                "units_per_launch": n,
-                "launch_includes": "per iteration: k_icp_verify (candidate caches) + k_icp_octant (search "
-                                   "list) + k_icp_ring (fallback) with their list compactions",
-                "fallback_frac": round(kernel.get("fallback", 0) / max(1, n * kernel["launches"]), 5),
+                "units_per_launch": r["units_per_launch"],
+                "launch_includes": "per iteration on rank 0: k_icp_verify (candidate caches) + k_icp_octant "
+                                   "(search list) + k_icp_ring (fallback) with their list compactions",
+                "fallback_frac": round(r["fallback_frac"], 5),
             },
-            "cpu_baseline": None if args.no_cpu else cpu_baseline(args, T_true),
+            "alt_modes": alt or None,
+            "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(args, T_true, synth),
         }
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

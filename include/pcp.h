@@ -211,6 +211,24 @@ int pcp_icp_accumulate_keys(pcp_ctx* ctx, pcp_icp* icp, const double T_host[16],
                             const uint64_t* keys_dev, int64_t lo, int64_t hi,
                             const float* shard_xyz_dev, size_t shard_stride_bytes,
                             double* acc_dev);
+/* Device-resident form of the target-sharded loop (pose T_dev: row-major 4x4 doubles in HBM):
+ * pcp_icp_keys_dev = pcp_icp_keys at the device pose.  After a ReduceScatter(MIN) of the keys
+ * (each rank keeps the keys of its slice of queries, original order), pcp_icp_accumulate_slice
+ * writes the 24 accumulators of that slice: q_dev = the slice's queries, keys_dev = its
+ * reduced keys, tgt_dev = the full target array indexed by the keys' global indices.  A SUM
+ * over ranks then gives the accumulators of every query (point_cloud_helper.cpp:75-166 ICP
+ * correspondence/transform step). */
+int pcp_icp_keys_dev(pcp_ctx* ctx, pcp_icp* icp, const double* T_dev, float rmax,
+                     int64_t target_offset, uint64_t* keys_dev);
+int pcp_icp_accumulate_slice(pcp_ctx* ctx, const double* T_dev, const float* q_dev,
+                             size_t q_stride_bytes, int64_t nq, const uint64_t* keys_dev,
+                             const float* tgt_dev, size_t tgt_stride_bytes, double* acc_dev);
+/* Co-partitioned (slab) multi-GPU mode: latch *flag_dev = 1 when the owned queries' box
+ * (host, {x0,x1,y0,y1,z0,z1}) under the device pose reaches outside x in [lo, hi], i.e.
+ * the rank's target halo no longer certifies its correspondences (one thread, on the
+ * context stream). */
+int pcp_slab_guard(pcp_ctx* ctx, const double* T_dev, const double box_host[6], double lo,
+                   double hi, int* flag_dev);
 /* Host Kabsch/Umeyama solve of the increment dT from 24 accumulators (host memory). */
 int pcp_icp_solve(const double acc_host[24], int do_scale, double dT_host[16]);
 /* Full loop: T_inout (row-major), `iters` iterations (stops early when the increment's

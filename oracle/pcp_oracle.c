@@ -828,9 +828,36 @@ static void mat4_mul(const double A[16], const double B[16], double C[16]) {
     memcpy(C, t, sizeof(t));
 }
 
-double ora_icp(const float* tgt, int nt, const float* q, int nq, double T[16], float rmax,
-               int iters, int do_scale, int nthreads) {
+/* accumulators over a static partition of the queries (one partial per thread, combined in
+ * thread order): what a multi-core CPU ICP does; equals ora_icp_accumulate up to rounding */
+static void icp_accumulate_par(const float* tgt, const float* q, int nq, const float R[9], const float tr[3],
+                               const int* idx, const float* d2, double acc[24], int nthreads) {
+    int nt = 1;
+#ifdef _OPENMP
+    nt = nthreads > 0 ? nthreads : omp_get_max_threads();
+#endif
+    if (nt <= 1 || nq < 65536) { ora_icp_accumulate(tgt, q, nq, R, tr, idx, d2, acc); return; }
+    double* part = (double*)calloc((size_t)nt * 24, sizeof(double));
+#pragma omp parallel for num_threads(nt) schedule(static, 1)
+    for (int t = 0; t < nt; t++) {
+        const int lo = (int)((int64_t)nq * t / nt), hi = (int)((int64_t)nq * (t + 1) / nt);
+        ora_icp_accumulate(tgt, q + 3 * (size_t)lo, hi - lo, R, tr, idx + lo, d2 + lo, part + 24 * t);
+    }
+    memset(acc, 0, 24 * sizeof(double));
+    for (int t = 0; t < nt; t++)
+        for (int k = 0; k < 24; k++) acc[k] += part[24 * t + k];
+    free(part);
+}
+
+double ora_icp_timed(const float* tgt, int nt, const float* q, int nq, double T[16], float rmax,
+                     int iters, int do_scale, int nthreads, int par_acc, double* build_s, double* iter_s) {
+#ifdef _OPENMP
+    double t0 = omp_get_wtime();
+#endif
     ora_f32index* ix = ora_f32index_build(tgt, nt);
+#ifdef _OPENMP
+    double t1 = omp_get_wtime();
+#endif
     int* idx = (int*)malloc((size_t)(nq > 0 ? nq : 1) * sizeof(int));
     float* d2 = (float*)malloc((size_t)(nq > 0 ? nq : 1) * sizeof(float));
     double err = -1.0;
@@ -842,14 +869,28 @@ double ora_icp(const float* tgt, int nt, const float* q, int nq, double T[16], f
         }
         ora_icp_correspond(ix, q, nq, R, tr, rmax, idx, d2, nthreads);
         double acc[24], dT[16];
-        ora_icp_accumulate(tgt, q, nq, R, tr, idx, d2, acc);
+        if (!par_acc || nthreads == 1) ora_icp_accumulate(tgt, q, nq, R, tr, idx, d2, acc);
+        else icp_accumulate_par(tgt, q, nq, R, tr, idx, d2, acc, nthreads);
         if (ora_icp_solve(acc, do_scale, dT) != 0) { err = -1.0; break; }
         err = sqrt(acc[22] / acc[0]);
         mat4_mul(dT, T, T);
     }
+#ifdef _OPENMP
+    double t2 = omp_get_wtime();
+    if (build_s) *build_s = t1 - t0;
+    if (iter_s) *iter_s = t2 - t1;
+#else
+    if (build_s) *build_s = 0;
+    if (iter_s) *iter_s = 0;
+#endif
     free(idx); free(d2);
     ora_f32index_free(ix);
     return err;
+}
+
+double ora_icp(const float* tgt, int nt, const float* q, int nq, double T[16], float rmax,
+               int iters, int do_scale, int nthreads) {
+    return ora_icp_timed(tgt, nt, q, nq, T, rmax, iters, do_scale, nthreads, 0, NULL, NULL);
 }
 
 float ora_get_rot_icp(const ora_point48* src, int ns, int src_dense, const ora_point48* tmp, int nt, int tmp_dense,

@@ -144,6 +144,10 @@ int ora_icp_solve(const double acc[24], int do_scale, double dT[16]);
 
 /* Full ICP: T (row-major 4x4 double, in: initial, out: result). Returns RMS error of the
  * last iteration's correspondences or -1 on failure. */
+/* ora_icp with the index build and the iterations timed separately (wall seconds); par_acc:
+ * accumulators over per-thread partials (the CPU baseline; equal up to rounding) */
+double ora_icp_timed(const float* tgt, int nt, const float* q, int nq, double T[16], float rmax,
+                     int iters, int do_scale, int nthreads, int par_acc, double* build_s, double* iter_s);
 double ora_icp(const float* tgt, int nt, const float* q, int nq, double T[16], float rmax,
                int iters, int do_scale, int nthreads);
 

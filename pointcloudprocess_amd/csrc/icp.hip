@@ -855,8 +855,16 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             const float m = fminf(fminf(fminf(fx - (float)bx, (float)(bx + 2) - fx),
                                         fminf(fy - (float)by, (float)(by + 2) - fy)),
                                   fminf(fz - (float)bz, (float)(bz + 2) - fz)) - a.mc;
+            // a query farther than rmax from the grid's box (a target-sharded rank: the queries
+            // of the other shards) is settled "no correspondence" without a scan, with D = that
+            // distance (every target lies inside the box)
+            const float ox = fmaxf(fmaxf(-fx, fx - (float)g.n[0]), 0.f);
+            const float oy = fmaxf(fmaxf(-fy, fy - (float)g.n[1]), 0.f);
+            const float oz = fmaxf(fmaxf(-fz, fz - (float)g.n[2]), 0.f);
+            const float dout = fmaxf(sqrtf(__fmaf_rn(oz, oz, __fmaf_rn(oy, oy, ox * ox))) - a.mc, 0.f) * g.hf;
+            const bool outside = dout * dout > a.r2 * 1.0001f;
             // the 4 x-rows of the octant: all 8 row bounds at once
-            const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
+            const int xa = max(bx, 0), xb = outside ? -1 : min(bx + 1, g.n[0] - 1);
             uint32_t rs[4], rn[4];
 #pragma unroll
             for (int r = 0; r < 4; r++) {
@@ -918,7 +926,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
 #else
             const float dnext = b.d4;
 #endif
-            settled = (found ? (b.d0 < dnext && b.d0 <= cert2) : a.r2 <= cert2) || (a.dbg & kDbgNoFallback);
+            settled = (found ? (b.d0 < dnext && b.d0 <= cert2) : a.r2 <= cert2) || outside || (a.dbg & kDbgNoFallback);
             // the winner among the cached ties by target index (rare: only when d1 == d0)
             win = b.p0;
             if (found && b.d1 == b.d0) {
@@ -940,7 +948,8 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             // the cache: the 4 nearest; D bounds every uncached point
             // settled: D bounds every uncached point for the verify pass.  Unsettled: the fallback
             // pass (which overwrites the cache) gets the octant's first uncached d2 instead.
-            const float D = settled ? fminf(sqrtf(dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : dnext;
+            const float D = outside ? dout * 0.9999f
+                                    : (settled ? fminf(sqrtf(dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : dnext);
 #if PCP_CACHE3
             a.cand[i] = make_uint4(b.p0, b.p1, b.p2, pack_dlb(D, a.launch));
 #else
@@ -1223,6 +1232,74 @@ __global__ void __launch_bounds__(256) k_sum_partials(const double* part, int nb
         if (threadIdx.x == 0) out[k] = s[0];
         __syncthreads();
     }
+}
+
+// reduce-scatter form of the target-sharded mode: the accumulators of this rank's slice of the
+// queries (original order), whose global winners come from the MIN-reduced keys; the winner's
+// coordinates are read from the full (replicated) target array by global index.  The pose is
+// the device 4x4 (cast to fp32 exactly as k_pose_set does).
+__global__ void __launch_bounds__(256) k_acc_slice(const double* T, const float* q, size_t qs, int64_t n,
+                                                   const uint64_t* keys, const float* tgt, size_t ts, double* partials) {
+    float R[9], t[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) R[3 * r + c] = (float)T[4 * r + c];
+        t[r] = (float)T[4 * r + 3];
+    }
+    double acc[kAcc - 1];
+#pragma unroll
+    for (int k = 0; k < kAcc - 1; k++) acc[k] = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = keys[i];
+        if (key == kNoKey) continue;
+        const float* qp = q + (size_t)i * qs;
+        const float* p = tgt + (size_t)(key & 0xffffffffull) * ts;
+        const float x = __fmaf_rn(R[2], qp[2], __fmaf_rn(R[1], qp[1], __fmaf_rn(R[0], qp[0], t[0])));
+        const float y = __fmaf_rn(R[5], qp[2], __fmaf_rn(R[4], qp[1], __fmaf_rn(R[3], qp[0], t[1])));
+        const float z = __fmaf_rn(R[8], qp[2], __fmaf_rn(R[7], qp[1], __fmaf_rn(R[6], qp[0], t[2])));
+        const double qv[3] = {x, y, z}, pv[3] = {p[0], p[1], p[2]};
+        acc[0] += 1.0;
+#pragma unroll
+        for (int c = 0; c < 3; c++) { acc[1 + c] += qv[c]; acc[4 + c] += pv[c]; }
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) acc[7 + 3 * r + c] += qv[r] * pv[c];
+        acc[16] += qv[0] * qv[0]; acc[17] += qv[0] * qv[1]; acc[18] += qv[0] * qv[2];
+        acc[19] += qv[1] * qv[1]; acc[20] += qv[1] * qv[2]; acc[21] += qv[2] * qv[2];
+        acc[22] += (double)__uint_as_float((uint32_t)(key >> 32));
+    }
+    __shared__ double sm[4][kAcc];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kAcc - 1; k++) {
+        double v = acc[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) sm[wv][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kAcc) {
+        double v = 0.0;
+        if (threadIdx.x < kAcc - 1)
+            for (int w = 0; w < 4; w++) v += sm[w][threadIdx.x];
+        partials[(int64_t)blockIdx.x * kAcc + threadIdx.x] = v;
+    }
+}
+
+// co-partitioned slab guard (one thread): the owned queries' box [b0..b5] = {x0,x1,y0,y1,z0,z1}
+// under the device pose must keep x within [lo, hi] (the slab core widened by the target halo
+// less rmax); the x-extreme of an affine image of a box is at a corner.  Latches flag = 1.
+__global__ void k_slab_guard(const double* T, double b0, double b1, double b2, double b3, double b4, double b5,
+                             double lo, double hi, int* flag) {
+    const double bx[2] = {b0, b1}, by[2] = {b2, b3}, bz[2] = {b4, b5};
+    double mn = INFINITY, mx = -INFINITY;
+    for (int c = 0; c < 8; c++) {
+        const double x = T[0] * bx[c & 1] + T[1] * by[(c >> 1) & 1] + T[2] * bz[c >> 2] + T[3];
+        mn = fmin(mn, x);
+        mx = fmax(mx, x);
+    }
+    if (!(mn >= lo && mx <= hi)) *flag = 1;
 }
 
 // ---- query order (pcp_icp_create): queries sorted once by target-grid cell in brick-major
@@ -1781,6 +1858,57 @@ int pcp_icp_keys(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, int
     if (icp->nq > 0)
         hipLaunchKernelGGL(pcp::k_make_keys, dim3(pcp::grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, a,
                            (uint32_t)target_offset, keys_dev);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_icp_keys_dev(pcp_ctx* ctx, pcp_icp* icp, const double* T_dev, float rmax, int64_t target_offset,
+                     uint64_t* keys_dev) {
+    if (!ctx || !icp || !T_dev || !keys_dev || !(rmax >= 0.f) || target_offset < 0 ||
+        target_offset + pcp_index_size(icp->target) > ((int64_t)1 << 32))
+        return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    icp->ctx = ctx;
+    const int saved = icp->dbg;
+    icp->dbg |= pcp::kDbgNoAccum;  // correspondences only
+    pcp::IcpArgs a{};
+    const int rc = pcp::icp_launch(icp, nullptr, rmax, icp->acc, nullptr, nullptr, T_dev, &a);
+    icp->dbg = saved;
+    PCP_TRY(rc);
+    if (icp->nq_in > icp->nq)
+        hipLaunchKernelGGL(pcp::k_fill_keys, dim3(pcp::grid_for(icp->nq_in, 256)), dim3(256), 0, ctx->stream, keys_dev,
+                           icp->nq_in);
+    if (icp->nq > 0)
+        hipLaunchKernelGGL(pcp::k_make_keys, dim3(pcp::grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, a,
+                           (uint32_t)target_offset, keys_dev);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_icp_accumulate_slice(pcp_ctx* ctx, const double* T_dev, const float* q_dev, size_t q_stride, int64_t nq,
+                             const uint64_t* keys_dev, const float* tgt_dev, size_t tgt_stride, double* acc_dev) {
+    if (!ctx || !T_dev || nq < 0 || (nq > 0 && (!q_dev || !keys_dev || !tgt_dev)) || !acc_dev) return PCP_ERR_ARG;
+    if (q_stride == 0) q_stride = 3 * sizeof(float);
+    if (tgt_stride == 0) tgt_stride = 3 * sizeof(float);
+    if (q_stride % sizeof(float) || tgt_stride % sizeof(float))
+        return pcp::set_error(ctx, PCP_ERR_ARG, "strides must be whole floats");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    const int nb = (int)std::min<int64_t>(std::max<int64_t>(1, (nq + 255) / 256), 2048);
+    double* part = nullptr;
+    PCP_TRY(pcp::dmalloc(ctx, &part, (size_t)nb * pcp::kAcc));
+    hipLaunchKernelGGL(pcp::k_acc_slice, dim3(nb), dim3(256), 0, ctx->stream, T_dev, q_dev, q_stride / sizeof(float),
+                       nq, keys_dev, tgt_dev, tgt_stride / sizeof(float), part);
+    hipLaunchKernelGGL(pcp::k_sum_partials, dim3(1), dim3(256), 0, ctx->stream, (const double*)part, nb, acc_dev);
+    pcp::dfree(ctx, part);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_slab_guard(pcp_ctx* ctx, const double* T_dev, const double box[6], double lo, double hi, int* flag_dev) {
+    if (!ctx || !T_dev || !box || !flag_dev) return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(pcp::k_slab_guard, dim3(1), dim3(1), 0, ctx->stream, T_dev, box[0], box[1], box[2], box[3],
+                       box[4], box[5], lo, hi, flag_dev);
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }

@@ -8,12 +8,17 @@ differs between the two partitionings:
   tile + target tile widened by a halo >= the largest correspondence distance), so every
   correspondence is found locally; the only collective is all_reduce(SUM) of the 24 fp64
   accumulators per iteration (192 bytes).
+* slab (bench.py headline, strong scaling): ONE registration split by x-slabs -- a rank owns
+  the queries of its slab and indexes the targets of the slab widened by a halo; a device
+  guard certifies every iteration that the pose keeps the owned queries inside the halo.
+  Collective: all_reduce(SUM) of 24 doubles per iteration.
 * target-sharded (the north_star layout): each rank indexes one shard of the target, the
   query set is replicated.  Per iteration: per-query int64 keys (fp32 d2 bits << 32 |
-  global target index) -> all_reduce(MIN) gives the global lexicographic (d2, index)
-  winner; each rank accumulates the queries whose winner lies in its shard ->
-  all_reduce(SUM) of the 24 accumulators.  8 bytes per query per iteration cross xGMI, so
-  it scales worse than co-partitioning; it needs no spatial partition of the queries.
+  global target index) -> MIN over ranks gives the global lexicographic (d2, index)
+  winner (all_reduce + per-shard accumulation, or -- device-resident -- ReduceScatter(MIN)
+  + accumulation of each rank's query slice) -> all_reduce(SUM) of the 24 accumulators.
+  8 bytes per query per iteration cross xGMI, so it scales worse than co-partitioning; it
+  needs no spatial partition of the queries.
 
 An *engine* supplies the local compute:
     step(T, rmax) -> acc            (24 float64, torch tensor on the engine's device)
@@ -94,6 +99,105 @@ def run_target_sharded(engine, T0, rmax, iters, lo, hi, do_scale=False):
     return err, T
 
 
+NO_KEY = torch.iinfo(torch.int64).max
+
+
+def _reduce_scatter_min(out, inp):
+    """out <- this rank's equal slice of the element-wise MIN over ranks of inp (RCCL
+    ReduceScatter; gloo, which has none, reduces everything and keeps the slice)."""
+    world = _world()
+    if world == 1:
+        out.copy_(inp)
+    elif dist.get_backend() == "gloo":
+        dist.all_reduce(inp, op=dist.ReduceOp.MIN)
+        out.copy_(inp.view(world, -1)[dist.get_rank()])
+    else:
+        dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.MIN)
+    return out
+
+
+def run_target_sharded_dev(engine, T0, rmax, iters, lo, q_all, tgt_all, do_scale=False, exchange=None):
+    """The north_star layout with the pose on the device: every rank indexes its target shard
+    (global indices from lo) and holds the replicated queries.  Per iteration: keys at the
+    device pose -> ReduceScatter(MIN) (each rank keeps the reduced keys of its 1/G slice of
+    the queries, original order) -> accumulators of that slice (winners read from the full
+    target by global index) -> all_reduce(SUM) of 24 doubles -> device solve.  No host round
+    trip.  `exchange`: optional list that receives (start, end) CUDA event pairs around the
+    ReduceScatter of each iteration.  Returns (err, T), identical on every rank."""
+    world = _world()
+    rank = dist.get_rank() if world > 1 else 0
+    nq = q_all.shape[0]
+    chunk = -(-nq // world)
+    keys = torch.full((chunk * world,), NO_KEY, dtype=torch.int64, device=q_all.device)
+    mine = torch.empty(chunk, dtype=torch.int64, device=q_all.device)
+    q0, q1 = min(nq, rank * chunk), min(nq, (rank + 1) * chunk)
+    T_dev, stats = engine.new_pose(T0)
+    for _ in range(iters):
+        engine.keys_dev(T_dev, rmax, lo, keys)
+        ev = None
+        if exchange is not None and q_all.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        _reduce_scatter_min(mine, keys)
+        if ev is not None:
+            ev[1].record()
+            exchange.append(ev)
+        acc = engine.accumulate_slice(T_dev, q_all[q0:q1], mine, tgt_all)
+        _allreduce(acc, dist.ReduceOp.SUM)
+        engine.solve_dev(acc, T_dev, stats, do_scale)
+    st = stats.cpu().numpy()
+    T = T_dev.cpu().numpy().reshape(4, 4)
+    return (float(st[1]) if st[0] == 0 and st[3] == iters else -1.0), T
+
+
+def slab_bounds(x, world):
+    """x-slab boundaries (world + 1 values, -inf/+inf at the ends) cutting the values x into
+    equal-count slabs (the same on every rank for the same x)."""
+    xs = np.sort(np.asarray(x, dtype=np.float64))
+    b = [-np.inf]
+    for r in range(1, world):
+        b.append(float(xs[(len(xs) * r) // world]) if len(xs) else 0.0)
+    b.append(np.inf)
+    return b
+
+
+def slab_select(q_x, t_x, bounds, rank, halo):
+    """Masks of this rank's owned queries (x in [b_r, b_r+1)) and target tile (the slab
+    widened by `halo` on both sides)."""
+    lo, hi = bounds[rank], bounds[rank + 1]
+    return (q_x >= lo) & (q_x < hi), (t_x >= lo - halo) & (t_x < hi + halo)
+
+
+def run_slab_dev(engine, T0, rmax, iters, guard=None, do_scale=False, exchange=None, out_stats=None):
+    """Co-partitioned strong scaling of ONE registration: every rank owns an x-slab of the
+    queries and indexes the targets of that slab widened by a halo, so every correspondence
+    is found locally; the only collective is all_reduce(SUM) of the 24 accumulators per
+    iteration, on the device stream.  guard = (box, lo, hi): the owned queries' box and the x
+    range over which the halo certifies them; a device flag latches if the pose ever takes
+    the box outside (the result is then not certified).  Returns (err, T, guard_ok)."""
+    T_dev, stats = engine.new_pose(T0)
+    flag = torch.zeros(1, dtype=torch.int32, device=T_dev.device)
+    for _ in range(iters):
+        if guard is not None:
+            engine.slab_guard(T_dev, guard[0], guard[1], guard[2], flag)
+        acc = engine.step_dev(T_dev, rmax)
+        ev = None
+        if exchange is not None and T_dev.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        _allreduce(acc, dist.ReduceOp.SUM)
+        if ev is not None:
+            ev[1].record()
+            exchange.append(ev)
+        engine.solve_dev(acc, T_dev, stats, do_scale)
+    st = stats.cpu().numpy()
+    T = T_dev.cpu().numpy().reshape(4, 4)
+    ok = int(flag.cpu().item()) == 0
+    if out_stats is not None:
+        out_stats["fallback"] = float(st[2])  # queries that needed the exact fallback, all iterations
+    return (float(st[1]) if st[0] == 0 and st[3] == iters else -1.0), T, ok
+
+
 def shard_range(n, world, rank):
     """Equal-count contiguous shard [lo, hi) of n items."""
     lo = (n * rank) // world
@@ -125,6 +229,15 @@ class GpuEngine:
 
     def accumulate_keys(self, T, keys, lo, hi):
         return self.icp.accumulate_keys(T, keys, lo, hi, self.target)
+
+    def keys_dev(self, T_dev, rmax, offset, out=None):
+        return self.icp.keys_dev(T_dev, rmax, offset, out)
+
+    def accumulate_slice(self, T_dev, q, keys, tgt):
+        return ops.accumulate_slice(self.index.ctx, T_dev, q, keys, tgt, self.icp.acc)
+
+    def slab_guard(self, T_dev, box, lo, hi, flag):
+        ops.slab_guard(self.index.ctx, T_dev, box, lo, hi, flag)
 
     def close(self):
         self.icp.close()

@@ -327,6 +327,14 @@ class ICP:
         ctx.check(ctx.lib.pcp_icp_keys(ctx.h, self.h, Tm, float(rmax), int(target_offset), _ptr(keys)))
         return keys
 
+    def keys_dev(self, T_dev, rmax, target_offset=0, out=None):
+        """keys() at the device pose T_dev (no host round trip)."""
+        ctx = self.ctx
+        keys = torch.empty(self.nq_in, dtype=torch.int64, device=ctx.device) if out is None else out
+        assert keys.dtype == torch.int64 and keys.numel() >= self.nq_in and keys.is_contiguous()
+        ctx.check(ctx.lib.pcp_icp_keys_dev(ctx.h, self.h, _ptr(T_dev), float(rmax), int(target_offset), _ptr(keys)))
+        return keys
+
     def accumulate_keys(self, T, keys, lo, hi, shard_xyz):
         """24 accumulators of the queries whose (MIN-reduced) winner is in [lo, hi)."""
         ctx = self.ctx
@@ -358,6 +366,24 @@ class ICP:
 
     def __del__(self):
         self.close()
+
+
+def accumulate_slice(ctx, T_dev, q, keys, tgt, acc=None):
+    """Accumulators of the queries q (n x 3 fp32, original order) with their MIN-reduced keys
+    (global indices into tgt, the full target): the reduce-scatter form of the sharded loop."""
+    acc = torch.zeros(24, dtype=torch.float64, device=ctx.device) if acc is None else acc
+    n = q.shape[0]
+    assert keys.numel() >= n and keys.dtype == torch.int64
+    ctx.check(ctx.lib.pcp_icp_accumulate_slice(ctx.h, _ptr(T_dev), _ptr(q) if n else None,
+                                               q.stride(0) * q.element_size(), n, _ptr(keys), _ptr(tgt),
+                                               tgt.stride(0) * tgt.element_size(), _ptr(acc)))
+    return acc
+
+
+def slab_guard(ctx, T_dev, box, lo, hi, flag):
+    """Latch flag[0] = 1 when the owned queries' box leaves x in [lo, hi] under T_dev."""
+    ctx.check(ctx.lib.pcp_slab_guard(ctx.h, _ptr(T_dev), _lib.f64arr(np.asarray(box, dtype=np.float64).reshape(6)),
+                                     float(lo), float(hi), _ptr(flag)))
 
 
 def icp_solve(acc, do_scale=False):

@@ -66,6 +66,9 @@ def load():
     lib.ora_icp_solve.argtypes = [vp, C.c_int, vp]
     lib.ora_icp.restype = C.c_double
     lib.ora_icp.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_float, C.c_int, C.c_int, C.c_int]
+    lib.ora_icp_timed.restype = C.c_double
+    lib.ora_icp_timed.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_float, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, vp, vp]
     lib.ora_get_rot_icp.restype = C.c_float
     lib.ora_get_rot_icp.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.c_float,
                                     C.c_int, C.c_int, C.c_int]
@@ -252,6 +255,18 @@ def icp_solve(acc, do_scale=False):
     dT = np.zeros(16)
     rc = lib.ora_icp_solve(acc.ctypes.data, int(do_scale), dT.ctypes.data)
     return rc, dT.reshape(4, 4)
+
+
+def icp_timed(tgt, q, T0, rmax, iters, do_scale=False, nthreads=0):
+    """CPU-baseline ICP: returns (err, T, build_s, iter_s) with per-thread accumulators."""
+    lib = load()
+    tgt = np.ascontiguousarray(tgt, dtype=np.float32).reshape(-1, 3)
+    q = np.ascontiguousarray(q, dtype=np.float32).reshape(-1, 3)
+    T = np.ascontiguousarray(np.array(T0, dtype=np.float64).reshape(16))
+    bs, its = C.c_double(), C.c_double()
+    err = lib.ora_icp_timed(tgt.ctypes.data, len(tgt), q.ctypes.data, len(q), T.ctypes.data, float(rmax),
+                            int(iters), int(do_scale), int(nthreads), 1, C.byref(bs), C.byref(its))
+    return err, T.reshape(4, 4), bs.value, its.value
 
 
 def icp(tgt, q, T0, rmax, iters, do_scale=False, nthreads=0):

@@ -62,3 +62,29 @@ class OracleEngine:
         idx = np.where(mine, g - lo, -1).astype(np.int32)
         d2 = np.where(mine, (k >> 32).astype(np.uint32).view(np.float32), np.inf).astype(np.float32)
         return torch.from_numpy(ora.icp_accumulate(self.t, self.q, R, t, idx, d2))
+
+    # reduce-scatter form of the sharded loop and the slab guard (device pose = CPU tensor)
+    def keys_dev(self, T_dev, rmax, offset, out=None):
+        k = self.keys(T_dev.numpy().reshape(4, 4), rmax, offset)
+        if out is None:
+            return k
+        out[:len(k)] = k
+        return out
+
+    def accumulate_slice(self, T_dev, q, keys, tgt):
+        R, t = _rt(T_dev.numpy().reshape(4, 4))
+        q = np.ascontiguousarray(np.asarray(q), dtype=np.float32)
+        k = keys.numpy()[:len(q)]
+        ok = k != NO_KEY
+        # the winners as a dense target table in slice order (accumulate reads tgt[idx[i]])
+        idx = np.where(ok, np.arange(len(q)), -1).astype(np.int32)
+        win = np.ascontiguousarray(np.asarray(tgt, dtype=np.float32)[np.where(ok, k & 0xFFFFFFFF, 0)])
+        d2 = np.where(ok, (k >> 32).astype(np.uint32).view(np.float32), np.inf).astype(np.float32)
+        return torch.from_numpy(ora.icp_accumulate(win, q, R, t, idx, d2))
+
+    def slab_guard(self, T_dev, box, lo, hi, flag):
+        T = T_dev.numpy().reshape(4, 4)
+        xs = [T[0, 0] * x + T[0, 1] * y + T[0, 2] * z + T[0, 3]
+              for x in box[0:2] for y in box[2:4] for z in box[4:6]]
+        if not (min(xs) >= lo and max(xs) <= hi):
+            flag[0] = 1

@@ -47,6 +47,22 @@ def _worker(rank, world, port, mode, out):
         eng = OracleEngine(tgt[tm], q[qm])
         run = D.run_copartitioned if mode == "copartitioned" else D.run_copartitioned_dev
         err, T = run(eng, np.eye(4), 0.25, 8)
+    elif mode == "slab_dev":
+        # one registration split into x-slabs (the bench's strong-scaling layout) + halo guard
+        b = D.slab_bounds(q[:, 0], world)
+        halo = 1.0
+        qm, tm = D.slab_select(q[:, 0], tgt[:, 0], b, rank, halo)
+        mine = q[qm]
+        box = [mine[:, 0].min(), mine[:, 0].max(), mine[:, 1].min(), mine[:, 1].max(), mine[:, 2].min(),
+               mine[:, 2].max()]
+        eng = OracleEngine(tgt[tm], mine)
+        err, T, ok = D.run_slab_dev(eng, np.eye(4), 0.25, 8, guard=(box, b[rank] - halo + 0.25,
+                                                                    b[rank + 1] + halo - 0.25))
+        assert ok
+    elif mode == "target_sharded_dev":
+        lo, hi = D.shard_range(len(tgt), world, rank)
+        eng = OracleEngine(tgt[lo:hi], q)
+        err, T = D.run_target_sharded_dev(eng, np.eye(4), 0.25, 8, lo, torch.from_numpy(q), torch.from_numpy(tgt))
     else:
         lo, hi = D.shard_range(len(tgt), world, rank)
         eng = OracleEngine(tgt[lo:hi], q)
@@ -55,7 +71,8 @@ def _worker(rank, world, port, mode, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["copartitioned", "copartitioned_dev", "target_sharded"])
+@pytest.mark.parametrize("mode", ["copartitioned", "copartitioned_dev", "target_sharded", "target_sharded_dev",
+                                  "slab_dev"])
 def test_two_ranks_match_single_process(mode):
     import oracle_ctypes as ora
     tgt, q, T_true = _data()
@@ -77,3 +94,17 @@ def test_shard_range_covers():
             rs = [shard_range(n, w, r) for r in range(w)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+
+
+def test_slab_guard_latches():
+    """The slab guard flags a pose that moves the owned queries' box out of the halo."""
+    from oracle_engine import OracleEngine
+    eng = OracleEngine(np.zeros((1, 3), np.float32), np.zeros((1, 3), np.float32))
+    flag = torch.zeros(1, dtype=torch.int32)
+    T = np.eye(4)
+    box = [0.0, 10.0, -5.0, 5.0, 0.0, 2.0]
+    eng.slab_guard(torch.from_numpy(T.reshape(16).copy()), box, -1.0, 11.0, flag)
+    assert flag.item() == 0
+    T[0, 3] = 1.5
+    eng.slab_guard(torch.from_numpy(T.reshape(16).copy()), box, -1.0, 11.0, flag)
+    assert flag.item() == 1

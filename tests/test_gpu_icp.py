@@ -241,3 +241,51 @@ def test_target_sharded_keys_match_oracle(ctx):
     assert np.allclose(acc[:23], eacc[:23], rtol=1e-12, atol=1e-12 * np.abs(eacc[:23]).max())
     for e in engines:
         e.close()
+
+
+def test_target_sharded_dev_reduce_scatter_form(ctx):
+    """Device-resident target-sharded loop pieces (keys_dev + accumulate_slice): x-slab shards
+    (so most queries lie outside a shard's grid and take the octant pass's out-of-grid exit,
+    then the verify pass), MIN of the keys = the oracle's global correspondences bit-exact at
+    every pose of a sequence; the two query slices' accumulators sum to the oracle's."""
+    import torch
+    from pointcloudprocess_amd import distributed as D, ops, synth
+    tgt, q = _pair(150_000, 33, synth.rigid())
+    tgt = tgt[torch.argsort(tgt[:, 0])].contiguous()  # global index = x order: slabs
+    n, nq = tgt.shape[0], q.shape[0]
+    dq, dt = q.to(ctx.device), tgt.to(ctx.device)
+    shards = [D.shard_range(n, 2, r) for r in range(2)]
+    engines = [D.GpuEngine(ctx, dt[lo:hi], dq, cell_size=0.1) for lo, hi in shards]
+    T_dev, _ = engines[0].new_pose(np.eye(4))
+    ix = ora.F32Index(tgt.numpy())
+    for T in (np.eye(4), synth.rigid(0.1, 0.05, 0.0, (0.02, 0.01, 0.0)), synth.rigid(0.3, 0.1, -0.05, (0.1, 0.0, 0.02)),
+              synth.rigid(0.1, 0.05, 0.0, (0.02, 0.01, 0.0))):
+        T_dev.copy_(torch.from_numpy(np.ascontiguousarray(T.reshape(16))).to(ctx.device))
+        keys = torch.minimum(engines[0].keys_dev(T_dev, 0.25, shards[0][0]),
+                             engines[1].keys_dev(T_dev, 0.25, shards[1][0]))
+        k = keys.cpu().numpy()
+        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+        ei, ed = ix.correspond(q.numpy(), R, t, 0.25)
+        none = k == np.iinfo(np.int64).max
+        assert np.array_equal(none, ei < 0)
+        assert np.array_equal((k[~none] & 0xFFFFFFFF).astype(np.int32), ei[~none])
+        assert np.array_equal((k[~none] >> 32).astype(np.uint32).view(np.float32), ed[~none])
+        h = nq // 2
+        acc = (ops.accumulate_slice(ctx, T_dev, dq[:h], keys[:h], dt).cpu().numpy().copy() +
+               ops.accumulate_slice(ctx, T_dev, dq[h:], keys[h:], dt).cpu().numpy().copy())
+        eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
+        assert np.allclose(acc[:23], eacc[:23], rtol=1e-12, atol=1e-12 * np.abs(eacc[:23]).max())
+    for e in engines:
+        e.close()
+
+
+def test_slab_guard_device(ctx):
+    from pointcloudprocess_amd import ops
+    flag = torch.zeros(1, dtype=torch.int32, device=ctx.device)
+    T = np.eye(4)
+    box = [0.0, 10.0, -5.0, 5.0, 0.0, 2.0]
+    ops.slab_guard(ctx, torch.from_numpy(T.reshape(16).copy()).to(ctx.device), box, -1.0, 11.0, flag)
+    assert flag.item() == 0
+    T[0, 3] = 1.5
+    ops.slab_guard(ctx, torch.from_numpy(T.reshape(16).copy()).to(ctx.device), box, -1.0, 11.0, flag)
+    assert flag.item() == 1

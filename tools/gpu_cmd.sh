@@ -1,6 +1,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/fold3; mkdir -p $O
-timeout -k 10 200 python3 tools/fold_micro.py > $O/fold_micro.log 2>&1
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+O=gpurun_out/mg2; mkdir -p $O
+
+timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err
+PCP_BENCH_DEVICE=0 PCP_BENCH_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --steps 2 --no-cpu > $O/bench_g2.json 2> $O/bench_g2.err
 echo done
