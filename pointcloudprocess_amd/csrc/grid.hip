@@ -88,6 +88,39 @@ __global__ void k_minmax(const T* cxyz, int64_t n, double* part) {
         for (int a = 0; a < 6; a++) part[blockIdx.x * 6 + a] = s[a][0];
 }
 
+// one pass over the caller's cloud: bbox of the finite points + the number of non-finite ones
+// (the fp32 build skips the compaction when that number is 0)
+template <typename T>
+__global__ void k_bbox_count(const T* xyz, size_t stride, int64_t n, double* part, unsigned long long* bad) {
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    unsigned nb = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const T* p = pt_ptr(xyz, stride, i);
+        const double v[3] = {(double)p[0], (double)p[1], (double)p[2]};
+        if (!(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]))) { nb++; continue; }
+        for (int a = 0; a < 3; a++) {
+            mn[a] = fmin(mn[a], v[a]);
+            mx[a] = fmax(mx[a], v[a]);
+        }
+    }
+    __shared__ double s[6][kB];
+    for (int a = 0; a < 3; a++) { s[a][threadIdx.x] = mn[a]; s[3 + a][threadIdx.x] = mx[a]; }
+    __syncthreads();
+    for (int w = kB / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int a = 0; a < 3; a++) {
+                s[a][threadIdx.x] = fmin(s[a][threadIdx.x], s[a][threadIdx.x + w]);
+                s[3 + a][threadIdx.x] = fmax(s[3 + a][threadIdx.x], s[3 + a][threadIdx.x + w]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int a = 0; a < 6; a++) part[blockIdx.x * 6 + a] = s[a][0];
+    for (int o = 32; o > 0; o >>= 1) nb += __shfl_xor(nb, o, 64);
+    if ((threadIdx.x & 63) == 0 && nb) atomicAdd(bad, (unsigned long long)nb);
+}
+
 template <typename T>
 __device__ __forceinline__ void cell_of_point(const GridDesc& g, const T* p, int& cx, int& cy, int& cz) {
     cx = clampi(cell_i<T>(g, p[0], 0), 0, g.n[0] - 1);
@@ -95,12 +128,13 @@ __device__ __forceinline__ void cell_of_point(const GridDesc& g, const T* p, int
     cz = clampi(cell_i<T>(g, p[2], 2), 0, g.n[2] - 1);
 }
 
+// points stride_t values apart: the compacted array (3) or the caller's all-finite cloud
 template <typename T>
-__global__ void k_mark(GridDesc g, const T* cxyz, int64_t n, int32_t* brick) {
+__global__ void k_mark(GridDesc g, const T* cxyz, size_t stride_t, int64_t n, int32_t* brick) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         int cx, cy, cz;
-        cell_of_point<T>(g, cxyz + 3 * i, cx, cy, cz);
+        cell_of_point<T>(g, cxyz + stride_t * i, cx, cy, cz);
         brick[brick_of(g, cx, cy, cz)] = 1;
     }
 }
@@ -223,15 +257,16 @@ __global__ void k_far_sentinel(float4* pts, int64_t n) {
     pts[n] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(0x7fffffff));
 }
 
-__global__ void k_cell_keys_rec(GridDesc g, const float* cxyz, const int32_t* mapping, int64_t n, uint32_t* key,
-                                float4* rec, int32_t* mark) {
+// mapping == null: the points are the caller's cloud itself (all finite, stride_f floats apart)
+__global__ void k_cell_keys_rec(GridDesc g, const float* cxyz, size_t stride_f, const int32_t* mapping, int64_t n,
+                                uint32_t* key, float4* rec, int32_t* mark) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const float* p = cxyz + 3 * i;
+        const float* p = cxyz + stride_f * i;
         int cx, cy, cz;
         cell_of_point<float>(g, p, cx, cy, cz);
         key[i] = (uint32_t)cell_id(g, cx, cy, cz);
-        rec[i] = make_float4(p[0], p[1], p[2], __int_as_float(mapping[i]));
+        rec[i] = make_float4(p[0], p[1], p[2], __int_as_float(mapping ? mapping[i] : (int32_t)i));
         if (mark) mark[brick_of(g, cx, cy, cz)] = 1;
     }
 }
@@ -309,39 +344,74 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     ix->n_in = n_in;
     auto fail = [&](int rc) { pcp_index_destroy(ix); return rc; };
 
+    int rc;
+    T* cxyz = nullptr;
+    double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
+    // ---- fp32 (ICP target): bbox + non-finite count in one pass; an all-finite cloud is keyed
+    // straight from the caller's array (no compaction, identity mapping)
+    bool direct = false;
+    if (!is_f64 && !indices && n_in > 0 && stride % sizeof(T) == 0) {
+        const unsigned nbk = grid_for(n_in, kB, 1024);
+        double* part = nullptr;
+        unsigned long long* d_bad = nullptr;
+        if ((rc = dmalloc(ctx, &part, 6 * (size_t)nbk)) || (rc = dmalloc(ctx, &d_bad, 1))) {
+            dfree(ctx, part);
+            return fail(rc);
+        }
+        hipError_t e = hipMemsetAsync(d_bad, 0, sizeof(unsigned long long), st);
+        hipLaunchKernelGGL(k_bbox_count<T>, dim3(nbk), dim3(kB), 0, st, xyz, stride, n_in, part, d_bad);
+        std::vector<double> hp(6 * nbk);
+        unsigned long long bad = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(hp.data(), part, hp.size() * sizeof(double), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        dfree(ctx, part);
+        dfree(ctx, d_bad);
+        if (e != hipSuccess) return fail(hip_fail(ctx, e, "bbox", __FILE__, __LINE__));
+        if (bad == 0) {
+            direct = true;
+            for (int a = 0; a < 3; a++) { mn[a] = INFINITY; mx[a] = -INFINITY; }
+            for (unsigned b = 0; b < nbk; b++)
+                for (int a = 0; a < 3; a++) {
+                    mn[a] = std::fmin(mn[a], hp[6 * b + a]);
+                    mx[a] = std::fmax(mx[a], hp[6 * b + 3 + a]);
+                }
+            ix->n = n_in;
+            ix->identity = 1;
+        }
+    }
     // ---- compaction (convertCloudToArray)
     uint32_t* flag = nullptr;
     uint32_t* bits = nullptr;
-    T* cxyz = nullptr;
-    int rc;
     const int64_t nw = (n_in + 31) / 32;
-    if ((rc = dmalloc(ctx, &flag, n_in + 1)) || (rc = dmalloc(ctx, &bits, nw + 1))) {
-        dfree(ctx, flag); dfree(ctx, bits);
-        return fail(rc);
+    if (!direct) {
+        if ((rc = dmalloc(ctx, &flag, n_in + 1)) || (rc = dmalloc(ctx, &bits, nw + 1))) {
+            dfree(ctx, flag); dfree(ctx, bits);
+            return fail(rc);
+        }
+        uint32_t nvalid = 0;
+        if (n_in > 0) {
+            hipLaunchKernelGGL(k_valid<T>, dim3(grid_for(n_in, kB)), dim3(kB), 0, st, xyz, stride, n_in, indices, flag);
+            hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)((n_in + kB - 1) / kB)), dim3(kB), 0, st, flag, n_in, bits);
+            rc = scan_u32_inplace(ctx, flag, n_in, &nvalid);
+            if (rc) { dfree(ctx, flag); dfree(ctx, bits); return fail(rc); }
+        }
+        ix->n = nvalid;
+        ix->identity = (indices == nullptr && (int64_t)nvalid == n_in) ? 1 : 0;
+        if ((rc = dmalloc(ctx, &cxyz, 3 * (size_t)(nvalid + 1))) || (rc = dmalloc(ctx, &ix->mapping, nvalid + 1))) {
+            dfree(ctx, flag); dfree(ctx, bits); dfree(ctx, cxyz);
+            return fail(rc);
+        }
+        if (n_in > 0)
+            hipLaunchKernelGGL(k_compact<T>, dim3(grid_for(n_in, kB)), dim3(kB), 0, st, xyz, stride, n_in,
+                               indices, flag, bits, cxyz, ix->mapping);
+        dfree(ctx, flag);
+        dfree(ctx, bits);  // cached: reuse is stream-ordered on ctx's stream
     }
-    uint32_t nvalid = 0;
-    if (n_in > 0) {
-        hipLaunchKernelGGL(k_valid<T>, dim3(grid_for(n_in, kB)), dim3(kB), 0, st, xyz, stride, n_in, indices, flag);
-        hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)((n_in + kB - 1) / kB)), dim3(kB), 0, st, flag, n_in, bits);
-        rc = scan_u32_inplace(ctx, flag, n_in, &nvalid);
-        if (rc) { dfree(ctx, flag); dfree(ctx, bits); return fail(rc); }
-    }
-    ix->n = nvalid;
-    ix->identity = (indices == nullptr && (int64_t)nvalid == n_in) ? 1 : 0;
-    if ((rc = dmalloc(ctx, &cxyz, 3 * (size_t)(nvalid + 1))) || (rc = dmalloc(ctx, &ix->mapping, nvalid + 1))) {
-        dfree(ctx, flag); dfree(ctx, bits); dfree(ctx, cxyz);
-        return fail(rc);
-    }
-    if (n_in > 0)
-        hipLaunchKernelGGL(k_compact<T>, dim3(grid_for(n_in, kB)), dim3(kB), 0, st, xyz, stride, n_in,
-                           indices, flag, bits, cxyz, ix->mapping);
-    dfree(ctx, flag);
-    dfree(ctx, bits);  // cached: reuse is stream-ordered on ctx's stream
-    const int64_t n = nvalid;
+    const int64_t n = ix->n;
 
     // ---- bbox
-    double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
-    if (n > 0) {
+    if (n > 0 && !direct) {
         const unsigned nbk = grid_for(n, kB, 1024);
         double* part;
         if ((rc = dmalloc(ctx, &part, 6 * (size_t)nbk))) { dfree(ctx, cxyz); return fail(rc); }
@@ -404,7 +474,9 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         } else {
             if ((rc = dmalloc(ctx, &ix->brick, g.nbricks))) break;
             PCP_HIP(ctx, hipMemsetAsync(ix->brick, 0, (size_t)g.nbricks * sizeof(int32_t), st));
-            if (n > 0) hipLaunchKernelGGL(k_mark<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, ix->brick);
+            if (n > 0)  // the direct (uncompacted) fp32 path keys the caller's cloud in place
+                hipLaunchKernelGGL(k_mark<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, direct ? xyz : cxyz,
+                                   direct ? stride / sizeof(T) : (size_t)3, n, ix->brick);
             const int64_t nbw = (g.nbricks + 31) / 32;
             uint32_t* bbits;
             if ((rc = dmalloc(ctx, &bbits, nbw + 1))) break;
@@ -445,8 +517,12 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             } else {
                 // no brick marks: the fp32 index serves ICP only, whose dense-grid searches never
                 // read brick occupancy (its brick table stays all-zero = "occupied")
-                hipLaunchKernelGGL(k_cell_keys_rec, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const float*)cxyz,
-                                   (const int32_t*)ix->mapping, n, skey, rec0, nullptr);
+                if (direct)
+                    hipLaunchKernelGGL(k_cell_keys_rec, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const float*)xyz,
+                                       stride / sizeof(float), (const int32_t*)nullptr, n, skey, rec0, nullptr);
+                else
+                    hipLaunchKernelGGL(k_cell_keys_rec, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, (const float*)cxyz,
+                                       (size_t)3, (const int32_t*)ix->mapping, n, skey, rec0, nullptr);
                 PCP_HIP(ctx, rocprim::radix_sort_pairs<RecSortConfig>(nullptr, tmp_bytes, skey, key1, rec0, (float4*)ix->pts,
                                                        (size_t)n, 0u, bits, st));
                 if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))

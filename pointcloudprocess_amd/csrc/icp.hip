@@ -801,17 +801,52 @@ struct Top3K {
 
 // ---- search pass (the verify pass's list; every query at the first launch)
 // One query per lane, 64-query chunks grid-stride over the list.  Each query scans its whole
-// 2x2x2 "octant" block of cells (the four x-rows [floor(f - 1/2), +1]) keeping its 4 nearest.
+// 2x2x2 "octant" block of cells (the four x-rows [floor(f - 1/2), +1]) keeping its 3 nearest.
 // The octant holds every target within m = the query's distance to its faces (>= 1/2 cell,
-// less the margin).  The nearest is the exact 1-NN when d0 <= m^2 and d0 < d4 (every point
+// less the margin).  The nearest is the exact 1-NN when d0 <= m^2 and d0 < d3 (every point
 // tied with it is cached, and the cache order by index decides); "nothing within rmax" is
-// certified when rmax <= m.  The cache is refreshed either way (D = min(d4, m) bounds every
+// certified when rmax <= m.  The cache is refreshed either way (D = min(d3, m) bounds every
 // uncached point); unsettled queries go to the fallback list.
+//
+// LDS staging (dense chunks): the 64 queries of a chunk are spatial neighbours (brick-major
+// query order), so their octants overlap heavily.  When the union box of the chunk's octant
+// blocks spans at most kStageRows (y,z) rows and kStageCap targets, the wave copies those
+// rows once into LDS (coalesced: each row's x-range is one contiguous run of the cell-sorted
+// targets, tagged with its sorted position) and every lane scans its octant from LDS --
+// ~7x fewer global loads than one gather per candidate per lane.  Wider chunks (the sparse
+// search lists of later launches) scan straight from HBM.
+#ifndef PCP_OCT_LDS
+#define PCP_OCT_LDS 0
+#endif
+#ifndef PCP_STAGE_CAP
+#define PCP_STAGE_CAP 384
+#endif
+constexpr int kStageCap = PCP_STAGE_CAP;  // staged targets per wave (16 B each)
+constexpr int kStageRows = 16;            // staged (y,z) rows per wave
+constexpr int kStageW = 16;               // cell starts per staged row (box width + 1)
+static_assert(PCP_CACHE3 && !PCP_TOPK_PACKED, "the search pass keeps a 3-point cache");
+
+__device__ __forceinline__ int wave_min_int(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
 __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a, const int32_t* list,
                                                                           const uint32_t* list_n) {
     load_pose(a);
     constexpr int kW = kIcpBlock / 64;
     __shared__ double s_acc[kW][kAcc];
+#if PCP_OCT_LDS
+    __shared__ float4 s_pts[kW][kStageCap];
+    __shared__ uint32_t s_rbase[kW][kStageRows + 1];  // LDS offset of each staged row (+ total)
+    __shared__ uint32_t s_cst[kW][kStageRows * kStageW];  // the box's cell starts, kStageW per row
+#endif
     const GridDesc& g = a.g;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;  // global wave id = fallback segment
@@ -834,129 +869,180 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             in_ = list ? (int64_t)list[j + 64 * nwaves] : j + 64 * nwaves;
             qn = a.q[in_];
         }
-#if PCP_TOPK_PACKED
-        Top3K b;
-        float4 wp = make_float4(0.f, 0.f, 0.f, 0.f);  // the winner's coordinates
-        float wd = INFINITY;                           // and exact d2
-#elif PCP_CACHE3
         Top3 b;
-#else
-        Top4 b;
-#endif
-        float qx = 0.f, qy = 0.f, qz = 0.f;
-        bool settled = false, found = false;
-        uint32_t win = ~0u;
+        float wx = 0.f, wy = 0.f, wz = 0.f;  // the nearest's coordinates when it came from the stage
+        bool wlds = false;
+        float qx = 0.f, qy = 0.f, qz = 0.f, fx = 0.f, fy = 0.f, fz = 0.f, dout = 0.f;
+        int bx = 0, by = 0, bz = 0;
+        bool outside = true;
         if (valid) {
             xform(a, qraw, qx, qy, qz);
-            const float fx = cell_f<float>(g, qx, 0), fy = cell_f<float>(g, qy, 1), fz = cell_f<float>(g, qz, 2);
-            const int bx = (int)floorf(fx - a.rho), by = (int)floorf(fy - a.rho), bz = (int)floorf(fz - a.rho);
-            // this query's certified radius (cells): its distance to the nearest face of the
-            // 2x2x2 block (>= 0.5 cell), less the margin
-            const float m = fminf(fminf(fminf(fx - (float)bx, (float)(bx + 2) - fx),
-                                        fminf(fy - (float)by, (float)(by + 2) - fy)),
-                                  fminf(fz - (float)bz, (float)(bz + 2) - fz)) - a.mc;
+            fx = cell_f<float>(g, qx, 0), fy = cell_f<float>(g, qy, 1), fz = cell_f<float>(g, qz, 2);
+            bx = (int)floorf(fx - a.rho), by = (int)floorf(fy - a.rho), bz = (int)floorf(fz - a.rho);
             // a query farther than rmax from the grid's box (a target-sharded rank: the queries
             // of the other shards) is settled "no correspondence" without a scan, with D = that
             // distance (every target lies inside the box)
             const float ox = fmaxf(fmaxf(-fx, fx - (float)g.n[0]), 0.f);
             const float oy = fmaxf(fmaxf(-fy, fy - (float)g.n[1]), 0.f);
             const float oz = fmaxf(fmaxf(-fz, fz - (float)g.n[2]), 0.f);
-            const float dout = fmaxf(sqrtf(__fmaf_rn(oz, oz, __fmaf_rn(oy, oy, ox * ox))) - a.mc, 0.f) * g.hf;
-            const bool outside = dout * dout > a.r2 * 1.0001f;
-            // the 4 x-rows of the octant: all 8 row bounds at once
-            const int xa = max(bx, 0), xb = outside ? -1 : min(bx + 1, g.n[0] - 1);
-            uint32_t rs[4], rn[4];
+            dout = fmaxf(sqrtf(__fmaf_rn(oz, oz, __fmaf_rn(oy, oy, ox * ox))) - a.mc, 0.f) * g.hf;
+            outside = dout * dout > a.r2 * 1.0001f;
+        }
+        const bool scanq = !outside;
+        // the octant's 4 x-rows (y = by + (r & 1), z = bz + (r >> 1)), cells [xa, xb]
+        const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
+        uint32_t rs[4], rn[4];
+        bool staged = false;
+#if PCP_OCT_LDS
+        {
+            // union box of the chunk's octant blocks, clipped to the grid (wave-uniform)
+            const int x0 = max(wave_min_int(scanq ? bx : INT_MAX), 0);
+            const int x1 = min(wave_max_int(scanq ? bx + 1 : INT_MIN), g.n[0] - 1);
+            const int y0 = max(wave_min_int(scanq ? by : INT_MAX), 0);
+            const int y1 = min(wave_max_int(scanq ? by + 1 : INT_MIN), g.n[1] - 1);
+            const int z0 = max(wave_min_int(scanq ? bz : INT_MAX), 0);
+            const int z1 = min(wave_max_int(scanq ? bz + 1 : INT_MIN), g.n[2] - 1);
+            const int nxb = x1 - x0 + 1, nyb = y1 - y0 + 1, nrow = nyb * (z1 - z0 + 1);
+            if (x0 <= x1 && y0 <= y1 && z0 <= z1 && nrow <= kStageRows && nxb < kStageW) {
+                // the box's cell starts, row by row (cells x0 .. x1 + 1): one coalesced round trip
+                const int ncs = nrow * (nxb + 1);
+#pragma unroll
+                for (int k = 0; k < (kStageRows * kStageW + 63) / 64; k++) {
+                    const int e = lane + 64 * k;
+                    if (e < ncs) {
+                        const int r = e / (nxb + 1), cx = e - r * (nxb + 1);
+                        s_cst[wid][r * kStageW + cx] = g.cstart[dense_id(g, x0 + cx, y0 + r % nyb, z0 + r / nyb)];
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint32_t cnt = 0;
+                if (lane < nrow) cnt = s_cst[wid][lane * kStageW + nxb] - s_cst[wid][lane * kStageW];
+                uint32_t inc = cnt;  // inclusive scan over the rows
+#pragma unroll
+                for (int o = 1; o < kStageRows; o <<= 1) {
+                    const uint32_t t = __shfl_up(inc, o, 64);
+                    if (lane >= o) inc += t;
+                }
+                const uint32_t total = __shfl(inc, kStageRows - 1, 64);
+                if (total <= (uint32_t)kStageCap) {
+                    staged = true;
+                    if (lane < nrow) s_rbase[wid][lane] = inc - cnt;
+                    if (lane == 0) s_rbase[wid][nrow] = total;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // fill: entry e = lane + 64 k of the concatenated rows -> LDS, .w = its sorted
+                    // position.  Rows by a branch-free binary search of the row bases (LDS), the
+                    // loads of a batch in flight together (one memory round trip).
+                    constexpr int kPer = kStageCap / 64, kBatch = (kPer % 3 == 0) ? 3 : 2;
+                    static_assert(kPer % kBatch == 0, "fill batches");
+#pragma unroll
+                    for (int k0 = 0; k0 < kPer; k0 += kBatch) {
+                        uint32_t gp[kBatch];
+                        float4 fp[kBatch];
+#pragma unroll
+                        for (int k = 0; k < kBatch; k++) {
+                            const uint32_t e = lane + 64u * (k0 + k);
+                            int r = 0;
+#pragma unroll
+                            for (int st = kStageRows / 2; st > 0; st >>= 1)
+                                r = (r + st < nrow && s_rbase[wid][r + st] <= e) ? r + st : r;
+                            gp[k] = s_cst[wid][r * kStageW] + (e - s_rbase[wid][r]);
+                        }
+#pragma unroll
+                        for (int k = 0; k < kBatch; k++)
+                            if (lane + 64u * (k0 + k) < total) fp[k] = a.tp[gp[k]];
+#pragma unroll
+                        for (int k = 0; k < kBatch; k++)
+                            if (lane + 64u * (k0 + k) < total)
+                                s_pts[wid][lane + 64 * (k0 + k)] =
+                                    make_float4(fp[k].x, fp[k].y, fp[k].z, __uint_as_float(gp[k]));
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // this lane's rows -> LDS ranges (from the staged cell starts)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int y = by + (r & 1), z = bz + (r >> 1);
+                        const bool in = scanq && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
+                        const int row = in ? (z - z0) * nyb + (y - y0) : 0;
+                        const uint32_t c0 = s_cst[wid][row * kStageW], base = s_rbase[wid][row];
+                        const uint32_t ca = s_cst[wid][row * kStageW + (xa - x0)];
+                        const uint32_t cb = s_cst[wid][row * kStageW + (xb - x0) + 1];
+                        rs[r] = in ? base + (ca - c0) : 0u;
+                        rn[r] = in ? cb - ca : 0u;
+                    }
+                    if (!(a.dbg & kDbgNoScan)) b.scan4(&s_pts[wid][0], rs, rn, qx, qy, qz);
+                    // the winner's coordinates straight from the stage; LDS slots -> sorted positions
+                    if (b.p0 != ~0u) {
+                        const float4 w = s_pts[wid][b.p0];
+                        wx = w.x; wy = w.y; wz = w.z;
+                        wlds = true;
+                    }
+                    b.p0 = b.p0 != ~0u ? __float_as_uint(s_pts[wid][b.p0].w) : ~0u;
+                    b.p1 = b.p1 != ~0u ? __float_as_uint(s_pts[wid][b.p1].w) : ~0u;
+                    b.p2 = b.p2 != ~0u ? __float_as_uint(s_pts[wid][b.p2].w) : ~0u;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();  // the next chunk overwrites the stage
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+#endif
+        if (!staged) {  // global path: the 4 rows' sorted ranges straight from the cell table
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int y = by + (r & 1), z = bz + (r >> 1);
-                const bool in = xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
+                const bool in = scanq && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
                 const int64_t cc = in ? dense_id(g, xa, y, z) : 0;
                 rs[r] = in ? g.cstart[cc] : 0u;
                 rn[r] = in ? g.cstart[cc + (xb - xa + 1)] : 0u;
             }
 #pragma unroll
             for (int r = 0; r < 4; r++) rn[r] -= rs[r];
-#if PCP_TOPK_PACKED
-            // a list too long for the key's index byte is left to the fallback pass (no message)
-            const bool big = rn[0] + rn[1] + rn[2] + rn[3] > kMaxOctList;
-            if (big) rn[0] = rn[1] = rn[2] = rn[3] = 0u;
-#endif
-            if (!(a.dbg & kDbgNoScan)) b.scan4(a.tp, rs, rn, qx, qy, qz);
-            if (a.dbg & kDbgCount) {
-                atomicAdd(a.dbgcnt, (unsigned long long)(rn[0] + rn[1] + rn[2] + rn[3]));
-                atomicAdd(a.dbgcnt + 2, 1ull);
-            }
+        }
+        if (!staged && scanq && !(a.dbg & kDbgNoScan)) b.scan4(a.tp, rs, rn, qx, qy, qz);
+        if (a.dbg & kDbgCount) {
+            atomicAdd(a.dbgcnt, (unsigned long long)(rn[0] + rn[1] + rn[2] + rn[3]));
+            atomicAdd(a.dbgcnt + 2, 1ull);
+            if (staged) atomicAdd(a.dbgcnt + 3, 1ull);
+        }
+        bool settled = false, found = false;
+        uint32_t win = ~0u;
+        if (valid) {
+            // this query's certified radius (cells): its distance to the nearest face of the
+            // 2x2x2 block (>= 0.5 cell), less the margin
+            const float m = fminf(fminf(fminf(fx - (float)bx, (float)(bx + 2) - fx),
+                                        fminf(fy - (float)by, (float)(by + 2) - fy)),
+                                  fminf(fz - (float)bz, (float)(bz + 2) - fz)) - a.mc;
             const float rr = m * g.hf;
             const float cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
-#if PCP_TOPK_PACKED
-            // the kept points' positions (list index -> row position) and exact (d2, index) winner
-            const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2];
-            const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
-            const uint32_t k0 = b.t0, k1 = b.t1, k2 = b.t2;
-            const uint32_t ps0 = k0 == kKeyMax ? ~0u : cat_addr(k0 & 0xffu, c1, c2, c3, o0, o1, o2, o3);
-            const uint32_t ps1 = k1 == kKeyMax ? ~0u : cat_addr(k1 & 0xffu, c1, c2, c3, o0, o1, o2, o3);
-            const uint32_t ps2 = k2 == kKeyMax ? ~0u : cat_addr(k2 & 0xffu, c1, c2, c3, o0, o1, o2, o3);
-            int wj = 0x7fffffff;
-            auto take = [&](const float4 P, uint32_t ps) {
-                const float e = icp_d2(qx, qy, qz, P);
-                const int id = __float_as_int(P.w);
-                const bool t = e < wd || (e == wd && id < wj);
-                wd = t ? e : wd;
-                wj = t ? id : wj;
-                wp = t ? P : wp;
-                win = t ? ps : win;
-            };
-            // the smallest key's point is the winner unless another kept key lies in the same or
-            // the next truncation bucket (then its exact d2 decides): one gather, rarely three
-            take(ld16(a.tp, min(ps0, a.ntp)), ps0);  // empty: the far sentinel
-            if ((k1 >> 8) - (k0 >> 8) <= 1u) take(ld16(a.tp, min(ps1, a.ntp)), ps1);
-            if ((k2 >> 8) - (k0 >> 8) <= 1u) take(ld16(a.tp, min(ps2, a.ntp)), ps2);
-            const float lbu = b.uncached_lb();  // every other scanned point: d2 >= lbu
-            found = wd <= a.r2;
-            settled = !big && (found ? (wd < lbu && wd <= cert2) : (lbu > a.r2 && a.r2 <= cert2));
-            settled = settled || (a.dbg & kDbgNoFallback);
-            // settled: D bounds every uncached point for the verify pass.  Unsettled: the
-            // fallback pass (which overwrites the cache) gets lbu as its message.
-            const float D = settled ? fminf(sqrtf(lbu), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : (big ? 0.f : lbu);
-            a.cand[i] = make_uint4(ps0, ps1, ps2, pack_dlb(D, a.launch));
-#else
             found = b.d0 <= a.r2;
-#if PCP_CACHE3
             const float dnext = b.d3;  // the first uncached d2
-#else
-            const float dnext = b.d4;
-#endif
-            settled = (found ? (b.d0 < dnext && b.d0 <= cert2) : a.r2 <= cert2) || outside || (a.dbg & kDbgNoFallback);
+            settled = (found ? (b.d0 < dnext && b.d0 <= cert2) : a.r2 <= cert2) || outside ||
+                      (a.dbg & kDbgNoFallback);
             // the winner among the cached ties by target index (rare: only when d1 == d0)
             win = b.p0;
             if (found && b.d1 == b.d0) {
                 int wj = __float_as_int(a.tp[b.p0].w);
-#if PCP_CACHE3
                 const uint32_t ps[2] = {b.p1, b.p2};
                 const float ds[2] = {b.d1, b.d2};
-#else
-                const uint32_t ps[3] = {b.p1, b.p2, b.p3};
-                const float ds[3] = {b.d1, b.d2, b.d3};
-#endif
 #pragma unroll
-                for (int s2 = 0; s2 < kCache - 1; s2++) {
+                for (int s2 = 0; s2 < 2; s2++) {
                     if (ds[s2] != b.d0) break;
                     const int id = __float_as_int(a.tp[ps[s2]].w);
                     if (id < wj) { wj = id; win = ps[s2]; }
                 }
             }
-            // the cache: the 4 nearest; D bounds every uncached point
-            // settled: D bounds every uncached point for the verify pass.  Unsettled: the fallback
-            // pass (which overwrites the cache) gets the octant's first uncached d2 instead.
+            // the cache: the 3 nearest; settled: D bounds every uncached point for the verify
+            // pass.  Unsettled: the fallback pass (which overwrites the cache) gets the
+            // octant's first uncached d2 instead.
             const float D = outside ? dout * 0.9999f
                                     : (settled ? fminf(sqrtf(dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : dnext);
-#if PCP_CACHE3
             a.cand[i] = make_uint4(b.p0, b.p1, b.p2, pack_dlb(D, a.launch));
-#else
-            a.cand[i] = make_uint4(b.p0, b.p1, b.p2, b.p3);
-            a.dlb[i] = pack_dlb(D, a.launch);
-#endif
-#endif  // PCP_TOPK_PACKED
         }
         // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
         const bool fb = valid && !settled;
@@ -968,12 +1054,8 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         }
         fbn += (uint32_t)__popcll(fbm);
         const bool acc_ok = valid && settled && found && !(a.dbg & kDbgNoAccum);
-#if PCP_TOPK_PACKED
-        const Best w{wd, 0, win, wp.x, wp.y, wp.z};
-#else
-        Best w{b.d0, 0, win, 0.f, 0.f, 0.f};
-        if (acc_ok) w.fetch(a.tp);
-#endif
+        Best w{b.d0, 0, win, wx, wy, wz};
+        if (acc_ok && !(wlds && win == b.p0)) w.fetch(a.tp);
         chunk_accumulate(acc_ok, qx, qy, qz, w, s_acc[wid], lane);
     }
     if (lane == 0) {  // every wave of the grid writes its count: no zeroing pass needed
