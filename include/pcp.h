@@ -51,6 +51,16 @@ typedef struct pcp_plane {
     float distance;   /* -(n . mean), calculate_feature.cpp:197 */
 } pcp_plane;
 
+/* LAS_POINT_PROPERTY (data_struct.h:161-172): the per-point record of
+ * calculate_plan_parameter_rpca; 48 bytes, the reference's layout. */
+typedef struct pcp_point_property {
+    float normal_x, normal_y, normal_z;
+    double distance;
+    double curvature;
+    int32_t point_id, segment_id;
+    float dis_from_point_plane;
+} pcp_point_property;
+
 /* ----------------------------------------------------------------------- context */
 typedef struct pcp_ctx pcp_ctx;     /* device, stream, scratch arena, last error */
 typedef struct pcp_index pcp_index; /* device-resident uniform-grid index over a cloud */
@@ -169,6 +179,18 @@ int pcp_remove_duplicate(pcp_ctx* ctx, const void* in_aos48_dev, int64_t n, int 
  * points dropped as non-finite get {0,0,0,1}); sign: largest-|.| component positive. */
 int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* index, int k, pcp_plane* out_dev,
                     int64_t n_out);
+
+/* F3: CalculateFeature::calculate_plan_parameter_rpca(cloud, radius (unused), Pr, epi)
+ * (calculate_feature.cpp:208-368; the pipeline's normals entry, static.cpp:17) over the
+ * caller's kNN rows knn_idx_dev (n x k int32, k <= 20, ascending d2, -1 padded: pcp_knn of
+ * the cloud's own points with k = 20).  Deterministic contract (the reference seeds rand()
+ * with time(NULL)): the 3 neighbours of iteration i of point j are
+ * splitmix64(seed, j, i, slot) % N; sorts are stable; min_value ties keep the earlier
+ * iteration.  segment_id and dis_from_point_plane are written 0 (the reference leaves them
+ * uninitialised).  Normal sign: largest-|.| component positive (OpenCV's is unpinned). */
+int pcp_normals_rpca(pcp_ctx* ctx, const double* xyz_dev, size_t stride_bytes, int64_t n,
+                     const int32_t* knn_idx_dev, int k, float pr, float epi, uint64_t seed,
+                     pcp_point_property* out_dev);
 
 /* One plane per CSR segment (calculate_plan_parameter_h_points, calculate_feature.cpp:
  * 119-206, per segment; with radiusSearch rows as segments this is the declared-only

@@ -643,27 +643,33 @@ public:
             tree.radiusSearchBatch(cloud->points, radius, off, idx, d2);
         });
     }
-    // F3 (:208-368) is randomised (srand(time), rand() under OMP); this build returns the
-    // deterministic F1 over the same kNN(20) neighbourhoods ("next" in §8(f)).
-    std::shared_ptr<LAS_POINT_PROPERTY> calculate_plan_parameter_rpca(CloudPtr cloud, double /*radius*/, float /*pr*/,
-                                                                       float /*epi*/) {
-        return per_point(cloud, [&](KdTreeFLANN<CloudItem>& tree, std::vector<int64_t>& off, std::vector<int>& idx) {
-            std::vector<double> d2;
-            const int k = 20;  // calculate_feature.cpp:233
-            tree.nearestKSearchBatch(cloud->points, k, idx, d2);
-            off.resize(cloud->points.size() + 1);
-            std::vector<int> kept;
-            kept.reserve(idx.size());
-            off[0] = 0;
-            for (size_t i = 0; i < cloud->points.size(); i++) {
-                int got = 0;
-                for (int r = 0; r < k; r++)
-                    if (idx[i * k + r] >= 0) { kept.push_back(idx[i * k + r]); got++; }
-                if (got <= 3) kept.resize(kept.size() - got);  // N > 3 guard (:237, 353-361)
-                off[i + 1] = (int64_t)kept.size();
-            }
-            idx.swap(kept);
-        });
+    // F3 (:208-368): robust RPCA normals over each point's kNN(20) on the GPU
+    // (pcp_normals_rpca).  Deterministic: the reference's rand() draws (srand(time) :210, :249)
+    // are a counter-based hash of (seed, point, iteration, slot); `seed` is this build's
+    // addition.  radius is unused, as in the reference.
+    std::shared_ptr<LAS_POINT_PROPERTY> calculate_plan_parameter_rpca(CloudPtr cloud, double /*radius*/, float pr,
+                                                                       float epi, uint64_t seed = 0) {
+        static_assert(sizeof(LAS_POINT_PROPERTY) == sizeof(pcp_point_property), "LAS_POINT_PROPERTY layout");
+        const size_t n = cloud ? cloud->points.size() : 0;
+        std::shared_ptr<LAS_POINT_PROPERTY> res(new LAS_POINT_PROPERTY[n ? n : 1],
+                                                std::default_delete<LAS_POINT_PROPERTY[]>());
+        if (!n) return res;
+        KdTreeFLANN<CloudItem> tree;
+        tree.setInputCloud(cloud);
+        const int k = 20;  // calculate_feature.cpp:233
+        std::vector<int> idx;
+        std::vector<double> d2;
+        tree.nearestKSearchBatch(cloud->points, k, idx, d2);
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        detail::DevBuf didx, dout;
+        didx.upload(idx.data(), idx.size() * sizeof(int));
+        dout.reserve(n * sizeof(pcp_point_property));
+        detail::check(pcp_normals_rpca(c, tree.device_cloud(), sizeof(CloudItem), (int64_t)n,
+                                       (const int32_t*)didx.ptr(), k, pr, epi, seed, (pcp_point_property*)dout.ptr()),
+                      c, "pcp_normals_rpca");
+        dout.download(res.get(), n * sizeof(LAS_POINT_PROPERTY));
+        return res;
     }
 
 private:

@@ -596,6 +596,126 @@ void ora_normals_knn(const ora_kdtree* t, const double* xyz, size_t stride, int 
     }
 }
 
+/* ---- F3: calculate_plan_parameter_rpca (calculate_feature.cpp:208-368), deterministic */
+
+/* SplitMix64 finaliser of (seed, point, iteration, slot): the build's counter-based stand-in
+ * for rand() (:249), identical on the GPU (knn.hip k_rpca) */
+uint32_t ora_rpca_draw(uint64_t seed, uint32_t j, uint32_t it, uint32_t slot) {
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (((uint64_t)j << 32) | ((uint64_t)it << 2) | slot) + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z >> 32);
+}
+
+/* TreeExtration::compute_distance_from_point_to_plane (extraction_tree.cpp:47-64): float
+ * coordinates and coefficients, float products, double sums, result float */
+static float rpca_plane_dist(const double* p, float a, float b, float c, float d) {
+    const float x1 = (float)p[0], y1 = (float)p[1], z1 = (float)p[2];
+    const float aa = a * a, bb = b * b, cc = c * c;
+    const double g = (double)sqrtf((aa + bb) + cc);
+    const double f1 = (double)(a * x1), f2 = (double)(b * y1), f3 = (double)(c * z1), f4 = (double)d;
+    const double f = fabs(((f1 + f2) + f3) + f4);
+    return (float)(f / g);
+}
+
+/* compute_iteration_number (calculate_feature.cpp:28-33): float log10 of (1 - Pr), double
+ * pow and quotient, truncated */
+static int rpca_iterations(float pr, float epi) {
+    const double num = (double)log10f(1.0f - pr);
+    const double den = log10(1.0 - pow((double)(1.0f - epi), 3));
+    return (int)(num / den);
+}
+
+/* the k-th smallest of v[0..n) (value only; ties do not change it) */
+static float kth_value(const float* v, int n, int k) {
+    for (int i = 0; i < n; i++) {
+        int less = 0, le = 0;
+        for (int m = 0; m < n; m++) { less += v[m] < v[i]; le += v[m] <= v[i]; }
+        if (less <= k && k < le) return v[i];
+    }
+    return v[0];
+}
+
+void ora_rpca(const double* xyz, size_t stride, int n, const int* knn_idx, int k, float pr, float epi,
+              uint64_t seed, ora_point_property* out, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    const int iters = rpca_iterations(pr, epi);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int j = 0; j < n; j++) {
+        ora_point_property* o = &out[j];
+        memset(o, 0, sizeof(*o));
+        o->point_id = j;
+        o->curvature = 1.0;  /* N <= 3 (:353-361) and no-inlier (:345-351) outcome */
+        const int* row = knn_idx + (size_t)j * k;
+        int N = 0;
+        while (N < k && row[N] >= 0) N++;
+        if (N <= 3) continue;
+        const int h_free = (int)(2.0 / 3 * N);  /* :238-239 */
+        double P[64][3];
+        float F[64][3];
+        for (int m = 0; m < N; m++)
+            for (int a = 0; a < 3; a++) {
+                P[m][a] = xyz[(size_t)row[m] * stride + a];
+                F[m][a] = (float)P[m][a];  /* LAS_POINT_PROPERTY_sim coordinates are float */
+            }
+        ora_plane best = {0, 0, 0, 0, 0, 0};
+        int have = 0;
+        for (int it = 0; it < iters; it++) {  /* :244-282 */
+            int num[3];
+            for (int s = 0; s < 3; s++) num[s] = (int)(ora_rpca_draw(seed, (uint32_t)j, (uint32_t)it, (uint32_t)s) % (uint32_t)N);
+            if (num[0] == num[1] || num[0] == num[2] || num[1] == num[2]) continue;
+            double tri[9];
+            for (int s = 0; s < 3; s++)
+                for (int a = 0; a < 3; a++) tri[3 * s + a] = P[num[s]][a];
+            ora_plane p3;
+            ora_plane_h_points(tri, 3, &p3);  /* calculate_plan_parameter_3points (:35-117) */
+            float dist[64];
+            int ord[64];
+            for (int m = 0; m < N; m++) {
+                dist[m] = rpca_plane_dist(P[m], p3.normal_x, p3.normal_y, p3.normal_z, p3.distance);
+                ord[m] = m;
+            }
+            for (int a = 1; a < N; a++) {  /* stable sort by distance (:269) */
+                const int t = ord[a];
+                int b = a;
+                while (b > 0 && dist[ord[b - 1]] > dist[t]) { ord[b] = ord[b - 1]; b--; }
+                ord[b] = t;
+            }
+            double hp[64 * 3];
+            for (int m = 0; m < h_free; m++)
+                for (int a = 0; a < 3; a++) hp[3 * m + a] = (double)F[ord[m]][a];
+            ora_plane ph;
+            ora_plane_h_points(hp, h_free, &ph);  /* :271-280 */
+            if (!have || ph.min_value < best.min_value) { best = ph; have = 1; }  /* min over planes (:283-286) */
+        }
+        if (!have) continue;  /* every draw repeated an index: planes[0] is undefined in the reference */
+        float d[64], ds[64], tm[64];
+        for (int m = 0; m < N; m++)
+            d[m] = rpca_plane_dist(P[m], best.normal_x, best.normal_y, best.normal_z, best.distance);
+        memcpy(ds, d, sizeof(float) * N);
+        const float med = kth_value(ds, N, N / 2);  /* :300-302 */
+        for (int m = 0; m < N; m++) tm[m] = fabsf(d[m] - med);
+        const float mad = (float)(1.4826 * (double)kth_value(tm, N, N / 2));  /* :305-312 */
+        double in[64 * 3];
+        int cnt = 0;
+        for (int m = 0; m < N; m++) {  /* :313-334, neighbour order */
+            if (mad != 0.0f && !((double)(fabsf(d[m] - med) / mad) < 2.5)) continue;
+            for (int a = 0; a < 3; a++) in[3 * cnt + a] = P[m][a];
+            cnt++;
+        }
+        if (cnt > 3) {  /* :337-345 */
+            ora_plane f;
+            ora_plane_h_points(in, cnt, &f);
+            o->normal_x = f.normal_x; o->normal_y = f.normal_y; o->normal_z = f.normal_z;
+            o->distance = (double)f.distance;
+            o->curvature = (double)f.curvature;
+        }
+    }
+}
+
 /* =============================================================== I: ICP ============= */
 typedef struct fnode { int lo, hi, dim; float split; int left, right; } fnode;
 struct ora_f32index {

@@ -116,6 +116,24 @@ void ora_plane_h_points(const double* xyz, int h, ora_plane* out);
 void ora_normals_knn(const ora_kdtree* t, const double* xyz, size_t stride_doubles, int n,
                      int k, ora_plane* out, int nthreads);
 
+/* LAS_POINT_PROPERTY (data_struct.h:161-172), 48 bytes. */
+typedef struct ora_point_property {
+    float normal_x, normal_y, normal_z;
+    double distance;
+    double curvature;
+    int point_id, segment_id;
+    float dis_from_point_plane;
+} ora_point_property;
+
+/* F3 calculate_plan_parameter_rpca (calculate_feature.cpp:208-368), made deterministic: the
+ * 3 random neighbours of iteration i of point j are hash(seed, j, i, slot) % N (the reference
+ * draws rand() % N after srand(time), under OpenMP), sorts are stable (the reference's
+ * std::sort is not), planes tied on min_value keep the earlier iteration.  knn_idx: n rows of
+ * k neighbour indices (kNN(20) of each point in ascending d2, -1 padded), as pcp_knn writes. */
+uint32_t ora_rpca_draw(uint64_t seed, uint32_t j, uint32_t it, uint32_t slot);
+void ora_rpca(const double* xyz, size_t stride_doubles, int n, const int* knn_idx, int k, float pr,
+              float epi, uint64_t seed, ora_point_property* out, int nthreads);
+
 /* 3x3 symmetric eigen (cyclic Jacobi, double). Eigenvalues descending, eigenvectors as
  * rows of E (the cvEigenVV convention used at calculate_feature.cpp:165). */
 void ora_eigen_sym3(const double A[9], double evals[3], double E[9]);

@@ -256,6 +256,23 @@ def normals_knn(index, k):
     return out[:n_out]
 
 
+POINT_PROPERTY = np.dtype([("normal_x", "<f4"), ("normal_y", "<f4"), ("normal_z", "<f4"), ("pad", "<u4"),
+                           ("distance", "<f8"), ("curvature", "<f8"), ("point_id", "<i4"),
+                           ("segment_id", "<i4"), ("dis_from_point_plane", "<f4"), ("pad2", "<u4")])
+
+
+def normals_rpca(ctx, xyz, knn_idx, pr=0.99, epi=0.5, seed=0):
+    """F3 robust normals (calculate_plan_parameter_rpca) from the cloud's kNN(20) rows;
+    returns a (n, 48) uint8 device tensor of LAS_POINT_PROPERTY records."""
+    n = xyz.shape[0]
+    k = knn_idx.shape[1]
+    out = torch.empty((max(n, 1), 48), dtype=torch.uint8, device=ctx.device)
+    ctx.check(ctx.lib.pcp_normals_rpca(ctx.h, _ptr(xyz), xyz.stride(0) * xyz.element_size(), n,
+                                       _ptr(knn_idx.contiguous()), int(k), float(pr), float(epi),
+                                       int(seed), _ptr(out)))
+    return out[:n]
+
+
 class ICP:
     """Device-resident ICP of a query set against an fp32 grid index (the target)."""
 

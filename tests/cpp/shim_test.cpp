@@ -198,6 +198,30 @@ static void test_features_and_icp() {
           "h_points plane");
     std::shared_ptr<LAS_POINT_PROPERTY> props = cf.calculate_plan_parameter(cloud, 0.3);
     CHECK(std::fabs(std::fabs(props.get()[0].normal_z) - 0.995) < 0.01, "radius normal %g", props.get()[0].normal_z);
+    // F3 calculate_plan_parameter_rpca (static.cpp:17 arguments Pr 0.99, epi 0.5): every field
+    // equal to the oracle's restatement over the oracle's own kNN(20)
+    {
+        CloudPtr small(new Cloud);
+        small->points.assign(cloud->points.begin(), cloud->points.begin() + 4000);
+        std::shared_ptr<LAS_POINT_PROPERTY> rp = cf.calculate_plan_parameter_rpca(small, 0.15, 0.99f, 0.5f);
+        std::vector<double> sx;
+        for (auto& p : small->points) { sx.push_back(p.x); sx.push_back(p.y); sx.push_back(p.z); }
+        ora_kdtree* t = ora_kdtree_build(sx.data(), 3, (int)small->size(), NULL, 0);
+        std::vector<int> ki((size_t)small->size() * 20);
+        std::vector<double> kd(ki.size());
+        ora_knn_batch(t, sx.data(), 3, (int)small->size(), 20, ki.data(), kd.data(), 0);
+        std::vector<ora_point_property> ep(small->size());
+        ora_rpca(sx.data(), 3, (int)small->size(), ki.data(), 20, 0.99f, 0.5f, 0, ep.data(), 0);
+        ora_kdtree_free(t);
+        int bad = 0;
+        for (size_t i = 0; i < small->size(); i++) {
+            const LAS_POINT_PROPERTY& g = rp.get()[i];
+            const ora_point_property& e = ep[i];
+            bad += !(g.normal_x == e.normal_x && g.normal_y == e.normal_y && g.normal_z == e.normal_z &&
+                     g.Distance == e.distance && g.curvature == e.curvature && g.PointID == e.point_id);
+        }
+        CHECK(bad == 0, "rpca records differing from the oracle: %d", bad);
+    }
     // get_rot_icp: recover a small motion (err > 0, pose within 1e-4)
     CloudPtr src = random_cloud(60000, 31, 8.0, 100.0);
     for (auto& p : src->points) p.z = 0.2 * std::sin(p.x) + ((p.y > 100.0) ? 0.0 : 0.5 * (p.x - 100.0));

@@ -48,6 +48,9 @@ def load():
     lib.ora_getminmax3d.argtypes = [vp, C.c_int, C.c_int, vp, vp]
     lib.ora_centroid.argtypes = [vp, C.c_int, C.c_int, vp]
     lib.ora_centroid.restype = C.c_uint
+    lib.ora_rpca.argtypes = [vp, C.c_size_t, C.c_int, vp, C.c_int, C.c_float, C.c_float, C.c_uint64, vp, C.c_int]
+    lib.ora_rpca_draw.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+    lib.ora_rpca_draw.restype = C.c_uint32
     lib.ora_centroid_concat.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp]
     lib.ora_centroid_concat.restype = C.c_uint
     lib.ora_transform.argtypes = [vp, vp, C.c_int, C.c_int, vp]
@@ -173,6 +176,22 @@ def centroid_concat(a, b, is_dense=True):
     a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
     lib.ora_centroid_concat(a.ctypes.data, len(a), b.ctypes.data, len(b), int(is_dense), c.ctypes.data)
     return c
+
+
+POINT_PROPERTY = np.dtype([("normal_x", "<f4"), ("normal_y", "<f4"), ("normal_z", "<f4"), ("pad", "<u4"),
+                           ("distance", "<f8"), ("curvature", "<f8"), ("point_id", "<i4"),
+                           ("segment_id", "<i4"), ("dis_from_point_plane", "<f4"), ("pad2", "<u4")])
+
+
+def rpca(xyz, knn_idx, pr=0.99, epi=0.5, seed=0, nthreads=0):
+    """F3 calculate_plan_parameter_rpca restated (ora_rpca) from kNN rows (n, k)."""
+    lib = load()
+    xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 3)
+    knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)
+    out = np.zeros(len(xyz), dtype=POINT_PROPERTY)
+    lib.ora_rpca(xyz.ctypes.data, 3, len(xyz), knn_idx.ctypes.data, knn_idx.shape[1], float(pr), float(epi),
+                 int(seed), out.ctypes.data, nthreads)
+    return out
 
 
 def minmax(cloud, is_dense=True):

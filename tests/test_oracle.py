@@ -220,3 +220,31 @@ def test_near_face_cloud_needs_the_sequential_fold():
     e = ora.remove_duplicate(c, 0.04)
     e2 = ora.remove_duplicate_c(c, 0.04, blocked)
     assert len(e) != len(e2) or e.tobytes() != e2.tobytes()
+
+
+def test_rpca_oracle_robust_and_deterministic():
+    """F3 restated (ora_rpca, calculate_feature.cpp:208-368): on a noisy plane with 10 %
+    outliers the robust normal stays on the plane's normal where the plain PCA (F1) tilts,
+    the draws are a pure function of (seed, point, iteration, slot), and N <= 3 rows give
+    {0, 0, 0, curvature 1} (:353-361)."""
+    rng = np.random.default_rng(5)
+    n = 3000
+    xyz = np.c_[rng.uniform(-1, 1, (n, 2)), rng.normal(0, 1e-3, n)]
+    out_i = rng.choice(n, n // 10, replace=False)
+    xyz[out_i, 2] += rng.uniform(0.05, 0.2, len(out_i))
+    _, idx = cKDTree(xyz).query(xyz, k=20)
+    idx = idx.astype(np.int32)
+    a = ora.rpca(xyz, idx, seed=7)
+    b = ora.rpca(xyz, idx, seed=7)
+    assert a.tobytes() == b.tobytes()
+    inl = np.setdiff1d(np.arange(n), out_i)
+    nz_r = np.abs(a["normal_z"][inl])
+    f1 = ora.normals_knn(xyz, 20)
+    nz_p = np.abs(f1["normal_z"][inl])
+    assert np.median(nz_r) > 0.999 and nz_r.mean() > nz_p.mean()
+    assert (a["point_id"] == np.arange(n)).all()
+    short = idx.copy()
+    short[:5, 3:] = -1
+    c = ora.rpca(xyz, short, seed=7)
+    assert (c["normal_x"][:5] == 0).all() and (c["curvature"][:5] == 1.0).all()
+    assert ora.load().ora_rpca_draw(1, 2, 3, 0) != ora.load().ora_rpca_draw(1, 2, 3, 1)
