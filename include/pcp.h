@@ -108,6 +108,25 @@ const void* pcp_index_sorted_points(const pcp_index* index);
 int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_stride_bytes,
             int64_t nq, int k, int32_t* out_idx_dev, double* out_d2_dev);
 
+/* C5 (BASELINE configs[4]): fp16 cell-relative index + radius search with fused normals.
+ * pcp_index_build_h16 sorts the cloud (fp32 xyz) into cells of `cell_size` (0 < h <= 0.5 m,
+ * dense table) and stores each point as fp16 offsets from its cell origin (8 B) + its cell id.
+ * Queries are the indexed points whose caller index is < n_owned (the rest are a multi-GPU
+ * slab's halo).  pcp_h16_radius_count: per owned point the number of points with d2 < r^2
+ * (itself included), r <= cell size; pcp_scan_counts -> offsets; pcp_h16_radius_fill: the
+ * rows in index order (radiusSearch with setSortedResults(false), kd_tree.h:739-753,863-903)
+ * as global_id_dev[caller] (or the caller index when NULL), and optionally one F1 plane per
+ * row (calculate_plan_parameter(cloud, radius), calculate_feature.h:15) from fp32 sums.
+ * Distances are fp32 of fp16 offsets: pairs within 3e-4 m of the radius may differ from an
+ * exact search. */
+int pcp_index_build_h16(pcp_ctx* ctx, const float* xyz_dev, size_t stride_bytes, int64_t n,
+                        double cell_size, pcp_index** out);
+int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* index, float radius, int64_t n_owned,
+                         int32_t* count_dev);
+int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* index, float radius, int64_t n_owned,
+                        const int64_t* offsets_dev, const int32_t* global_id_dev,
+                        int32_t* idx_dev, pcp_plane* normals_dev);
+
 /* Batch KdTreeFLANN::radiusSearch (kd_tree.h:863-903): d2 < radius*radius (strict),
  * sorted by (d2, internal j), truncated to max_nn (0 or > size = unlimited).
  * Two-phase CSR: pcp_radius_count writes per-query counts; the caller scans them into

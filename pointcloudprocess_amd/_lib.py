@@ -43,6 +43,9 @@ SIGNATURES = [
     ("pcp_knn", _i32, [_vp, _vp, _vp, _sz, _i64, _i32, _vp, _vp]),
     ("pcp_radius_count", _i32, [_vp, _vp, _vp, _sz, _i64, _f64, _u32, _vp]),
     ("pcp_radius_fill", _i32, [_vp, _vp, _vp, _sz, _i64, _f64, _u32, _vp, _vp, _vp]),
+    ("pcp_index_build_h16", _i32, [_vp, _vp, _sz, _i64, _f64, _P(_vp)]),
+    ("pcp_h16_radius_count", _i32, [_vp, _vp, _f32, _i64, _vp]),
+    ("pcp_h16_radius_fill", _i32, [_vp, _vp, _f32, _i64, _vp, _vp, _vp, _vp]),
     ("pcp_scan_counts", _i32, [_vp, _vp, _i64, _vp, _P(_i64)]),
     ("pcp_knn_bruteforce", _i32, [_vp, _vp, _sz, _i64, _vp, _sz, _i64, _i32, _vp, _vp]),
     ("pcp_knn_bruteforce_last_fallback", _i32, [_vp, _vp]),

@@ -126,5 +126,10 @@ struct pcp_index {
     int32_t* mapping = nullptr; // internal j -> caller index (n)
     int32_t* sorted_j = nullptr; // sorted position -> internal j (n)
     int32_t* pos_of_j = nullptr; // internal j -> sorted position (n, fp64 index only)
+    // fp16 cell-relative index (C5, h16.hip): per sorted point its offset from its cell's
+    // origin as 3 x fp16 (+ 16-bit pad) and its dense cell id; pts is released after the build
+    int is_h16 = 0;
+    uint2* h16 = nullptr;
+    uint32_t* cell = nullptr;
     pcp_ctx* owner = nullptr;
 };

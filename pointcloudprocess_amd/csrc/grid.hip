@@ -621,6 +621,8 @@ int pcp_index_destroy(pcp_index* ix) {
     pcp::dfree(ix->owner, ix->mapping);
     pcp::dfree(ix->owner, ix->sorted_j);
     pcp::dfree(ix->owner, ix->pos_of_j);
+    pcp::dfree(ix->owner, ix->h16);
+    pcp::dfree(ix->owner, ix->cell);
     delete ix;
     return PCP_OK;
 }

@@ -1,0 +1,241 @@
+// C5 (BASELINE.json configs[4]): radius search r + per-point normals over a cloud stored as
+// fp16 offsets relative to each point's grid cell, accumulated in fp32
+// (KdTreeFLANN::radiusSearch kd_tree.h:863-903 with setSortedResults(false) :739-753, and the
+// declared-only calculate_plan_parameter(cloud, radius), calculate_feature.h:15 = F1 over
+// each radius neighbourhood, calculate_feature.cpp:119-206).
+//
+// Layout (HBM): the points in cell order (the fp32 grid build's radix sort), each as 8 bytes
+// {fp16 x, y, z offset from its cell origin o + c h, pad} (absolute fp16 would resolve only
+// ~6 cm at 100 m; offsets within a cell of h <= 0.4 m resolve <= 1.2e-4 m), its dense cell id
+// (4 B) and its caller index (4 B), plus the dense cell-start table.  Cell size h >= r, so a
+// query's neighbours lie in its 3x3x3 cells; rows of cells are pruned by the query's distance
+// to the cell faces.
+//
+// Numerics: d = (dc * h + (o_p - o_q)) per axis in fp32 (the fp16 difference is exact in
+// fp32), d2 = fmaf chain, neighbour iff d2 < r^2 (strict, as FLANN's RadiusResultSet).  Against
+// the exact fp64 search a pair can differ only when | |p - q| - r | < 3e-4 m (the fp16
+// quantisation bound); tests exclude that band.  Rows are in index (scan) order, the
+// reference's unsorted mode.  Normals: fp32 sums of the neighbours' offsets from the query
+// (n, S, S S^T), the covariance formed in fp64, then the F1 eigen core (pca.hpp).
+#include <cmath>
+
+#include "grid.hpp"
+#include "pca.hpp"
+
+namespace pcp {
+namespace {
+
+constexpr int kB = 256;
+
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+    const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+    return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+}
+__device__ __forceinline__ float h_lo(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)); }
+__device__ __forceinline__ float h_hi(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); }
+
+// sorted fp32 records -> fp16 cell offsets, cell ids, caller indices
+__global__ void k_h16_convert(GridDesc g, const float4* pts, int64_t n, uint2* rec, uint32_t* cell, int32_t* mapping) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 p = pts[i];
+        // the build's own cell of the point (grid.hip cell_of_point, fp32)
+        const int cx = clampi(cell_i<float>(g, p.x, 0), 0, g.n[0] - 1);
+        const int cy = clampi(cell_i<float>(g, p.y, 1), 0, g.n[1] - 1);
+        const int cz = clampi(cell_i<float>(g, p.z, 2), 0, g.n[2] - 1);
+        const float ox = (float)((double)p.x - (g.o[0] + (double)cx * g.h));
+        const float oy = (float)((double)p.y - (g.o[1] + (double)cy * g.h));
+        const float oz = (float)((double)p.z - (g.o[2] + (double)cz * g.h));
+        rec[i] = make_uint2(pack_h2(ox, oy), pack_h2(oz, 0.f));
+        cell[i] = (uint32_t)dense_id(g, cx, cy, cz);
+        mapping[i] = __float_as_int(p.w);
+    }
+}
+
+struct H16Args {
+    GridDesc g;
+    const uint2* rec;
+    const uint32_t* cell;
+    const int32_t* mapping;
+    int64_t n, n_owned;
+    float hf, r2, rcut2;  // cell size, r^2 (the test), (r + margin)^2 (cell pruning)
+};
+
+// one lane per sorted point; halo points (caller index >= n_owned) are not queries
+template <bool FILL>
+__global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, const int64_t* offsets,
+                                                   const int32_t* gid, int32_t* out_idx, pcp_plane* out_nrm) {
+    const GridDesc& g = a.g;
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < a.n; s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t caller = a.mapping[s];
+        if (caller >= a.n_owned) continue;
+        const uint2 qr = a.rec[s];
+        const float qx = h_lo(qr.x), qy = h_hi(qr.x), qz = h_lo(qr.y);
+        const uint32_t cid = a.cell[s];
+        const int cx = (int)(cid % (uint32_t)g.n[0]);
+        const int cy = (int)((cid / (uint32_t)g.n[0]) % (uint32_t)g.n[1]);
+        const int cz = (int)(cid / ((uint32_t)g.n[0] * (uint32_t)g.n[1]));
+        // distances to the faces of the query's cell (offsets can round a hair outside [0, h])
+        const float gxl = fmaxf(qx, 0.f), gxr = fmaxf(a.hf - qx, 0.f);
+        const float gyl = fmaxf(qy, 0.f), gyr = fmaxf(a.hf - qy, 0.f);
+        const float gzl = fmaxf(qz, 0.f), gzr = fmaxf(a.hf - qz, 0.f);
+        int64_t o = 0;
+        if (FILL) o = offsets[caller];
+        uint32_t cnt = 0;
+        float S0 = 0.f, S1 = 0.f, S2 = 0.f, S00 = 0.f, S01 = 0.f, S02 = 0.f, S11 = 0.f, S12 = 0.f, S22 = 0.f;
+        for (int dz = -1; dz <= 1; dz++) {
+            const int z = cz + dz;
+            if (z < 0 || z >= g.n[2]) continue;
+            const float gz = dz < 0 ? gzl : (dz > 0 ? gzr : 0.f);
+            for (int dy = -1; dy <= 1; dy++) {
+                const int y = cy + dy;
+                if (y < 0 || y >= g.n[1]) continue;
+                const float gy = dy < 0 ? gyl : (dy > 0 ? gyr : 0.f);
+                const float gyz = __fmaf_rn(gy, gy, gz * gz);
+                if (gyz >= a.rcut2) continue;
+                const int xa = (cx > 0 && __fmaf_rn(gxl, gxl, gyz) < a.rcut2) ? cx - 1 : cx;
+                const int xb = (cx + 1 < g.n[0] && __fmaf_rn(gxr, gxr, gyz) < a.rcut2) ? cx + 1 : cx;
+                const int64_t c0 = dense_id(g, xa, y, z), cq = dense_id(g, cx, y, z);
+                const uint32_t k0 = g.cstart[c0], k1 = g.cstart[c0 + (xb - xa + 1)];
+                const uint32_t b1 = g.cstart[cq], b2 = g.cstart[cq + 1];  // the query's x column
+                const float ey = (float)dy * a.hf - qy, ez = (float)dz * a.hf - qz;
+                for (uint32_t k = k0; k < k1; k++) {
+                    const uint2 pr = a.rec[k];
+                    const float dxc = k < b1 ? -a.hf : (k < b2 ? 0.f : a.hf);
+                    const float dx = dxc + (h_lo(pr.x) - qx);
+                    const float dy_ = ey + h_hi(pr.x);
+                    const float dz_ = ez + h_lo(pr.y);
+                    const float d2 = __fmaf_rn(dz_, dz_, __fmaf_rn(dy_, dy_, dx * dx));
+                    if (d2 < a.r2) {
+                        if (FILL) {
+                            const int32_t m = a.mapping[k];
+                            out_idx[o + cnt] = gid ? gid[m] : m;
+                            S0 += dx; S1 += dy_; S2 += dz_;
+                            S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy_, S01); S02 = __fmaf_rn(dx, dz_, S02);
+                            S11 = __fmaf_rn(dy_, dy_, S11); S12 = __fmaf_rn(dy_, dz_, S12); S22 = __fmaf_rn(dz_, dz_, S22);
+                        }
+                        cnt++;
+                    }
+                }
+            }
+        }
+        if (!FILL) {
+            count[caller] = (int32_t)cnt;
+        } else if (out_nrm) {
+            pcp_plane pl{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
+            if (cnt > 0) {
+                const double nn = (double)cnt;
+                const double m0 = S0 / nn, m1 = S1 / nn, m2 = S2 / nn;
+                const double C[9] = {S00 - nn * m0 * m0, S01 - nn * m0 * m1, S02 - nn * m0 * m2,
+                                     S01 - nn * m0 * m1, S11 - nn * m1 * m1, S12 - nn * m1 * m2,
+                                     S02 - nn * m0 * m2, S12 - nn * m1 * m2, S22 - nn * m2 * m2};
+                // the absolute mean = the query's position + the mean offset
+                const double xa = g.o[0] + (double)cx * g.h + (double)qx + m0;
+                const double ya = g.o[1] + (double)cy * g.h + (double)qy + m1;
+                const double za = g.o[2] + (double)cz * g.h + (double)qz + m2;
+                plane_from_cov(C, xa, ya, za, pl);
+            }
+            out_nrm[caller] = pl;
+        }
+    }
+}
+
+__global__ void k_h16_plane_default(pcp_plane* out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = pcp_plane{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};  // points dropped as non-finite
+}
+
+H16Args make_args(const pcp_index* ix, float r, int64_t n_owned) {
+    H16Args a{};
+    a.g = ix->g;
+    a.rec = ix->h16;
+    a.cell = ix->cell;
+    a.mapping = ix->mapping;
+    a.n = ix->n;
+    a.n_owned = n_owned;
+    a.hf = (float)ix->g.h;
+    a.r2 = r * r;
+    const float rc = r * 1.0001f + 2e-4f;  // conservative: fp16 offsets and fp32 face gaps
+    a.rcut2 = rc * rc;
+    return a;
+}
+
+int check_query(pcp_ctx* ctx, const pcp_index* ix, float r, int64_t n_owned) {
+    if (!ix || !ix->is_h16) return set_error(ctx, PCP_ERR_ARG, "not an fp16 (pcp_index_build_h16) index");
+    if (!(r > 0.f) || (double)r > ix->g.h * 1.000001)
+        return set_error(ctx, PCP_ERR_UNSUPPORTED, "h16 radius must satisfy 0 < r <= cell size (3x3x3 cells)");
+    if (n_owned < 0) return set_error(ctx, PCP_ERR_ARG, "n_owned < 0");
+    return PCP_OK;
+}
+
+}  // namespace
+}  // namespace pcp
+
+using namespace pcp;
+
+extern "C" {
+
+int pcp_index_build_h16(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size, pcp_index** out) {
+    if (!ctx || !out || !(cell_size > 0)) return set_error(ctx, PCP_ERR_ARG, "pcp_index_build_h16: bad arguments");
+    if (cell_size > 0.5) return set_error(ctx, PCP_ERR_UNSUPPORTED, "h16 cells > 0.5 m lose fp16 offset precision");
+    pcp_index* ix = nullptr;
+    PCP_TRY(pcp_index_build_f32(ctx, xyz, stride, n, cell_size, &ix));
+    if (!ix->g.dense) {
+        pcp_index_destroy(ix);
+        return set_error(ctx, PCP_ERR_UNSUPPORTED, "h16 index needs a dense cell table (bbox too large for the cell size)");
+    }
+    int rc = PCP_OK;
+    if ((rc = dmalloc(ctx, &ix->h16, ix->n + 1)) || (rc = dmalloc(ctx, &ix->cell, ix->n + 1)) ||
+        (!ix->mapping && (rc = dmalloc(ctx, &ix->mapping, ix->n + 1)))) {
+        pcp_index_destroy(ix);
+        return rc;
+    }
+    if (ix->n > 0)
+        hipLaunchKernelGGL(k_h16_convert, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, ix->g,
+                           (const float4*)ix->pts, ix->n, ix->h16, ix->cell, ix->mapping);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        pcp_index_destroy(ix);
+        return hip_fail(ctx, e, "h16 convert", __FILE__, __LINE__);
+    }
+    dfree(ctx, ix->pts);  // the fp32 records are not needed by the fp16 search
+    ix->pts = nullptr;
+    ix->is_h16 = 1;
+    *out = ix;
+    return PCP_OK;
+}
+
+int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t n_owned, int32_t* count_dev) {
+    if (!ctx || (n_owned > 0 && !count_dev)) return set_error(ctx, PCP_ERR_ARG, "pcp_h16_radius_count: bad arguments");
+    PCP_TRY(check_query(ctx, ix, radius, n_owned));
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (n_owned == 0) return PCP_OK;
+    // rows of owned points the build dropped as non-finite stay empty
+    PCP_HIP(ctx, hipMemsetAsync(count_dev, 0, (size_t)n_owned * sizeof(int32_t), ctx->stream));
+    if (ix->n == 0) return PCP_OK;
+    const H16Args a = make_args(ix, radius, n_owned);
+    hipLaunchKernelGGL(k_h16_radius<false>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, count_dev,
+                       (const int64_t*)nullptr, (const int32_t*)nullptr, (int32_t*)nullptr, (pcp_plane*)nullptr);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t n_owned, const int64_t* offsets_dev,
+                        const int32_t* global_id_dev, int32_t* idx_dev, pcp_plane* normals_dev) {
+    if (!ctx || (n_owned > 0 && (!offsets_dev || !idx_dev)))
+        return set_error(ctx, PCP_ERR_ARG, "pcp_h16_radius_fill: bad arguments");
+    PCP_TRY(check_query(ctx, ix, radius, n_owned));
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (n_owned == 0) return PCP_OK;
+    if (normals_dev)
+        hipLaunchKernelGGL(k_h16_plane_default, dim3(grid_for(n_owned, kB)), dim3(kB), 0, ctx->stream, normals_dev,
+                           n_owned);
+    if (ix->n == 0) return PCP_OK;
+    const H16Args a = make_args(ix, radius, n_owned);
+    hipLaunchKernelGGL(k_h16_radius<true>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, (int32_t*)nullptr,
+                       offsets_dev, global_id_dev, idx_dev, normals_dev);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+}  // extern "C"

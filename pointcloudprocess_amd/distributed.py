@@ -242,3 +242,28 @@ class GpuEngine:
     def close(self):
         self.icp.close()
         self.index.close()
+
+
+# ---- C5 radius + normals over x-slabs with an r-wide halo ("for radius,
+# exchange a halo of width r between slabs instead, so no per-query collective is needed")
+def radius_slab_split(x, world, rank, r):
+    """(owned, halo) indices of this rank's x-slab of the points with x-coordinates `x`:
+    equal-count slabs, halo = the points within r of the slab's faces (on the neighbours)."""
+    b = slab_bounds(x, world)
+    lo, hi = b[rank], b[rank + 1]
+    x = np.asarray(x)
+    own = np.nonzero((x >= lo) & (x < hi))[0]
+    halo = np.nonzero(((x >= lo - r) & (x < lo)) | ((x >= hi) & (x < hi + r)))[0]
+    return own, halo
+
+
+def radius_rows_slab(engine, xyz, r, world=None, rank=None):
+    """Rows (CSR over this rank's owned points, global ids) of the radius search with the
+    slab split; engine.radius_rows(local_xyz, n_owned, gid, r) -> (offsets, idx) does the
+    local search over owned + halo points.  No collective: every row is complete locally."""
+    world = _world() if world is None else world
+    rank = (dist.get_rank() if world > 1 else 0) if rank is None else rank
+    own, halo = radius_slab_split(np.asarray(xyz)[:, 0], world, rank, r)
+    gid = np.concatenate([own, halo]).astype(np.int32)
+    offs, idx = engine.radius_rows(np.asarray(xyz)[gid], len(own), gid, r)
+    return own, offs, idx

@@ -145,6 +145,41 @@ def radius(index, q, r, max_nn=0):
     return offs, idx[:total.value], d2[:total.value]
 
 
+class H16Index:
+    """C5 fp16 cell-relative index over an (n, 3) fp32 cloud (pcp_index_build_h16)."""
+
+    def __init__(self, ctx, xyz, cell_size):
+        self.ctx = ctx
+        self.src = xyz
+        h = C.c_void_p()
+        ctx.check(ctx.lib.pcp_index_build_h16(ctx.h, _ptr(xyz), xyz.stride(0) * xyz.element_size(), xyz.shape[0],
+                                              float(cell_size), C.byref(h)))
+        self.h = h
+
+    def radius_normals(self, r, n_owned=None, global_id=None, normals=True):
+        """Rows (offsets int64 (n_owned+1), idx int32) of the owned points + their planes."""
+        ctx = self.ctx
+        n_owned = self.src.shape[0] if n_owned is None else int(n_owned)
+        cnt = torch.empty(max(n_owned, 1), dtype=torch.int32, device=ctx.device)
+        ctx.check(ctx.lib.pcp_h16_radius_count(ctx.h, self.h, float(r), n_owned, _ptr(cnt)))
+        offs = torch.empty(n_owned + 1, dtype=torch.int64, device=ctx.device)
+        total = C.c_int64()
+        ctx.check(ctx.lib.pcp_scan_counts(ctx.h, _ptr(cnt), n_owned, _ptr(offs), C.byref(total)))
+        idx = torch.empty(max(total.value, 1), dtype=torch.int32, device=ctx.device)
+        nrm = torch.empty((max(n_owned, 1), 6), dtype=torch.float32, device=ctx.device) if normals else None
+        ctx.check(ctx.lib.pcp_h16_radius_fill(ctx.h, self.h, float(r), n_owned, _ptr(offs), _ptr(global_id),
+                                              _ptr(idx), _ptr(nrm)))
+        return offs, idx[:total.value], (nrm[:n_owned] if normals else None)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.pcp_index_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
 def nearest_query(index, q, init_bound=9999.0):
     """find_cloud_nearest_point_in_kdtree: (query index or -1, its 1-NN d2)."""
     ctx = index.ctx

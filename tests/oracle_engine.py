@@ -88,3 +88,18 @@ class OracleEngine:
               for x in box[0:2] for y in box[2:4] for z in box[4:6]]
         if not (min(xs) >= lo and max(xs) <= hi):
             flag[0] = 1
+
+
+class RadiusOracleEngine:
+    """C5 slab protocol on the CPU: exact fp64 radius rows (oracle kd-tree, d2 < r^2) of the
+    owned points over owned + halo, mapped to global ids."""
+
+    def radius_rows(self, local_xyz, n_owned, gid, r):
+        t = ora.KdTree(np.ascontiguousarray(local_xyz, dtype=np.float64))
+        offs = [0]
+        idx = []
+        for q in range(n_owned):
+            i, _ = t.radius(local_xyz[q], r, cap=len(local_xyz))
+            idx.extend(gid[i].tolist())
+            offs.append(len(idx))
+        return np.array(offs, np.int64), np.array(idx, np.int32)

@@ -108,3 +108,43 @@ def test_slab_guard_latches():
     T[0, 3] = 1.5
     eng.slab_guard(torch.from_numpy(T.reshape(16).copy()), box, -1.0, 11.0, flag)
     assert flag.item() == 1
+
+
+def _radius_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle_engine import RadiusOracleEngine
+    from pointcloudprocess_amd import distributed as D
+    xyz = _radius_data()
+    own, offs, idx = D.radius_rows_slab(RadiusOracleEngine(), xyz, 0.2)
+    out[rank] = (own, offs, idx)
+    dist.destroy_process_group()
+
+
+def _radius_data():
+    from pointcloudprocess_amd import synth
+    return synth.street_scene(60_000, 93, extent=(30.0, 30.0)).double().numpy()
+
+
+def test_radius_slab_halo_two_ranks():
+    """C5's multi-GPU layout (x-slabs + an r-wide halo, no collective in the data path) on
+    gloo: the union of the ranks' rows equals the single-process radius search (as sets;
+    exact fp64 on both sides)."""
+    import oracle_ctypes as ora
+    xyz = _radius_data()
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    mp.start_processes(_radius_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    t = ora.KdTree(xyz)
+    seen = np.zeros(len(xyz), bool)
+    for r in range(2):
+        own, offs, idx = out[r]
+        assert not seen[own].any()
+        seen[own] = True
+        for k in range(0, len(own), 7):
+            e, _ = t.radius(xyz[own[k]], 0.2, cap=len(xyz))
+            assert set(idx[offs[k]:offs[k + 1]].tolist()) == set(e.tolist())
+    assert seen.all()

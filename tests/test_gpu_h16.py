@@ -1,0 +1,109 @@
+"""C5 (BASELINE.json configs[4]): radius r = 0.2 + normals over fp16 cell-relative
+coordinates with fp32 accumulation (h16.hip).  Tolerance-based parity, as the config's
+fp16 storage implies (SURVEY.md §7 hard part 6):
+* neighbour sets: for every sampled query, every point closer than r - eps is in its row and
+  every point of its row is closer than r + eps (eps = 3e-4 m, the fp16 offset quantisation
+  bound), against an exact fp64 search (scipy cKDTree as the checker);
+* normals: the row's F1 plane (calculate_feature.cpp:119-206) against a float64 PCA of the
+  same row; sign canonicalised as everywhere in this build.
+* multi-GPU slab + halo split (two slabs on one GPU): each slab's rows use global ids and the
+  union equals the single-index result within the same band."""
+import numpy as np
+import pytest
+import torch
+from scipy.spatial import cKDTree
+
+pytestmark = pytest.mark.gpu
+R = 0.2
+EPS = 3e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from pointcloudprocess_amd import ops
+    return ops.Context(0)
+
+
+@pytest.fixture(scope="module")
+def scene():
+    from pointcloudprocess_amd import synth
+    xyz = synth.street_scene(1_500_000, 5101, extent=(40.0, 40.0)).numpy()  # C5 density
+    return xyz
+
+
+def _check_rows(xyz, offs, idx, sample, gid_of=None):
+    x64 = xyz.astype(np.float64)
+    tree = cKDTree(x64)
+    bad = 0
+    for q in sample:
+        row = idx[offs[q]:offs[q + 1]]
+        d = np.linalg.norm(x64[row] - x64[q], axis=1)
+        bad += int((d >= R + EPS).sum())  # nothing far outside
+        near = tree.query_ball_point(x64[q], R - EPS)
+        bad += len(set(near) - set(row.tolist()))  # nothing clearly inside missing
+        bad += len(row) - len(set(row.tolist()))  # no duplicates
+    return bad
+
+
+def test_h16_radius_rows_and_normals(ctx, scene):
+    from pointcloudprocess_amd import ops
+    xyz = scene
+    ix = ops.H16Index(ctx, torch.from_numpy(xyz).to(ctx.device), cell_size=R)
+    offs, idx, nrm = ix.radius_normals(R)
+    offs, idx, nrm = offs.cpu().numpy(), idx.cpu().numpy(), nrm.cpu().numpy()
+    n = len(xyz)
+    assert offs[0] == 0 and offs[-1] == len(idx) and (np.diff(offs) >= 1).all()  # itself included
+    mean_nb = len(idx) / n
+    assert 40 < mean_nb < 200, mean_nb
+    rng = np.random.default_rng(7)
+    sample = rng.choice(n, 4000, replace=False)
+    assert _check_rows(xyz, offs, idx, sample) == 0
+    # normals vs a float64 PCA of the same rows
+    dots, curv = [], []
+    x64 = xyz.astype(np.float64)
+    for q in sample:
+        row = idx[offs[q]:offs[q + 1]]
+        if len(row) < 10:
+            continue
+        P = x64[row]
+        C = np.cov((P - P.mean(0)).T, bias=True) * len(P)
+        w, V = np.linalg.eigh(C)
+        nv = V[:, 0]
+        dots.append(abs(float(np.dot(nv, nrm[q, :3]))))
+        curv.append(abs(w[0] / w.sum() - nrm[q, 4]))
+    dots, curv = np.array(dots), np.array(curv)
+    print(f"normals: 1-|dot| max {1 - dots.min():.3e} p99 {np.percentile(1 - dots, 99):.3e}; "
+          f"curvature err max {curv.max():.3e}")
+    assert np.percentile(1 - dots, 99) < 1e-6 and (1 - dots).max() < 1e-5 and curv.max() < 5e-4
+    ix.close()
+
+
+def test_h16_slab_halo_split_matches(ctx, scene):
+    """x-slab split with an r-wide halo (SURVEY.md §8(e) for radius): rank-local rows with
+    global ids == the single-index rows (band excepted)."""
+    from pointcloudprocess_amd import ops
+    xyz = scene
+    n = len(xyz)
+    cut = float(np.median(xyz[:, 0]))
+    rows = {}
+    for lo, hi in ((-np.inf, cut), (cut, np.inf)):
+        own = np.nonzero((xyz[:, 0] >= lo) & (xyz[:, 0] < hi))[0]
+        halo = np.nonzero(((xyz[:, 0] >= lo - R) & (xyz[:, 0] < lo)) | ((xyz[:, 0] >= hi) & (xyz[:, 0] < hi + R)))[0]
+        gid = np.concatenate([own, halo]).astype(np.int32)
+        ix = ops.H16Index(ctx, torch.from_numpy(xyz[gid]).to(ctx.device), cell_size=R)
+        offs, idx, _ = ix.radius_normals(R, n_owned=len(own), global_id=torch.from_numpy(gid).to(ctx.device),
+                                         normals=False)
+        offs, idx = offs.cpu().numpy(), idx.cpu().numpy()
+        for k in range(0, len(own), 97):
+            rows[int(own[k])] = idx[offs[k]:offs[k + 1]]
+        ix.close()
+    keys = np.array(sorted(rows))
+    x64 = xyz.astype(np.float64)
+    tree = cKDTree(x64)
+    bad = 0
+    for q in keys:
+        row = rows[q]
+        d = np.linalg.norm(x64[row] - x64[q], axis=1)
+        bad += int((d >= R + EPS).sum())
+        bad += len(set(tree.query_ball_point(x64[q], R - EPS)) - set(row.tolist()))
+    assert bad == 0 and len(keys) > 10000
