@@ -53,6 +53,7 @@ struct pcp_icp {
     size_t ntev = 0;              // pairs recorded since the last pcp_icp_kernel_ms
     int dbg = 0;                  // PCP_ICP_ABLATE flags (profiling only)
     unsigned long long* dbgcnt = nullptr;  // kDbgCount: [candidates, rows, queries]
+    uint2* dbgfz = nullptr;       // kDbgCount: per 64-query chunk {slack bits, launch} (freeze model)
     double last_ms = 0.0;
     int last_launches = 0;
     uint32_t last_fallback = 0;
@@ -111,6 +112,7 @@ struct IcpArgs {
     int dbg;            // ablation flags (PCP_ICP_ABLATE, profiling builds of the bench only)
     const float* pose;  // device poses (current, previous: 24 floats) overriding R/t, Rp/tq, or null
     unsigned long long* dbgcnt;  // kDbgCount counters, or null
+    uint2* dbgfz;       // kDbgCount: chunk freeze model state
 };
 
 // the pose as the kernels use it: from the device copy when the loop is device-resident
@@ -639,6 +641,49 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
                 a.sv[gw * a.sv_seg + pos] = (int32_t)i;
             }
             svn += (uint32_t)__popcll(msk);
+            if (a.dbg & kDbgCount) {
+                // chunk freeze model (counts only): a chunk frozen at launch s with slack tau (the
+                // min over members of the gap that keeps the winner) stays valid while every
+                // member moved less than tau since s
+                const int64_t ch = cstart_ + k * cstep;
+                const uint2 fz = a.dbgfz[ch];
+                const float tau = __uint_as_float(fz.x);
+                const uint32_t fsl = fz.y & 0xffu;
+                const float4 FA = s_pose[fsl][0], FB = s_pose[fsl][1], FC = s_pose[fsl][2];
+                const float fx_ = qx - __fmaf_rn(FA.z, qq.z, __fmaf_rn(FA.y, qq.y, __fmaf_rn(FA.x, qq.x, FC.y)));
+                const float fy_ = qy - __fmaf_rn(FB.y, qq.z, __fmaf_rn(FB.x, qq.y, __fmaf_rn(FA.w, qq.x, FC.z)));
+                const float fz_ = qz - __fmaf_rn(FC.x, qq.z, __fmaf_rn(FB.w, qq.y, __fmaf_rn(FB.z, qq.x, FC.w)));
+                float dq = valid ? sqrtf(fz_ * fz_ + fy_ * fy_ + fx_ * fx_) : 0.f;
+                for (int o = 32; o > 0; o >>= 1) dq = fmaxf(dq, __shfl_xor(dq, o, 64));
+                const bool skip = fz.y != 0u && tau > 0.f && ((a.launch - fz.y) & 0xffu) < kMaxAge && dq < tau;
+                const uint32_t nsrch = (uint32_t)__popcll(msk);
+                if (skip) {
+                    if (lane == 0) {
+                        atomicAdd(a.dbgcnt + 16, 1ull);
+                        atomicAdd(a.dbgcnt + 17, (unsigned long long)nsrch);  // must stay 0
+                    }
+                } else {
+                    float sl = INFINITY;
+                    if (valid) {
+                        if (!ok) {
+                            sl = 0.f;
+                        } else {
+                            float e0 = icp_d2(qx, qy, qz, p0), e1 = icp_d2(qx, qy, qz, p1), e2 = icp_d2(qx, qy, qz, p2);
+                            const float lo = fminf(e0, fminf(e1, e2));
+                            const float m2 = e0 == lo ? fminf(e1, e2) : (e1 == lo ? fminf(e0, e2) : fminf(e0, e1));
+                            const float d0 = sqrtf(m), d1 = sqrtf(m2);
+                            sl = fminf(0.5f * (fminf(lb, d1) - d0), fabsf(d0 - sqrtf(a.r2)));
+                            sl = fmaxf(sl * 0.999f - 1e-6f, 0.f);
+                        }
+                    }
+                    for (int o = 32; o > 0; o >>= 1) sl = fminf(sl, __shfl_xor(sl, o, 64));
+                    if (lane == 0) {
+                        a.dbgfz[ch] = make_uint2(__float_as_uint(sl), a.launch | 0x80000000u);
+                        if (sl > 0.f) atomicAdd(a.dbgcnt + 19, 1ull);
+                    }
+                }
+                if (lane == 0) atomicAdd(a.dbgcnt + 18, 1ull);
+            }
             if (ok && m <= a.r2 && !(a.dbg & kDbgNoAccum)) acc.add(qx, qy, qz, px, py, pz, m, ccx, ccy, ccz);
         }
         acc.flush(s_acc[wid], lane, ccx, ccy, ccz);
@@ -1006,9 +1051,19 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         }
         if (!staged && scanq && !(a.dbg & kDbgNoScan)) b.scan4(a.tp, rs, rn, qx, qy, qz);
         if (a.dbg & kDbgCount) {
-            atomicAdd(a.dbgcnt, (unsigned long long)(rn[0] + rn[1] + rn[2] + rn[3]));
+            const uint32_t len = scanq ? rn[0] + rn[1] + rn[2] + rn[3] : 0u;
+            atomicAdd(a.dbgcnt, (unsigned long long)len);
             atomicAdd(a.dbgcnt + 2, 1ull);
             if (staged) atomicAdd(a.dbgcnt + 3, 1ull);
+            // per chunk: the wave's longest list (what sets the chunk's time) and its histogram
+            const int wmax = wave_max_int((int)len);
+            if (lane == 0) {
+                atomicAdd(a.dbgcnt + 1, (unsigned long long)wmax);
+                atomicAdd(a.dbgcnt + 4, 1ull);
+                int bkt = 0;
+                while (bkt < 7 && wmax >= (32 << bkt)) bkt++;
+                atomicAdd(a.dbgcnt + 8 + bkt, 1ull);
+            }
         }
         bool settled = false, found = false;
         uint32_t win = ~0u;
@@ -1605,6 +1660,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.ring_all = a.g.dense ? 0 : 1;
     a.dbg = icp->dbg;
     a.dbgcnt = icp->dbgcnt;
+    a.dbgfz = icp->dbgfz;
     double* part_v = icp->partials;
     double* part_o = part_v + (int64_t)icp->nb_ver * kAcc;
     double* part_r = part_o + (int64_t)icp->nb_fast * kAcc;
@@ -1623,7 +1679,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
         e1 = icp->tev[icp->ntev].second;
         icp->ntev++;
     }
-    if (icp->dbgcnt) PCP_HIP(ctx, hipMemsetAsync(icp->dbgcnt, 0, 16 * sizeof(unsigned long long), ctx->stream));
+    if (icp->dbgcnt) PCP_HIP(ctx, hipMemsetAsync(icp->dbgcnt, 0, 32 * sizeof(unsigned long long), ctx->stream));
     PCP_HIP(ctx, hipEventRecord(e0, ctx->stream));
     const bool verify = a.g.dense && icp->launches > 0;  // the first launch has nothing cached
     icp->last_verified = verify;
@@ -1842,7 +1898,10 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
                 hipEventCreate(&icp->ev_mid) != hipSuccess || hipEventCreate(&icp->ev_ver) != hipSuccess))
         rc = pcp::set_error(ctx, PCP_ERR_HIP, "hipEventCreate failed");
     if (const char* ab = std::getenv("PCP_ICP_ABLATE")) icp->dbg = std::atoi(ab);
-    if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgcnt, 16);
+    if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgcnt, 32);
+    if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgfz, icp->nq / 64 + 2);
+    if (!rc && icp->dbgfz && hipMemsetAsync(icp->dbgfz, 0, (icp->nq / 64 + 2) * sizeof(uint2), ctx->stream) != hipSuccess)
+        rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
     if (rc) {
         pcp_icp_destroy(icp);
         return rc;
@@ -1866,6 +1925,7 @@ int pcp_icp_destroy(pcp_icp* icp) {
     pcp::dfree(icp->ctx, icp->svc);
 
     pcp::dfree(icp->ctx, icp->dbgcnt);
+    pcp::dfree(icp->ctx, icp->dbgfz);
     pcp::dfree(icp->ctx, icp->fb);
     pcp::dfree(icp->ctx, icp->fb_count);
     pcp::dfree(icp->ctx, icp->fb_off);
@@ -1909,13 +1969,16 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
         std::fprintf(stderr, "[pcp icp dbg=%d] verify %.4f ms  octant %.4f ms  fallback %.4f ms  searched %u  "
                      "n_fallback %u\n", icp->dbg, mv, m1 - mv, ms - m1, nsv, icp->last_fallback);
         if (icp->dbgcnt) {
-            unsigned long long c[16];
+            unsigned long long c[32];
             PCP_HIP(ctx, hipMemcpy(c, icp->dbgcnt, sizeof(c), hipMemcpyDeviceToHost));
-            std::fprintf(stderr, "[pcp icp dbg] octant candidates/query %.2f  rows/query %.2f  wave max/chunk %.2f\n",
-                         (double)c[0] / (double)(c[2] ? c[2] : 1), (double)c[1] / (double)(c[2] ? c[2] : 1),
-                         (double)c[3] * 64.0 / (double)(c[2] ? c[2] : 1));
+            std::fprintf(stderr, "[pcp icp dbg] octant candidates/query %.2f  wave max list/chunk %.2f  chunks %llu  "
+                         "chunk max-list histogram <32,<64,<128,<256,<512,<1k,<2k,>=2k: %llu %llu %llu %llu %llu %llu %llu %llu\n",
+                         (double)c[0] / (double)(c[2] ? c[2] : 1), (double)c[1] / (double)(c[4] ? c[4] : 1), c[4],
+                         c[8], c[9], c[10], c[11], c[12], c[13], c[14], c[15]);
             std::fprintf(stderr, "[pcp icp dbg] fallback: settled by the 3x3x3 stage %llu, with a correspondence %llu\n",
                          c[5], c[6]);
+            std::fprintf(stderr, "[pcp icp dbg] freeze model: chunks %llu skippable %llu (searched lanes in them %llu) "
+                         "refrozen with slack>0 %llu\n", c[18], c[16], c[17], c[19]);
         }
     }
     return PCP_OK;

@@ -42,6 +42,11 @@ for rep in range(args.reps):
         print(f"rep{rep} iter{it}: {ms:.4f} ms  fallback {icp.last_fallback()}", flush=True)
         if rc != 0:
             break
-        T = dT @ T
+        Tn = dT @ T
+        # largest displacement this update causes over the scene's box (corners at +-100 m, z 0..20)
+        cs = np.array([[x, y, z, 1.0] for x in (-100, 100) for y in (-100, 100) for z in (0, 20)])
+        disp = np.abs((cs @ (Tn - T).T)[:, :3]).max()
+        print(f"   pose step max corner displacement {disp * 1e3:.3f} mm", flush=True)
+        T = Tn
     print(f"rep{rep}: {tot:.3f} ms over {args.iters} iterations ({tot / args.iters:.4f} ms/iter)  "
           f"|T-T_true| {np.abs(T - T_true).max():.2e}", flush=True)
