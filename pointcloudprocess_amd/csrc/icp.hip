@@ -641,6 +641,22 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
                 a.sv[gw * a.sv_seg + pos] = (int32_t)i;
             }
             svn += (uint32_t)__popcll(msk);
+            if ((a.dbg & kDbgCount) && valid) {
+                // why queries are searched: reason and where the winner sits relative to D
+                const float Dv = __uint_as_float(Dw & ~0xffu);
+                if (ok) {
+                    atomicAdd(a.dbgcnt + 20, 1ull);
+                } else if (((a.launch - Dw) & 0xffu) >= kMaxAge) {
+                    atomicAdd(a.dbgcnt + 21, 1ull);
+                } else if (Dv == 0.f) {
+                    atomicAdd(a.dbgcnt + 22, 1ull);
+                } else {
+                    const float r = sqrtf(m) / Dv;
+                    atomicAdd(a.dbgcnt + (r < 0.5f ? 23 : r < 0.75f ? 24 : r < 1.f ? 25 : 26), 1ull);
+                    const float rd = delta / Dv;
+                    atomicAdd(a.dbgcnt + (rd < 0.1f ? 27 : rd < 0.25f ? 28 : rd < 0.5f ? 29 : 30), 1ull);
+                }
+            }
             if (a.dbg & kDbgCount) {
                 // chunk freeze model (counts only): a chunk frozen at launch s with slack tau (the
                 // min over members of the gap that keeps the winner) stays valid while every
@@ -696,51 +712,6 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
 }
 
-// running kCache(=4)-NN of the search pass: d0 <= d1 <= d2 <= d3 with positions p0..p3, and
-// d4 = the 5th smallest d2 scanned (every uncached scanned point is >= d4).  Equal d2 values
-// keep scan order.  ~16 VALU ops per candidate beyond the d2 (med3 insertion network).
-struct Top4 {
-    float d0 = INFINITY, d1 = INFINITY, d2 = INFINITY, d3 = INFINITY, d4 = INFINITY;
-    uint32_t p0 = ~0u, p1 = ~0u, p2 = ~0u, p3 = ~0u;
-    __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t k) {
-        const float x = icp_d2(qx, qy, qz, p);
-        const bool c0 = x < d0, c1 = x < d1, c2 = x < d2, c3 = x < d3;
-        d4 = __builtin_amdgcn_fmed3f(d3, d4, x);
-        p3 = c2 ? p2 : (c3 ? k : p3);
-        d3 = __builtin_amdgcn_fmed3f(d2, d3, x);
-        p2 = c1 ? p1 : (c2 ? k : p2);
-        d2 = __builtin_amdgcn_fmed3f(d1, d2, x);
-        p1 = c0 ? p0 : (c1 ? k : p1);
-        d1 = __builtin_amdgcn_fmed3f(d0, d1, x);
-        p0 = c0 ? k : p0;
-        d0 = fminf(d0, x);
-    }
-    // rows [rs[r], rs[r] + rn[r]) scanned as one concatenated list, U loads in flight;
-    // branch-free addressing: k = v + off(v), off from 3 compares against the row prefixes
-    __device__ __forceinline__ void scan4(const float4* pts, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
-                                          float qx, float qy, float qz) {
-        const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
-        const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
-        auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3, o0, o1, o2, o3); };
-        constexpr int U = PCP_SCAN_UNROLL;
-        uint32_t v = 0;
-        for (; v + U <= L; v += U) {
-            uint32_t k[U];
-            float4 p[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) k[u] = addr(v + u);
-#pragma unroll
-            for (int u = 0; u < U; u++) p[u] = pts[k[u]];
-#pragma unroll
-            for (int u = 0; u < U; u++) consider(qx, qy, qz, p[u], k[u]);
-        }
-        for (; v < L; v++) {
-            const uint32_t k = addr(v);
-            consider(qx, qy, qz, pts[k], k);
-        }
-    }
-};
-
 // running 3-NN (kCache = 3): d0 <= d1 <= d2 with positions, d3 = the 4th smallest d2 scanned
 struct Top3 {
     float d0 = INFINITY, d1 = INFINITY, d2 = INFINITY, d3 = INFINITY;
@@ -789,19 +760,13 @@ struct Top3 {
     }
 };
 
-// running 3-NN on packed keys (PCP_TOPK_PACKED): key = (bits(d2') & ~255) | v, v the
-// candidate's index in the concatenated octant list (< 256), d2' the contract's d2 chain
-// started from FLT_MIN (so no key is denormal).  Positive floats order like their bits, so a
-// v_med3_u32 network on the keys keeps the 4 smallest keys -- values and list indices
-// together -- in 4 VALU ops per candidate (the compare-swap form needs 13).  The truncated
-// d2 only chooses WHICH points are cached: the winner among them is decided on the exact d2
-// afterwards, and the 4th key with its low byte cleared bounds every uncached point's d2.
-// Measured (r15f-j): exact, 7 % faster on the full first launch, but 10-20 % slower on the
-// later launches' scattered search lists (latency-bound there; 8 waves only recover parity),
-// so it is off by default.
-#ifndef PCP_TOPK_PACKED
-#define PCP_TOPK_PACKED 0
-#endif
+// running 3-NN on packed keys: key = (bits(d2) & ~255) | v, v the candidate's index in the
+// concatenated octant list (< 256).  Non-negative floats order like their bits, so a
+// v_med3_u32 network keeps the 4 smallest keys -- values and list indices together -- in 4 VALU
+// ops per candidate (the compare-swap form, Top3, needs 16).  The truncated d2 only chooses
+// WHICH points are cached: the winner among them is decided on the exact d2 afterwards, and
+// the 4th key with its low byte cleared bounds the d2 of every scanned point not kept (an
+// uncached point's key is >= t3, so its d2 bits are >= t3 & ~255).
 constexpr uint32_t kKeyMax = 0x7f7fffffu;  // FLT_MAX: above every real key
 constexpr uint32_t kMaxOctList = 256;       // list indices that fit the key's low byte
 // median of three u32 (one v_med3_u32; the float form adds canonicalizing ops on bit-cast keys)
@@ -810,37 +775,59 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
-struct Top3K {
+// position of candidate v of the concatenated rows, or the far sentinel `sent` past the list
+__device__ __forceinline__ uint32_t cat_addr_l(uint32_t v, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t L,
+                                               uint32_t o0, uint32_t o1, uint32_t o2, uint32_t o3, uint32_t sent) {
+    const uint32_t d = v < L ? o3 : sent - v;
+    const uint32_t c = v < c3 ? o2 : d;
+    const uint32_t b = v < c2 ? o1 : c;
+    return v + (v < c1 ? o0 : b);
+}
+__device__ __forceinline__ int wave_max_u(int v) {
+    v = max(v, __shfl_xor(v, 1, 64));
+    v = max(v, __shfl_xor(v, 2, 64));
+    v = max(v, __shfl_xor(v, 4, 64));
+    v = max(v, __shfl_xor(v, 8, 64));
+    v = max(v, __shfl_xor(v, 16, 64));
+    v = max(v, __shfl_xor(v, 32, 64));
+    return v;
+}
+struct Top3P {
     uint32_t t0 = kKeyMax, t1 = kKeyMax, t2 = kKeyMax, t3 = kKeyMax;
     __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t v) {
-        const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
-        const float d = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, __fmaf_rn(dx, dx, 1.17549435e-38f)));
+        const float d = icp_d2(qx, qy, qz, p);
         const uint32_t x = (__float_as_uint(d) & ~0xffu) | v;
         t3 = umed3(t2, t3, x);
         t2 = umed3(t1, t2, x);
         t1 = umed3(t0, t1, x);
         t0 = min(t0, x);
     }
-    __device__ __forceinline__ void scan4(const float4* pts, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
-                                          float qx, float qy, float qz) {
+    // the wave's lists with a uniform trip count (lanes past their own list read the far
+    // sentinel: d2 = inf, never kept), U loads per step, the next step's loads issued before
+    // this step's keys are formed (software pipeline: two batches in flight)
+    __device__ __forceinline__ void scan4(const float4* pts, uint32_t sent, const uint32_t (&rs)[4],
+                                          const uint32_t (&rn)[4], uint32_t Lw, float qx, float qy, float qz) {
         const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
         const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
-        auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3, o0, o1, o2, o3); };
-        constexpr int U = PCP_SCAN_UNROLL;
-        uint32_t v = 0;
-        for (; v + U <= L; v += U) {
-            float4 p[U];
+        auto addr = [=](uint32_t v) { return cat_addr_l(v, c1, c2, c3, L, o0, o1, o2, o3, sent); };
+        constexpr int U = 4;
+        float4 A[U], B[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) p[u] = pts[addr(v + u)];
+        for (int u = 0; u < U; u++) A[u] = ld16(pts, addr(u));
+        for (uint32_t v = 0; v < Lw; v += 2 * U) {
+            // two register sets, no copies: B's loads are in flight while A's keys are formed
 #pragma unroll
-            for (int u = 0; u < U; u++) consider(qx, qy, qz, p[u], v + u);
+            for (int u = 0; u < U; u++) B[u] = ld16(pts, addr(v + U + u));
+            __builtin_amdgcn_sched_barrier(0);  // keep B's loads ahead of A's keys
+#pragma unroll
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, A[u], v + u);
+            if (v + U >= Lw) break;
+#pragma unroll
+            for (int u = 0; u < U; u++) A[u] = ld16(pts, addr(v + 2 * U + u));
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, B[u], v + U + u);
         }
-        for (; v < L; v++) consider(qx, qy, qz, pts[addr(v)], v);
-    }
-    // lower bound on the d2 of every scanned point that is not among the 3 kept
-    __device__ __forceinline__ float uncached_lb() const {
-        const uint32_t k = t3;
-        return k == kKeyMax ? INFINITY : __uint_as_float(k & ~0xffu) * (1.f - 1e-6f);
     }
 };
 
@@ -853,33 +840,71 @@ struct Top3K {
 // certified when rmax <= m.  The cache is refreshed either way (D = min(d3, m) bounds every
 // uncached point); unsettled queries go to the fallback list.
 //
-// LDS staging (dense chunks): the 64 queries of a chunk are spatial neighbours (brick-major
-// query order), so their octants overlap heavily.  When the union box of the chunk's octant
-// blocks spans at most kStageRows (y,z) rows and kStageCap targets, the wave copies those
-// rows once into LDS (coalesced: each row's x-range is one contiguous run of the cell-sorted
-// targets, tagged with its sorted position) and every lane scans its octant from LDS --
-// ~7x fewer global loads than one gather per candidate per lane.  Wider chunks (the sparse
-// search lists of later launches) scan straight from HBM.
-#ifndef PCP_OCT_LDS
-#define PCP_OCT_LDS 0
-#endif
-#ifndef PCP_STAGE_CAP
-#define PCP_STAGE_CAP 384
-#endif
-constexpr int kStageCap = PCP_STAGE_CAP;  // staged targets per wave (16 B each)
-constexpr int kStageRows = 16;            // staged (y,z) rows per wave
-constexpr int kStageW = 16;               // cell starts per staged row (box width + 1)
-static_assert(PCP_CACHE3 && !PCP_TOPK_PACKED, "the search pass keeps a 3-point cache");
+// The scan keeps packed (d2, list index) keys (Top3P, 4 VALU ops per candidate) with a
+// wave-uniform trip count; a chunk with a list longer than 256 candidates (the key's low byte)
+// uses the compare-swap form (Top3).  Both end in the same OctResult: the exact (d2, index)
+// winner among the 3 kept, its coordinates, the 3 cached positions and the first-uncached bound.
+static_assert(PCP_CACHE3, "the search pass keeps a 3-point cache");
 
-__device__ __forceinline__ int wave_min_int(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
+struct OctResult {
+    float d0 = INFINITY;       // exact d2 of the winner among the kept points
+    uint32_t win = ~0u;        // its sorted position (~0u: nothing scanned)
+    float wx = 0.f, wy = 0.f, wz = 0.f;
+    uint32_t c0 = ~0u, c1 = ~0u, c2 = ~0u;  // the cache: positions of the 3 kept points
+    float dnext = INFINITY;    // lower bound on the d2 of every scanned point not kept
+};
+
+__device__ __forceinline__ void take_exact(OctResult& o, const float4 p, uint32_t pos, float qx, float qy, float qz,
+                                           int& wj) {
+    const float e = icp_d2(qx, qy, qz, p);
+    const int id = __float_as_int(p.w);
+    const bool t = pos != ~0u && (e < o.d0 || (e == o.d0 && id < wj));
+    o.d0 = t ? e : o.d0;
+    wj = t ? id : wj;
+    o.win = t ? pos : o.win;
+    o.wx = t ? p.x : o.wx;
+    o.wy = t ? p.y : o.wy;
+    o.wz = t ? p.z : o.wz;
 }
-__device__ __forceinline__ int wave_max_int(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
+
+// packed-key scan (every lane's list < 256 candidates)
+__device__ __forceinline__ OctResult octant_packed(const IcpArgs& a, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
+                                                   uint32_t Lw, float qx, float qy, float qz) {
+    Top3P k;
+    k.scan4(a.tp, a.ntp, rs, rn, Lw, qx, qy, qz);
+    const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
+    const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
+    OctResult o;
+    o.c0 = k.t0 != kKeyMax ? cat_addr_l(k.t0 & 0xffu, c1, c2, c3, L, o0, o1, o2, o3, a.ntp) : ~0u;
+    o.c1 = k.t1 != kKeyMax ? cat_addr_l(k.t1 & 0xffu, c1, c2, c3, L, o0, o1, o2, o3, a.ntp) : ~0u;
+    o.c2 = k.t2 != kKeyMax ? cat_addr_l(k.t2 & 0xffu, c1, c2, c3, L, o0, o1, o2, o3, a.ntp) : ~0u;
+    const float4 p0 = ld16(a.tp, min(o.c0, a.ntp)), p1 = ld16(a.tp, min(o.c1, a.ntp)), p2 = ld16(a.tp, min(o.c2, a.ntp));
+    int wj = 0x7fffffff;
+    take_exact(o, p0, o.c0, qx, qy, qz, wj);
+    take_exact(o, p1, o.c1, qx, qy, qz, wj);
+    take_exact(o, p2, o.c2, qx, qy, qz, wj);
+    o.dnext = k.t3 == kKeyMax ? INFINITY : __uint_as_float(k.t3 & ~0xffu);
+    return o;
+}
+
+// compare-swap scan (a chunk with a list of 256 or more candidates)
+__device__ __noinline__ OctResult octant_exact(const IcpArgs& a, uint32_t rs0, uint32_t rs1, uint32_t rs2, uint32_t rs3,
+                                               uint32_t rn0, uint32_t rn1, uint32_t rn2, uint32_t rn3, float qx, float qy,
+                                               float qz) {
+    const uint32_t rs[4] = {rs0, rs1, rs2, rs3}, rn[4] = {rn0, rn1, rn2, rn3};
+    Top3 b;
+    b.scan4(a.tp, rs, rn, qx, qy, qz);
+    OctResult o;
+    o.c0 = b.p0;
+    o.c1 = b.p1;
+    o.c2 = b.p2;
+    const float4 p0 = ld16(a.tp, min(b.p0, a.ntp)), p1 = ld16(a.tp, min(b.p1, a.ntp)), p2 = ld16(a.tp, min(b.p2, a.ntp));
+    int wj = 0x7fffffff;
+    take_exact(o, p0, o.c0, qx, qy, qz, wj);
+    take_exact(o, p1, o.c1, qx, qy, qz, wj);
+    take_exact(o, p2, o.c2, qx, qy, qz, wj);
+    o.dnext = b.d3;
+    return o;
 }
 
 __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a, const int32_t* list,
@@ -887,11 +912,6 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
     load_pose(a);
     constexpr int kW = kIcpBlock / 64;
     __shared__ double s_acc[kW][kAcc];
-#if PCP_OCT_LDS
-    __shared__ float4 s_pts[kW][kStageCap];
-    __shared__ uint32_t s_rbase[kW][kStageRows + 1];  // LDS offset of each staged row (+ total)
-    __shared__ uint32_t s_cst[kW][kStageRows * kStageW];  // the box's cell starts, kStageW per row
-#endif
     const GridDesc& g = a.g;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;  // global wave id = fallback segment
@@ -914,9 +934,6 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             in_ = list ? (int64_t)list[j + 64 * nwaves] : j + 64 * nwaves;
             qn = a.q[in_];
         }
-        Top3 b;
-        float wx = 0.f, wy = 0.f, wz = 0.f;  // the nearest's coordinates when it came from the stage
-        bool wlds = false;
         float qx = 0.f, qy = 0.f, qz = 0.f, fx = 0.f, fy = 0.f, fz = 0.f, dout = 0.f;
         int bx = 0, by = 0, bz = 0;
         bool outside = true;
@@ -937,136 +954,39 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         // the octant's 4 x-rows (y = by + (r & 1), z = bz + (r >> 1)), cells [xa, xb]
         const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
         uint32_t rs[4], rn[4];
-        bool staged = false;
-#if PCP_OCT_LDS
-        {
-            // union box of the chunk's octant blocks, clipped to the grid (wave-uniform)
-            const int x0 = max(wave_min_int(scanq ? bx : INT_MAX), 0);
-            const int x1 = min(wave_max_int(scanq ? bx + 1 : INT_MIN), g.n[0] - 1);
-            const int y0 = max(wave_min_int(scanq ? by : INT_MAX), 0);
-            const int y1 = min(wave_max_int(scanq ? by + 1 : INT_MIN), g.n[1] - 1);
-            const int z0 = max(wave_min_int(scanq ? bz : INT_MAX), 0);
-            const int z1 = min(wave_max_int(scanq ? bz + 1 : INT_MIN), g.n[2] - 1);
-            const int nxb = x1 - x0 + 1, nyb = y1 - y0 + 1, nrow = nyb * (z1 - z0 + 1);
-            if (x0 <= x1 && y0 <= y1 && z0 <= z1 && nrow <= kStageRows && nxb < kStageW) {
-                // the box's cell starts, row by row (cells x0 .. x1 + 1): one coalesced round trip
-                const int ncs = nrow * (nxb + 1);
 #pragma unroll
-                for (int k = 0; k < (kStageRows * kStageW + 63) / 64; k++) {
-                    const int e = lane + 64 * k;
-                    if (e < ncs) {
-                        const int r = e / (nxb + 1), cx = e - r * (nxb + 1);
-                        s_cst[wid][r * kStageW + cx] = g.cstart[dense_id(g, x0 + cx, y0 + r % nyb, z0 + r / nyb)];
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                uint32_t cnt = 0;
-                if (lane < nrow) cnt = s_cst[wid][lane * kStageW + nxb] - s_cst[wid][lane * kStageW];
-                uint32_t inc = cnt;  // inclusive scan over the rows
-#pragma unroll
-                for (int o = 1; o < kStageRows; o <<= 1) {
-                    const uint32_t t = __shfl_up(inc, o, 64);
-                    if (lane >= o) inc += t;
-                }
-                const uint32_t total = __shfl(inc, kStageRows - 1, 64);
-                if (total <= (uint32_t)kStageCap) {
-                    staged = true;
-                    if (lane < nrow) s_rbase[wid][lane] = inc - cnt;
-                    if (lane == 0) s_rbase[wid][nrow] = total;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    // fill: entry e = lane + 64 k of the concatenated rows -> LDS, .w = its sorted
-                    // position.  Rows by a branch-free binary search of the row bases (LDS), the
-                    // loads of a batch in flight together (one memory round trip).
-                    constexpr int kPer = kStageCap / 64, kBatch = (kPer % 3 == 0) ? 3 : 2;
-                    static_assert(kPer % kBatch == 0, "fill batches");
-#pragma unroll
-                    for (int k0 = 0; k0 < kPer; k0 += kBatch) {
-                        uint32_t gp[kBatch];
-                        float4 fp[kBatch];
-#pragma unroll
-                        for (int k = 0; k < kBatch; k++) {
-                            const uint32_t e = lane + 64u * (k0 + k);
-                            int r = 0;
-#pragma unroll
-                            for (int st = kStageRows / 2; st > 0; st >>= 1)
-                                r = (r + st < nrow && s_rbase[wid][r + st] <= e) ? r + st : r;
-                            gp[k] = s_cst[wid][r * kStageW] + (e - s_rbase[wid][r]);
-                        }
-#pragma unroll
-                        for (int k = 0; k < kBatch; k++)
-                            if (lane + 64u * (k0 + k) < total) fp[k] = a.tp[gp[k]];
-#pragma unroll
-                        for (int k = 0; k < kBatch; k++)
-                            if (lane + 64u * (k0 + k) < total)
-                                s_pts[wid][lane + 64 * (k0 + k)] =
-                                    make_float4(fp[k].x, fp[k].y, fp[k].z, __uint_as_float(gp[k]));
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    // this lane's rows -> LDS ranges (from the staged cell starts)
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const int y = by + (r & 1), z = bz + (r >> 1);
-                        const bool in = scanq && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
-                        const int row = in ? (z - z0) * nyb + (y - y0) : 0;
-                        const uint32_t c0 = s_cst[wid][row * kStageW], base = s_rbase[wid][row];
-                        const uint32_t ca = s_cst[wid][row * kStageW + (xa - x0)];
-                        const uint32_t cb = s_cst[wid][row * kStageW + (xb - x0) + 1];
-                        rs[r] = in ? base + (ca - c0) : 0u;
-                        rn[r] = in ? cb - ca : 0u;
-                    }
-                    if (!(a.dbg & kDbgNoScan)) b.scan4(&s_pts[wid][0], rs, rn, qx, qy, qz);
-                    // the winner's coordinates straight from the stage; LDS slots -> sorted positions
-                    if (b.p0 != ~0u) {
-                        const float4 w = s_pts[wid][b.p0];
-                        wx = w.x; wy = w.y; wz = w.z;
-                        wlds = true;
-                    }
-                    b.p0 = b.p0 != ~0u ? __float_as_uint(s_pts[wid][b.p0].w) : ~0u;
-                    b.p1 = b.p1 != ~0u ? __float_as_uint(s_pts[wid][b.p1].w) : ~0u;
-                    b.p2 = b.p2 != ~0u ? __float_as_uint(s_pts[wid][b.p2].w) : ~0u;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();  // the next chunk overwrites the stage
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
+        for (int r = 0; r < 4; r++) {
+            const int y = by + (r & 1), z = bz + (r >> 1);
+            const bool in = scanq && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
+            const int64_t cc = in ? dense_id(g, xa, y, z) : 0;
+            rs[r] = in ? g.cstart[cc] : 0u;
+            rn[r] = in ? g.cstart[cc + (xb - xa + 1)] : 0u;
         }
-#endif
-        if (!staged) {  // global path: the 4 rows' sorted ranges straight from the cell table
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int y = by + (r & 1), z = bz + (r >> 1);
-                const bool in = scanq && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
-                const int64_t cc = in ? dense_id(g, xa, y, z) : 0;
-                rs[r] = in ? g.cstart[cc] : 0u;
-                rn[r] = in ? g.cstart[cc + (xb - xa + 1)] : 0u;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++) rn[r] -= rs[r];
+        for (int r = 0; r < 4; r++) rn[r] -= rs[r];
+        const uint32_t len = rn[0] + rn[1] + rn[2] + rn[3];
+        const uint32_t Lw = (uint32_t)__builtin_amdgcn_readfirstlane(wave_max_u((int)len));  // wave-uniform
+        OctResult o;
+        if (!(a.dbg & kDbgNoScan)) {
+            if (Lw <= kMaxOctList)
+                o = octant_packed(a, rs, rn, Lw, qx, qy, qz);
+            else
+                o = octant_exact(a, rs[0], rs[1], rs[2], rs[3], rn[0], rn[1], rn[2], rn[3], qx, qy, qz);
         }
-        if (!staged && scanq && !(a.dbg & kDbgNoScan)) b.scan4(a.tp, rs, rn, qx, qy, qz);
         if (a.dbg & kDbgCount) {
-            const uint32_t len = scanq ? rn[0] + rn[1] + rn[2] + rn[3] : 0u;
             atomicAdd(a.dbgcnt, (unsigned long long)len);
             atomicAdd(a.dbgcnt + 2, 1ull);
-            if (staged) atomicAdd(a.dbgcnt + 3, 1ull);
+            if (Lw > kMaxOctList) atomicAdd(a.dbgcnt + 3, 1ull);
             // per chunk: the wave's longest list (what sets the chunk's time) and its histogram
-            const int wmax = wave_max_int((int)len);
             if (lane == 0) {
-                atomicAdd(a.dbgcnt + 1, (unsigned long long)wmax);
+                atomicAdd(a.dbgcnt + 1, (unsigned long long)Lw);
                 atomicAdd(a.dbgcnt + 4, 1ull);
                 int bkt = 0;
-                while (bkt < 7 && wmax >= (32 << bkt)) bkt++;
+                while (bkt < 7 && Lw >= (32u << bkt)) bkt++;
                 atomicAdd(a.dbgcnt + 8 + bkt, 1ull);
             }
         }
         bool settled = false, found = false;
-        uint32_t win = ~0u;
         if (valid) {
             // this query's certified radius (cells): its distance to the nearest face of the
             // 2x2x2 block (>= 0.5 cell), less the margin
@@ -1075,29 +995,15 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
                                   fminf(fz - (float)bz, (float)(bz + 2) - fz)) - a.mc;
             const float rr = m * g.hf;
             const float cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
-            found = b.d0 <= a.r2;
-            const float dnext = b.d3;  // the first uncached d2
-            settled = (found ? (b.d0 < dnext && b.d0 <= cert2) : a.r2 <= cert2) || outside ||
+            found = o.d0 <= a.r2;
+            settled = (found ? (o.d0 < o.dnext && o.d0 <= cert2) : a.r2 <= cert2) || outside ||
                       (a.dbg & kDbgNoFallback);
-            // the winner among the cached ties by target index (rare: only when d1 == d0)
-            win = b.p0;
-            if (found && b.d1 == b.d0) {
-                int wj = __float_as_int(a.tp[b.p0].w);
-                const uint32_t ps[2] = {b.p1, b.p2};
-                const float ds[2] = {b.d1, b.d2};
-#pragma unroll
-                for (int s2 = 0; s2 < 2; s2++) {
-                    if (ds[s2] != b.d0) break;
-                    const int id = __float_as_int(a.tp[ps[s2]].w);
-                    if (id < wj) { wj = id; win = ps[s2]; }
-                }
-            }
             // the cache: the 3 nearest; settled: D bounds every uncached point for the verify
             // pass.  Unsettled: the fallback pass (which overwrites the cache) gets the
             // octant's first uncached d2 instead.
             const float D = outside ? dout * 0.9999f
-                                    : (settled ? fminf(sqrtf(dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : dnext);
-            a.cand[i] = make_uint4(b.p0, b.p1, b.p2, pack_dlb(D, a.launch));
+                                    : (settled ? fminf(sqrtf(o.dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : o.dnext);
+            a.cand[i] = make_uint4(o.c0, o.c1, o.c2, pack_dlb(D, a.launch));
         }
         // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
         const bool fb = valid && !settled;
@@ -1109,8 +1015,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         }
         fbn += (uint32_t)__popcll(fbm);
         const bool acc_ok = valid && settled && found && !(a.dbg & kDbgNoAccum);
-        Best w{b.d0, 0, win, wx, wy, wz};
-        if (acc_ok && !(wlds && win == b.p0)) w.fetch(a.tp);
+        const Best w{o.d0, 0, o.win, o.wx, o.wy, o.wz};
         chunk_accumulate(acc_ok, qx, qy, qz, w, s_acc[wid], lane);
     }
     if (lane == 0) {  // every wave of the grid writes its count: no zeroing pass needed
@@ -1971,14 +1876,17 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
         if (icp->dbgcnt) {
             unsigned long long c[32];
             PCP_HIP(ctx, hipMemcpy(c, icp->dbgcnt, sizeof(c), hipMemcpyDeviceToHost));
-            std::fprintf(stderr, "[pcp icp dbg] octant candidates/query %.2f  wave max list/chunk %.2f  chunks %llu  "
+            std::fprintf(stderr, "[pcp icp dbg] octant candidates/query %.2f  wave max list/chunk %.2f  chunks %llu (compare-swap %llu)  "
                          "chunk max-list histogram <32,<64,<128,<256,<512,<1k,<2k,>=2k: %llu %llu %llu %llu %llu %llu %llu %llu\n",
-                         (double)c[0] / (double)(c[2] ? c[2] : 1), (double)c[1] / (double)(c[4] ? c[4] : 1), c[4],
+                         (double)c[0] / (double)(c[2] ? c[2] : 1), (double)c[1] / (double)(c[4] ? c[4] : 1), c[4], c[3],
                          c[8], c[9], c[10], c[11], c[12], c[13], c[14], c[15]);
             std::fprintf(stderr, "[pcp icp dbg] fallback: settled by the 3x3x3 stage %llu, with a correspondence %llu\n",
                          c[5], c[6]);
             std::fprintf(stderr, "[pcp icp dbg] freeze model: chunks %llu skippable %llu (searched lanes in them %llu) "
                          "refrozen with slack>0 %llu\n", c[18], c[16], c[17], c[19]);
+            std::fprintf(stderr, "[pcp icp dbg] verify: settled %llu  searched: aged %llu  fallback-reset(D=0) %llu  "
+                         "d_win/D <.5 %llu <.75 %llu <1 %llu >=1 %llu | delta/D <.1 %llu <.25 %llu <.5 %llu >=.5 %llu\n",
+                         c[20], c[21], c[22], c[23], c[24], c[25], c[26], c[27], c[28], c[29], c[30]);
         }
     }
     return PCP_OK;
