@@ -23,6 +23,16 @@ torch.distributed.run from a parent that never touches the GPU):
 At N > 1 the line also carries the two other modes under "alt_modes" (--no-alt skips them).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode slab|sharded|weak] [--n 50000000]
+
+The other BASELINE.json configs print the same JSON contract with --config (one step = one
+pass of that config's hot path over one batch; every rank runs its own batch, so N > 1 is weak
+scaling with no collective):
+  --config C1   voxel_grid leaf 0.1 of a 105k-pt cloud + index + 1-NN of 100k queries
+  --config C2   1M-vs-1M brute-force kNN k=8 (fp32 MFMA ranking, certified fp64 re-rank)
+  --config C3   10M-pt street scene: VoxelGrid leaf 0.05, then the fp64 index of the centroids
+                and calculate_feature normals k=32
+  --config C5   radius r=0.2 + normals over the fp16 cell-relative index: 25M pts per GPU (one
+                eighth of the 200M-pt scene at its density)
 """
 import argparse
 import glob
@@ -59,6 +69,7 @@ def parse():
     ap.add_argument("--cpu-iters1", type=int, default=3, help="CPU baseline iterations on 1 thread")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-alt", action="store_true", help="N > 1: skip the alt_modes runs")
+    ap.add_argument("--config", choices=("C1", "C2", "C3", "C4", "C5"), default="C4")
     return ap.parse_args()
 
 
@@ -177,6 +188,10 @@ def main():
 
     from pointcloudprocess_amd import distributed as D
     from pointcloudprocess_amd import ops, synth
+
+    if args.config != "C4":
+        import bench_configs  # the other BASELINE.json configs (same JSON contract)
+        return bench_configs.main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -15,6 +15,8 @@
 #include <cmath>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "grid.hpp"
 #include "topk.hpp"
 #include "pca.hpp"
@@ -115,6 +117,273 @@ __global__ __launch_bounds__(kB) void k_knn(GridDesc g, const double4* pts, cons
         for (int r = kk; r < k; r++) {
             ri[r] = -1;
             if (od2) rd[r] = INFINITY;
+        }
+    }
+}
+
+// ---- the far pass, wave-cooperative: one query per wave.  The deferred queries are the few
+// whose k-th neighbour lies beyond the near pass's cell rings -- isolated points, where one lane
+// walking rings of bricks alone took milliseconds.  Here the cells of each Chebyshev ring (then
+// the bricks of each brick ring) are dealt round-robin over the 64 lanes; every lane keeps its
+// own exact top-k of what it scanned, pruned by min(own k-th, the wave's shared bound), where
+// the shared bound -- the minimum over lanes of their k-th -- is an upper bound on the global
+// k-th (a superset has a smaller k-th), refreshed at each ring.  Every point within the final
+// global k-th distance was scanned by some lane, so merging the lanes' lists (k rounds of a
+// wave-wide lexicographic argmin) gives the exact FLANN (d2, j) order.
+template <int K>
+struct CoopVisitor {
+    const double4* pts;
+    double qx, qy, qz;
+    double shared = INFINITY;  // wave-uniform
+    TopK<K> top;
+    __device__ double bound() const { return fmin(top.kth(), shared) * (1.0 + 1e-12); }
+    __device__ double ubound() const { return shared * (1.0 + 1e-12); }
+    __device__ void visit(uint32_t s, uint32_t e) {
+        for (uint32_t t = s; t < e; t++) {
+            const double4 p = pts[t];
+            top.push(l2_simple(qx, qy, qz, p), (int)p.w);
+        }
+    }
+};
+// the exact k-th (d2, j) of the union of the lanes' lists (wave-uniform; every lane calls):
+// k rounds of a wave-wide lexicographic argmin on a copy of the lists
+template <int K>
+__device__ double global_kth(const TopK<K>& top, int kk, int lane) {
+    TopK<K> c = top;
+    c.normalize(kk);
+    double kth = INFINITY;
+    for (int r = 0; r < kk; r++) {
+        double bd = c.best_d();
+        int bj = c.best_j(), bl = lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(bd, o, 64);
+            const int oj = __shfl_xor(bj, o, 64), ol = __shfl_xor(bl, o, 64);
+            const bool take = lex_less(od, oj, bd, bj);
+            bd = take ? od : bd;
+            bj = take ? oj : bj;
+            bl = take ? ol : bl;
+        }
+        if (bj == INT_MAX) return INFINITY;  // fewer than kk points scanned
+        if (lane == bl) c.pop_best();
+        kth = bd;
+    }
+    return kth;
+}
+
+template <int K>
+__device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int lane, int kk) {
+    const double fx = cell_f<double>(g, v.qx, 0), fy = cell_f<double>(g, v.qy, 1), fz = cell_f<double>(g, v.qz, 2);
+    const int cx = (int)floor(fx), cy = (int)floor(fy), cz = (int)floor(fz);
+    const double lx = fx - cx, ly = fy - cy, lz = fz - cz;
+    const double h2 = g.h * g.h;
+    const double dmin = fmin(fmin(fmin(lx, 1 - lx), fmin(ly, 1 - ly)), fmin(lz, 1 - lz));
+    int far = 0;
+    far = max(far, max(cx - (g.n[0] - 1), -cx));
+    far = max(far, max(cy - (g.n[1] - 1), -cy));
+    far = max(far, max(cz - (g.n[2] - 1), -cz));
+    const int rmax = far + max(g.n[0], max(g.n[1], g.n[2]));
+    const int smax = min(rmax, kCellRings);
+    uint32_t t = 0;  // the wave's cell / brick counter: item t belongs to lane t % 64
+    for (int s = 0; s <= smax + 1; s++) {
+        if (s > 0) {
+            v.shared = global_kth<K>(v.top, kk, lane);
+            const double rmin = (double)(s - 1) + dmin - mc;
+            if (rmin > 0 && rmin * rmin * h2 > v.ubound()) return;
+        }
+        if (s > smax) break;
+        const int z0 = max(cz - s, 0), z1 = min(cz + s, g.n[2] - 1);
+        const int y0 = max(cy - s, 0), y1 = min(cy + s, g.n[1] - 1);
+        const int x0 = max(cx - s, 0), x1 = min(cx + s, g.n[0] - 1);
+        if (z0 > z1 || y0 > y1 || x0 > x1) continue;
+        for (int z = z0; z <= z1; z++) {
+            const bool zface = (z == cz - s) || (z == cz + s);
+            const double gz2 = sq_gap(axis_gap<double>(z, cz, lz), mc);
+            if (gz2 * h2 > v.ubound()) continue;
+            for (int y = y0; y <= y1; y++) {
+                const bool yface = zface || (y == cy - s) || (y == cy + s);
+                const double gyz2 = gz2 + sq_gap(axis_gap<double>(y, cy, ly), mc);
+                if (gyz2 * h2 > v.ubound()) continue;
+                const int step = yface ? 1 : 2 * s;
+                for (int x = yface ? x0 : cx - s; x <= x1; x += (step > 0 ? step : 1)) {
+                    if (x < x0) continue;
+                    if ((t++ & 63u) != (uint32_t)lane) continue;
+                    if ((gyz2 + sq_gap(axis_gap<double>(x, cx, lx), mc)) * h2 > v.bound()) continue;
+                    uint32_t st, en;
+                    if (cell_range(g, x, y, z, st, en)) v.visit(st, en);
+                }
+            }
+        }
+    }
+    if (rmax <= kCellRings) return;
+    // bricks of 4x4x4 cells, rings outward, the cells phase 1 covered skipped
+    const int bx = cx >> 2, by = cy >> 2, bz = cz >> 2;
+    const double ox = fx - 4 * bx, oy = fy - 4 * by, oz = fz - 4 * bz;
+    const double bdmin = fmin(fmin(fmin(ox, 4 - ox), fmin(oy, 4 - oy)), fmin(oz, 4 - oz));
+    int farb = 0;
+    farb = max(farb, max(bx - (g.nb[0] - 1), -bx));
+    farb = max(farb, max(by - (g.nb[1] - 1), -by));
+    farb = max(farb, max(bz - (g.nb[2] - 1), -bz));
+    const int sbmax = farb + max(g.nb[0], max(g.nb[1], g.nb[2]));
+    // rings closer than `farb` lie wholly outside the grid (a query far away from it)
+    for (int sb = farb; sb <= sbmax; sb++) {
+        v.shared = global_kth<K>(v.top, kk, lane);
+        if (sb > 0) {
+            const double rmin = (double)(4 * (sb - 1)) + bdmin - mc;
+            if (rmin > 0 && rmin * rmin * h2 > v.ubound()) return;
+        }
+        // the shell's bricks inside the grid: two z-faces, two y-faces (z strictly inside), two
+        // x-faces (y and z strictly inside), each a rectangle clipped to the grid; brick t of the
+        // shell goes to lane t % 64
+        const int X0 = max(bx - sb, 0), X1 = min(bx + sb, g.nb[0] - 1);
+        const int Y0 = max(by - sb, 0), Y1 = min(by + sb, g.nb[1] - 1);
+        const int Z0 = max(bz - sb, 0), Z1 = min(bz + sb, g.nb[2] - 1);
+        if (X0 > X1 || Y0 > Y1 || Z0 > Z1) continue;
+        const int Yi0 = max(by - sb + 1, 0), Yi1 = min(by + sb - 1, g.nb[1] - 1);
+        const int Zi0 = max(bz - sb + 1, 0), Zi1 = min(bz + sb - 1, g.nb[2] - 1);
+        int64_t area[6];
+        int fixc[6];
+        const int nx = X1 - X0 + 1, ny = Y1 - Y0 + 1, nyi = max(Yi1 - Yi0 + 1, 0), nzi = max(Zi1 - Zi0 + 1, 0);
+        for (int f = 0; f < 6; f++) {
+            const int sgn = (f & 1) ? 1 : -1;
+            if (f < 2) {  // z = bz -+ sb
+                fixc[f] = bz + sgn * sb;
+                area[f] = (fixc[f] >= 0 && fixc[f] < g.nb[2] && (sb > 0 || f == 0)) ? (int64_t)nx * ny : 0;
+            } else if (f < 4) {  // y = by -+ sb, z inside
+                fixc[f] = by + sgn * sb;
+                area[f] = (sb > 0 && fixc[f] >= 0 && fixc[f] < g.nb[1]) ? (int64_t)nx * nzi : 0;
+            } else {  // x = bx -+ sb, y and z inside
+                fixc[f] = bx + sgn * sb;
+                area[f] = (sb > 0 && fixc[f] >= 0 && fixc[f] < g.nb[0]) ? (int64_t)nyi * nzi : 0;
+            }
+        }
+        const int64_t total = area[0] + area[1] + area[2] + area[3] + area[4] + area[5];
+        for (int64_t t = lane; t < total; t += 64) {
+            int f = 0;
+            int64_t r = t;
+            while (r >= area[f]) { r -= area[f]; f++; }
+            int xb, yb, zb;
+            if (f < 2) {
+                xb = X0 + (int)(r % nx); yb = Y0 + (int)(r / nx); zb = fixc[f];
+            } else if (f < 4) {
+                xb = X0 + (int)(r % nx); zb = Zi0 + (int)(r / nx); yb = fixc[f];
+            } else {
+                yb = Yi0 + (int)(r % nyi); zb = Zi0 + (int)(r / nyi); xb = fixc[f];
+            }
+            const double gz = zb < bz ? (oz + 4.0 * (bz - zb - 1)) : (zb > bz ? (4.0 - oz + 4.0 * (zb - bz - 1)) : 0.0);
+            const double gy = yb < by ? (oy + 4.0 * (by - yb - 1)) : (yb > by ? (4.0 - oy + 4.0 * (yb - by - 1)) : 0.0);
+            const double gx = xb < bx ? (ox + 4.0 * (bx - xb - 1)) : (xb > bx ? (4.0 - ox + 4.0 * (xb - bx - 1)) : 0.0);
+            if ((sq_gap(gz, mc) + sq_gap(gy, mc) + sq_gap(gx, mc)) * h2 > v.bound()) continue;
+            if (g.brick[((int64_t)zb * g.nb[1] + yb) * g.nb[0] + xb] < 0) continue;  // empty brick
+            for (int z = 4 * zb; z < min(4 * zb + 4, g.n[2]); z++) {
+                const double cz2 = sq_gap(axis_gap<double>(z, cz, lz), mc);
+                const bool zin = abs(z - cz) <= kCellRings;
+                for (int y = 4 * yb; y < min(4 * yb + 4, g.n[1]); y++) {
+                    const double cyz2 = cz2 + sq_gap(axis_gap<double>(y, cy, ly), mc);
+                    if (cyz2 * h2 > v.bound()) continue;
+                    const bool yzin = zin && abs(y - cy) <= kCellRings;
+                    for (int x = 4 * xb; x < min(4 * xb + 4, g.n[0]); x++) {
+                        if (yzin && abs(x - cx) <= kCellRings) continue;
+                        if ((cyz2 + sq_gap(axis_gap<double>(x, cx, lx), mc)) * h2 > v.bound()) continue;
+                        uint32_t st, en;
+                        if (cell_range(g, x, y, z, st, en)) v.visit(st, en);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// merge the lanes' top-k lists: round r leaves the r-th (d2, j) of the query in lane r's
+// (md, mj) (r < kk); every lane must call it
+template <int K>
+__device__ __forceinline__ void coop_merge(CoopVisitor<K>& v, int kk, int lane, double& md, int& mj) {
+    v.top.normalize(kk);
+    md = INFINITY;
+    mj = INT_MAX;
+    for (int r = 0; r < kk; r++) {
+        double bd = v.top.best_d();
+        int bj = v.top.best_j(), bl = lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(bd, o, 64);
+            const int oj = __shfl_xor(bj, o, 64), ol = __shfl_xor(bl, o, 64);
+            const bool take = lex_less(od, oj, bd, bj);
+            bd = take ? od : bd;
+            bj = take ? oj : bj;
+            bl = take ? ol : bl;
+        }
+        if (lane == bl && bj != INT_MAX) v.top.pop_best();
+        if (lane == r) { md = bd; mj = bj; }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kB) void k_knn_coop(GridDesc g, const double4* pts, const int32_t* mapping, int identity,
+                                                 const double* q, size_t qstride, int k, int kk, double mc,
+                                                 int32_t* oidx, double* od2, FarList far) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64), cnt = *far.count;
+    for (int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6); w < cnt; w += nwaves) {
+        const int64_t i = far.list[w];
+        const double* qp = qptr(q, qstride, i);
+        CoopVisitor<K> v;
+        v.pts = pts;
+        v.qx = qp[0]; v.qy = qp[1]; v.qz = qp[2];
+        v.top.init(kk);
+        coop_search<K>(g, mc, v, lane, kk);
+        double md;
+        int mj;
+        coop_merge<K>(v, kk, lane, md, mj);
+        if (lane < k) {
+            const bool ok = lane < kk && mj != INT_MAX;
+            oidx[i * k + lane] = ok ? (identity ? mj : mapping[mj]) : -1;
+            if (od2) od2[i * k + lane] = ok ? md : INFINITY;
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kB) void k_normals_coop(GridDesc g, const double4* pts, const int32_t* mapping,
+                                                     int identity, const int32_t* pos_of_j, int kk, double mc,
+                                                     pcp_plane* out, int64_t n_out, FarList far) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64), cnt = *far.count;
+    for (int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6); w < cnt; w += nwaves) {
+        const int64_t s = far.list[w];
+        const double4 qp = pts[s];
+        CoopVisitor<K> v;
+        v.pts = pts;
+        v.qx = qp.x; v.qy = qp.y; v.qz = qp.z;
+        v.top.init(kk);
+        coop_search<K>(g, mc, v, lane, kk);
+        double md;
+        int mj;
+        coop_merge<K>(v, kk, lane, md, mj);
+        const int jq = (int)qp.w;
+        const int64_t oi = identity ? jq : mapping[jq];
+        if (oi >= n_out) continue;
+        // mean and X X^T, sequential in kNN order (calculate_feature.cpp:131-164), wave-uniform
+        double xa = 0, ya = 0, za = 0;
+        for (int r = 0; r < kk; r++) {
+            const int j = __shfl(mj, r, 64);
+            const double4 p = pts[pos_of_j[j]];
+            xa += p.x; ya += p.y; za += p.z;
+        }
+        xa /= kk; ya /= kk; za /= kk;
+        double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+        for (int r = 0; r < kk; r++) {
+            const int j = __shfl(mj, r, 64);
+            const double4 p = pts[pos_of_j[j]];
+            const double x0 = p.x - xa, x1 = p.y - ya, x2 = p.z - za;
+            c00 += x0 * x0; c01 += x0 * x1; c02 += x0 * x2;
+            c11 += x1 * x1; c12 += x1 * x2; c22 += x2 * x2;
+        }
+        if (lane == 0) {
+            const double C[9] = {c00, c01, c02, c01, c11, c12, c02, c12, c22};
+            pcp_plane pl;
+            plane_from_cov(C, xa, ya, za, pl);
+            out[oi] = pl;
         }
     }
 }
@@ -302,13 +571,16 @@ __global__ void k_plane_default(pcp_plane* out, int64_t n) {
 }
 
 // queries = the indexed points themselves, walked in the index's spatial order
+// `in` (near pass only): the sorted positions to process (the tiled kernel's uncertified
+// queries), or every point when in.list is null
 template <int K, bool FAR>
 __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, const int32_t* mapping, int identity,
                                                 const int32_t* pos_of_j, int64_t n, int kk, double mc,
-                                                pcp_plane* out, int64_t n_out, FarList far) {
-    const int64_t nw = work_count<FAR>(far, n);
+                                                pcp_plane* out, int64_t n_out, FarList far,
+                                                FarList in = FarList{nullptr, nullptr}) {
+    const int64_t nw = (!FAR && in.list) ? (int64_t)*in.count : work_count<FAR>(far, n);
     for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t s = work_item<FAR>(far, w);
+        const int64_t s = (!FAR && in.list) ? (int64_t)in.list[w] : work_item<FAR>(far, w);
         const double4 qp = pts[s];
         KnnVisitor<K> v;
         v.pts = pts;
@@ -339,6 +611,290 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
         pcp_plane pl;
         plane_from_cov(C, xa, ya, za, pl);
         out[oi] = pl;
+    }
+}
+
+// F1 over kNN, tiled (dense grids, k <= 32): one wave per 64 consecutive sorted points.
+// The wave copies the union of its queries' neighbourhoods -- the box of their cells grown by
+// R cells, one contiguous point run per (y, z) row -- into LDS as fp32 coordinates relative to
+// the box corner plus the sorted position.  Every lane then scans the whole list (uniform trip
+// count, broadcast LDS reads, no divergence) keeping its M = K + 4 smallest packed keys
+// (bits(fp32 d2) & ~1023 | list index) and the (M+1)-th as a bound with a v_med3_u32 network
+// (M + 1 VALU ops per candidate instead of the fp64 register top-k's divergent shifts).  The
+// kept candidates are re-ranked by the exact FLANN fp64 (d2, j) and sorted; the lane's result
+// is certified when its k-th exact d2 lies strictly below both the bound on every uncached
+// list point (the (M+1)-th key less the fp32 error) and the squared distance to the box faces
+// (points outside the box).  Uncertified lanes go to the exact two-level search (the far pass
+// of k_normals), so the output is that of the exact path bit for bit.
+constexpr int kTileCap = 2048;   // union points per wave (11-bit list index)
+constexpr int kTileRows = 256;   // (y, z) rows per wave
+constexpr int kTileQ = 16383;    // 14-bit fixed-point coordinates: squared distances fit in int32
+constexpr int kTileExt = 96;     // box extent (cells) cap: keeps the fixed-point step fine
+__device__ __forceinline__ uint32_t umed3_(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// squared distance of two packed 14-bit points: (x | y << 16, z) -- v_pk_sub_i16 + v_dot2_i32_i16
+__device__ __forceinline__ uint32_t qd2(uint32_t qxy, int qz, uint32_t pxy, int pz) {
+    uint32_t dxy;
+    asm("v_pk_sub_i16 %0, %1, %2" : "=v"(dxy) : "v"(qxy), "v"(pxy));
+    const int dz = qz - pz;
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %1, %2" : "=v"(r) : "v"(dxy), "v"(dz * dz));
+    return (uint32_t)r;
+}
+__device__ __forceinline__ int wmin_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wmax_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int quant14(double v, double inv) {
+    const double t = rint(v * inv);
+    return (int)(t < 0.0 ? 0.0 : (t > (double)kTileQ ? (double)kTileQ : t));
+}
+
+// the union box of the lanes with `in` set, grown by R cells; its rows' point runs are listed
+// (start and exclusive prefix in s_rs / s_rb) when `write` is set
+struct TileBox {
+    int x0, x1, y0, y1, z0, z1, ny, nrow;
+    uint32_t total;  // points in the box (0xffffffff: too many rows / too wide)
+};
+__device__ __forceinline__ TileBox tile_box(const GridDesc& g, int cx, int cy, int cz, bool in, int R, int lane,
+                                            uint32_t* s_rs, uint32_t* s_rb, bool write) {
+    TileBox b;
+    b.x0 = max(wmin_i(in ? cx : INT_MAX) - R, 0), b.x1 = min(wmax_i(in ? cx : INT_MIN) + R, g.n[0] - 1);
+    b.y0 = max(wmin_i(in ? cy : INT_MAX) - R, 0), b.y1 = min(wmax_i(in ? cy : INT_MIN) + R, g.n[1] - 1);
+    b.z0 = max(wmin_i(in ? cz : INT_MAX) - R, 0), b.z1 = min(wmax_i(in ? cz : INT_MIN) + R, g.n[2] - 1);
+    b.ny = b.y1 - b.y0 + 1;
+    b.nrow = b.ny * (b.z1 - b.z0 + 1);
+    b.total = 0xffffffffu;
+    const int ext = max(max(b.x1 - b.x0, b.y1 - b.y0), b.z1 - b.z0) + 1;
+    if (b.nrow > kTileRows || ext > kTileExt) return b;
+    uint32_t carry = 0;
+    for (int r0 = 0; r0 < b.nrow; r0 += 64) {
+        const int r = r0 + lane;
+        uint32_t st = 0, cnt = 0;
+        if (r < b.nrow) {
+            const int y = b.y0 + r % b.ny, z = b.z0 + r / b.ny;
+            st = g.cstart[dense_id(g, b.x0, y, z)];
+            cnt = g.cstart[dense_id(g, b.x1, y, z) + 1] - st;
+        }
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        if (write && r < b.nrow) {
+            s_rs[r] = st;
+            s_rb[r] = carry + inc - cnt;
+        }
+        carry += __shfl(inc, 63, 64);
+    }
+    if (write && lane == 0) s_rb[b.nrow] = carry;
+    b.total = carry;
+    return b;
+}
+
+// query order of the tiled kernel: sorted positions by 8x8x8-cell brick (stable, so row-major
+// inside a brick), so that a wave's 64 queries are neighbours in all three axes -- in the index's
+// row-major order the points of one x-row of a facade are metres apart
+constexpr int kTileBrick = 3;  // log2 brick edge (cells)
+__global__ void k_brick_keys(GridDesc g, const double4* pts, int64_t n, uint32_t* key, uint32_t* pos) {
+    const int nbx = (g.n[0] + 7) >> kTileBrick, nby = (g.n[1] + 7) >> kTileBrick;
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+        const double4 p = pts[s];
+        const int cx = clampi(cell_i<double>(g, p.x, 0), 0, g.n[0] - 1) >> kTileBrick;
+        const int cy = clampi(cell_i<double>(g, p.y, 1), 0, g.n[1] - 1) >> kTileBrick;
+        const int cz = clampi(cell_i<double>(g, p.z, 2), 0, g.n[2] - 1) >> kTileBrick;
+        key[s] = (uint32_t)(((int64_t)cz * nby + cy) * nbx + cx);
+        pos[s] = (uint32_t)s;
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* pts, const int32_t* mapping,
+                                                     int identity, int64_t n, int kk, int R, double mc,
+                                                     pcp_plane* out, int64_t n_out, FarList far,
+                                                     unsigned long long* stats, const uint32_t* order) {
+    constexpr int M = K + 4;
+    constexpr uint32_t kMax = 0xffffffffu;
+    __shared__ uint2 s_u[kTileCap];
+    __shared__ uint32_t s_rs[kTileRows], s_rb[kTileRows + 1];
+    const int lane = threadIdx.x;
+    for (int64_t c = blockIdx.x; c * 64 < n; c += gridDim.x) {
+        const bool valid = c * 64 + lane < n;
+        const int64_t s = order[valid ? c * 64 + lane : c * 64];  // a sorted position
+        const double4 q = pts[s];
+        const int cx = cell_i<double>(g, q.x, 0), cy = cell_i<double>(g, q.y, 1), cz = cell_i<double>(g, q.z, 2);
+        // split the wave into G groups (1, 2 or 4) so that every group's box fits the LDS list
+        int G = 1;
+        bool fits = false;
+        for (; G <= 4; G *= 2) {
+            fits = true;
+            for (int gi = 0; gi < G && fits; gi++) {
+                const TileBox b = tile_box(g, cx, cy, cz, lane / (64 / G) == gi, R, lane, s_rs, s_rb, false);
+                fits = b.total <= (uint32_t)kTileCap;
+            }
+            if (fits) break;
+        }
+        if (!fits) {  // the whole wave takes the exact search
+            if (valid) defer(far, s);
+            if (stats && lane == 0) atomicAdd(stats + 1, 64ull);
+            continue;
+        }
+        if (stats && lane == 0 && G > 1) atomicAdd(stats + 3, (unsigned long long)G);
+        for (int gi = 0; gi < G; gi++) {
+            const bool mine = lane / (64 / G) == gi;
+            wave_lds_fence();  // the previous group's readers are done with the lists
+            const TileBox b = tile_box(g, cx, cy, cz, mine, R, lane, s_rs, s_rb, true);
+            const uint32_t total = b.total;
+            wave_lds_fence();
+            // 14-bit fixed point relative to the box corner, one step for all three axes
+            const double ox = g.o[0] + (double)b.x0 * g.h, oy = g.o[1] + (double)b.y0 * g.h,
+                         oz = g.o[2] + (double)b.z0 * g.h;
+            const int ext = max(max(b.x1 - b.x0, b.y1 - b.y0), b.z1 - b.z0) + 1;
+            const double step = (double)ext * g.h / (double)kTileQ, inv = 1.0 / step;
+            const int nrow = b.nrow;
+            auto row_of = [&](uint32_t e) {
+                int r = 0;
+#pragma unroll
+                for (int stp = kTileRows / 2; stp > 0; stp >>= 1)
+                    r = (r + stp < nrow && s_rb[r + stp] <= e) ? r + stp : r;
+                return r;
+            };
+            for (uint32_t e = lane; e < total; e += 64) {
+                const int r = row_of(e);
+                const double4 p = pts[s_rs[r] + (e - s_rb[r])];
+                s_u[e] = make_uint2((uint32_t)quant14(p.x - ox, inv) | ((uint32_t)quant14(p.y - oy, inv) << 16),
+                                    (uint32_t)quant14(p.z - oz, inv));
+            }
+            wave_lds_fence();
+            const uint32_t qxy = (uint32_t)quant14(q.x - ox, inv) | ((uint32_t)quant14(q.y - oy, inv) << 16);
+            const int qz = quant14(q.z - oz, inv);
+            uint32_t t[M + 1];
+#pragma unroll
+            for (int i = 0; i <= M; i++) t[i] = kMax;
+            // keys: the float bits of the integer d2 (relative precision 2^-12 after the index
+            // bits, whatever the step) | list index
+            auto insert = [&](uint32_t d, uint32_t e) {
+                const uint32_t x = (__float_as_uint((float)d) & ~(uint32_t)(kTileCap - 1)) | e;
+#pragma unroll
+                for (int i = M; i >= 1; i--) t[i] = umed3_(t[i - 1], t[i], x);
+                t[0] = min(t[0], x);
+            };
+            uint32_t e = 0;
+            for (; e + 4 <= total; e += 4) {
+                uint2 p[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) p[u] = s_u[e + u];
+#pragma unroll
+                for (int u = 0; u < 4; u++) insert(qd2(qxy, qz, p[u].x, (int)p[u].y), e + u);
+            }
+            for (; e < total; e++) {
+                const uint2 pp = s_u[e];
+                insert(qd2(qxy, qz, pp.x, (int)pp.y), e);
+            }
+            if (!mine) continue;  // (no wave-wide operation follows)
+            // exact FLANN re-rank of the kept candidates
+            double D[M];
+            uint32_t P[M];
+#pragma unroll
+            for (int i = 0; i < M; i++) {
+                const bool has = t[i] != kMax;
+                const uint32_t ei = t[i] & (uint32_t)(kTileCap - 1);
+                const int r = row_of(has ? ei : 0u);
+                P[i] = has ? s_rs[r] + (ei - s_rb[r]) : 0u;
+                D[i] = has ? l2_simple(q.x, q.y, q.z, pts[P[i]]) : INFINITY;
+            }
+            // every list point not kept: its quantised distance is >= sqrt(float(t[M] & ~2047))
+            // steps (the int -> float rounding is covered by the 2^-20), and quantisation moves
+            // each coordinate of both points by <= step / 2
+            double lb = INFINITY;
+            if (t[M] != kMax) {
+                const double v =
+                    (sqrt((double)__uint_as_float(t[M] & ~(uint32_t)(kTileCap - 1))) * (1.0 - 0x1p-20) -
+                     1.7320508075688772 - 1e-3) * step;
+                lb = v > 0.0 ? v * v * (1.0 - 1e-12) : 0.0;
+            }
+            // sort (d2, j) ascending: odd-even transposition rounds until no swap (the approximate
+            // order is almost exact, so this ends after one or two rounds)
+            bool any = true;
+            while (any) {
+                any = false;
+#pragma unroll
+                for (int par = 0; par < 2; par++) {
+#pragma unroll
+                    for (int i = par; i + 1 < M; i += 2) {
+                        bool gt = D[i] > D[i + 1];
+                        if (D[i] == D[i + 1] && D[i] != INFINITY)
+                            gt = (int)pts[P[i]].w > (int)pts[P[i + 1]].w;
+                        const double dl = gt ? D[i + 1] : D[i], dh = gt ? D[i] : D[i + 1];
+                        const uint32_t pl = gt ? P[i + 1] : P[i], ph = gt ? P[i] : P[i + 1];
+                        D[i] = dl; D[i + 1] = dh; P[i] = pl; P[i + 1] = ph;
+                        any = any || gt;
+                    }
+                }
+            }
+            // the box faces that have grid cells beyond them bound every point outside the list
+            double bd = INFINITY;
+            if (b.x0 > 0) bd = fmin(bd, q.x - ox);
+            if (b.x1 < g.n[0] - 1) bd = fmin(bd, ox + (double)(b.x1 - b.x0 + 1) * g.h - q.x);
+            if (b.y0 > 0) bd = fmin(bd, q.y - oy);
+            if (b.y1 < g.n[1] - 1) bd = fmin(bd, oy + (double)(b.y1 - b.y0 + 1) * g.h - q.y);
+            if (b.z0 > 0) bd = fmin(bd, q.z - oz);
+            if (b.z1 < g.n[2] - 1) bd = fmin(bd, oz + (double)(b.z1 - b.z0 + 1) * g.h - q.z);
+            bd -= mc * g.h + 1e-12 * (fabs(q.x) + fabs(q.y) + fabs(q.z) + 1.0);
+            const double b2 = bd > 0.0 ? bd * bd * (1.0 - 1e-12) : (bd == INFINITY ? INFINITY : 0.0);
+            double dk = INFINITY;
+#pragma unroll
+            for (int i = 0; i < M; i++)
+                if (i == kk - 1) dk = D[i];
+            if (!valid) continue;
+            if (!(dk < lb && dk < b2)) {
+                defer(far, s);
+                if (stats) atomicAdd(stats + (dk < lb ? 2 : 0), 1ull);
+                continue;
+            }
+            const int jq = (int)q.w;
+            const int64_t oi = identity ? jq : mapping[jq];
+            if (oi >= n_out) continue;
+            // mean, sequential in kNN order (calculate_feature.cpp:131-142)
+            double xa = 0, ya = 0, za = 0;
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+                if (i < kk) {
+                    const double4 p = pts[P[i]];
+                    xa += p.x; ya += p.y; za += p.z;
+                }
+            }
+            xa /= kk; ya /= kk; za /= kk;
+            double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+                if (i < kk) {
+                    const double4 p = pts[P[i]];
+                    const double a0 = p.x - xa, a1 = p.y - ya, a2 = p.z - za;
+                    c00 += a0 * a0; c01 += a0 * a1; c02 += a0 * a2;
+                    c11 += a1 * a1; c12 += a1 * a2; c22 += a2 * a2;
+                }
+            }
+            const double C[9] = {c00, c01, c02, c01, c11, c12, c02, c12, c22};
+            pcp_plane pl;
+            plane_from_cov(C, xa, ya, za, pl);
+            out[oi] = pl;
+        }
     }
 }
 
@@ -561,8 +1117,8 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t qstride, 
 #define LAUNCH_KNN(KV)                                                                                          \
     hipLaunchKernelGGL((k_knn<KV, false>), dim3(blocks_for(nq)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,  \
                        ix->identity, q, qstride, nq, k, kk, mc, oidx, od2, fb.f);                                  \
-    hipLaunchKernelGGL((k_knn<KV, true>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,        \
-                       ix->identity, q, qstride, nq, k, kk, mc, oidx, od2, fb.f)
+    hipLaunchKernelGGL((k_knn_coop<KV>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,         \
+                       ix->identity, q, qstride, k, kk, mc, oidx, od2, fb.f)
     switch (K) {
         case 1: LAUNCH_KNN(1); break;
         case 4: LAUNCH_KNN(4); break;
@@ -656,11 +1212,74 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
     const double4* pts = (const double4*)ix->pts;
     FarBuf fb;
     PCP_TRY(fb.alloc(ctx, ix->n));
+    const char* tenv = getenv("PCP_NORMALS_TILE");
+    const int tile_R = tenv ? atoi(tenv) : (kk <= 8 ? 1 : 2);  // 0 disables the tiled kernel
+    if (ix->g.dense && tile_R > 0) {
+        unsigned long long* st = nullptr;
+        if (getenv("PCP_KNN_DEBUG")) {
+            PCP_TRY(dmalloc(ctx, &st, 4));
+            PCP_HIP(ctx, hipMemsetAsync(st, 0, 4 * sizeof(unsigned long long), ctx->stream));
+        }
+        const unsigned nbt = (unsigned)std::min<int64_t>((ix->n + 63) / 64, 1 << 20);
+        // brick order of the queries: (brick key, sorted position) radix-sorted
+        uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *order = nullptr;
+        void* tmp = nullptr;
+        size_t tb = 0;
+        struct Free {
+            pcp_ctx* c;
+            uint32_t **a, **b, **d, **e;
+            void** t;
+            ~Free() { dfree(c, *a); dfree(c, *b); dfree(c, *d); dfree(c, *e); dfree(c, (char*)*t); }
+        } fr{ctx, &k0, &k1, &v0, &order, &tmp};
+        PCP_TRY(dmalloc(ctx, &k0, ix->n));
+        PCP_TRY(dmalloc(ctx, &k1, ix->n));
+        PCP_TRY(dmalloc(ctx, &v0, ix->n));
+        PCP_TRY(dmalloc(ctx, &order, ix->n));
+        hipLaunchKernelGGL(k_brick_keys, dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->n, k0, v0);
+        const int64_t nbr = (int64_t)((ix->g.n[0] + 7) >> kTileBrick) * ((ix->g.n[1] + 7) >> kTileBrick) *
+                            ((ix->g.n[2] + 7) >> kTileBrick);
+        unsigned bits = 1;
+        while (bits < 32 && ((int64_t)1 << bits) < nbr) bits++;
+        PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, order, (size_t)ix->n, 0u, bits, ctx->stream));
+        PCP_TRY(dmalloc(ctx, (char**)&tmp, tb));
+        PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tb, k0, k1, v0, order, (size_t)ix->n, 0u, bits, ctx->stream));
+        FarBuf fb2;  // the near pass's own deferred queries
+        PCP_TRY(fb2.alloc(ctx, ix->n));
+#define LAUNCH_TILE(KV)                                                                                          \
+        hipLaunchKernelGGL((k_normals_tile<KV>), dim3(nbt), dim3(64), 0, ctx->stream, ix->g, pts, ix->mapping,      \
+                           ix->identity, ix->n, kk, tile_R, mc, out, n_out, fb.f, st, order);                     \
+        hipLaunchKernelGGL((k_normals<KV, false>), dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts,   \
+                           ix->mapping, ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb2.f, fb.f);       \
+        hipLaunchKernelGGL((k_normals_coop<KV>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts,            \
+                           ix->mapping, ix->identity, ix->pos_of_j, kk, mc, out, n_out, fb2.f)
+        switch (K) {
+            case 1: case 4: LAUNCH_TILE(4); break;
+            case 8: LAUNCH_TILE(8); break;
+            case 16: LAUNCH_TILE(16); break;
+            default: LAUNCH_TILE(32); break;
+        }
+#undef LAUNCH_TILE
+        PCP_LAUNCH_CHECK(ctx);
+        if (st) {
+            unsigned long long h[4] = {0, 0, 0, 0};
+            unsigned c = 0;
+            hipMemcpy(h, st, sizeof(h), hipMemcpyDeviceToHost);
+            hipMemcpy(&c, fb.f.count, 4, hipMemcpyDeviceToHost);
+            unsigned c2 = 0;
+            hipMemcpy(&c2, fb2.f.count, 4, hipMemcpyDeviceToHost);
+            fprintf(stderr, "pcp_normals_knn tile: the near pass deferred %u to the brick search\n", c2);
+            fprintf(stderr, "pcp_normals_knn tile: k=%d R=%d n=%lld uncertified lanes: by the list bound %llu, by the "
+                    "box %llu; oversized-wave lanes: rows %llu, points %llu; deferred %u\n", k, tile_R,
+                    (long long)ix->n, h[0], h[2], h[1], h[3], c);
+            dfree(ctx, st);
+        }
+        return PCP_OK;
+    }
 #define LAUNCH_NRM(KV)                                                                                              \
     hipLaunchKernelGGL((k_normals<KV, false>), dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts,          \
                        ix->mapping, ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb.f);                      \
-    hipLaunchKernelGGL((k_normals<KV, true>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,      \
-                       ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb.f)
+    hipLaunchKernelGGL((k_normals_coop<KV>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts, ix->mapping,       \
+                       ix->identity, ix->pos_of_j, kk, mc, out, n_out, fb.f)
     switch (K) {
         case 1: LAUNCH_NRM(1); break;
         case 4: LAUNCH_NRM(4); break;
