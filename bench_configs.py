@@ -91,7 +91,7 @@ def cfg_c1(ctx, args, rank, timer):
     base = rng.uniform(-10, 10, (100_000, 3)).astype(np.float32).astype(np.float64)
     pts = np.concatenate([base, base[rng.integers(0, len(base), 5000)]])
     cloud = np.zeros(len(pts), dtype=ops.POINT48)
-    cloud["x"], cloud["y"], cloud["z"], cloud["pad"] = pts[:, 0], pts[:, 1], pts[:, 2], 1.0
+    cloud["x"], cloud["y"], cloud["z"], cloud["w"] = pts[:, 0], pts[:, 1], pts[:, 2], 1.0
     cloud = ops.cloud_to_device(cloud, ctx.device)
     q = torch.from_numpy(np.random.default_rng(1002 + rank).uniform(-10, 10, (100_000, 3))).to(ctx.device)
     n = len(pts)
@@ -115,7 +115,7 @@ def cfg_c1(ctx, args, rank, timer):
         host = ops.cloud_to_host(cloud)
         qh = q.cpu().numpy()
         t0 = time.perf_counter()
-        vox = ora.voxel_filter(host, 0.1)
+        vox, _ = ora.voxel_filter(host, 0.1)
         vx = np.stack([vox["x"], vox["y"], vox["z"]], 1)
         ora.KdTree(vx).knn(qh, 1)
         dt = time.perf_counter() - t0
@@ -197,7 +197,7 @@ def cfg_c3(ctx, args, rank, timer):
         s = 1_000_000
         host = ops.cloud_to_host(cloud[:s])
         t0 = time.perf_counter()
-        vox = ora.voxel_filter(host, 0.05)
+        vox, _ = ora.voxel_filter(host, 0.05)
         tv = time.perf_counter() - t0
         vx = np.stack([vox["x"], vox["y"], vox["z"]], 1)
         t0 = time.perf_counter()
