@@ -311,6 +311,23 @@ int pcp_get_rot_icp(pcp_ctx* ctx, const void* src_aos48_dev, int64_t ns, int src
                     double mat_rot_host[16], float rmax, int iters, int do_scale,
                     double cell_size, float* err);
 
+/* ----------------------------------------------------------------------- I4: pose lines
+ * Host-only (no device work): n frames' poses as row-major 4x4 doubles, rots[16 * i].
+ *
+ * pcp_pose_interpolate: do_transform_interpolation (main_blend.cpp:934-980): frames
+ * [start, end] re-posed by the slerp-interpolated correction of
+ * rot[end] * rot[start]^-1 applied to rot[start].
+ * pcp_pose_lum_elch: PointCloudClosure::do_lum_elch (point_cloud_closure.cpp:194-233):
+ * rots[i] = E_i * rots[i] over [start, end], E_i the weight-(i-start)/(len-1) share of `loop`.
+ * pcp_pose_loop_closure: PointCloudClosure::do_loop_closure (point_cloud_closure.cpp:235-276):
+ * splice the optimised span opt (matched by stamp) into ori, spread the start jump over the
+ * `window` (400 in the reference) preceding frames, carry the end jump to every later frame.
+ * PCP_ERR_ARG where the reference returns false (stamp not found, span length mismatch). */
+int pcp_pose_interpolate(double* rots_host, int64_t n, int64_t start, int64_t end);
+int pcp_pose_lum_elch(double* rots_host, int64_t n, int64_t start, int64_t end, const double loop_host[16]);
+int pcp_pose_loop_closure(double* ori_host, const uint64_t* ori_stamps_host, int64_t n_ori, const double* opt_host,
+                          const uint64_t* opt_stamps_host, int64_t n_opt, int64_t window);
+
 #ifdef __cplusplus
 }
 #endif

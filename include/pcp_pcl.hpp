@@ -748,6 +748,57 @@ public:
     std::string _time_stamp_str;
 };
 
+// pose lines: the reference's Eigen composition restated in libpcp (pcp_pose_*, host-only)
+namespace detail {
+inline std::vector<double> pack_rots(const std::vector<CloudStampRot>& r) {
+    std::vector<double> a(16 * r.size());
+    for (size_t i = 0; i < r.size(); i++) std::memcpy(&a[16 * i], r[i]._rot.m, 16 * sizeof(double));
+    return a;
+}
+inline void unpack_rots(const std::vector<double>& a, std::vector<CloudStampRot>& r) {
+    for (size_t i = 0; i < r.size(); i++) std::memcpy(r[i]._rot.m, &a[16 * i], 16 * sizeof(double));
+}
+}  // namespace detail
+
+// do_transform_interpolation (main_blend.cpp:934-980)
+inline void do_transform_interpolation(std::vector<CloudStampRot>& line, int start_index, int end_index) {
+    std::vector<double> a = detail::pack_rots(line);
+    detail::check(pcp_pose_interpolate(a.data(), (int64_t)line.size(), start_index, end_index), nullptr,
+                  "do_transform_interpolation");
+    detail::unpack_rots(a, line);
+}
+
+class PointCloudClosure {  // point_cloud_closure.cpp:185-276 (the pose-line members)
+public:
+    static int get_index_from_rots(const std::vector<CloudStampRot>& rots, uint64_t stamp) {
+        for (size_t i = 0; i < rots.size(); i++)
+            if (rots[i]._stamp == stamp) return (int)i;
+        return -1;
+    }
+    template <class M>
+    static bool do_lum_elch(std::vector<CloudStampRot>& rots, int start_index, int end_index, const M& loop_transform) {
+        double L[16];
+        for (int r = 0; r < 4; r++)
+            for (int c = 0; c < 4; c++) L[4 * r + c] = loop_transform(r, c);
+        std::vector<double> a = detail::pack_rots(rots);
+        if (pcp_pose_lum_elch(a.data(), (int64_t)rots.size(), start_index, end_index, L) != PCP_OK) return false;
+        detail::unpack_rots(a, rots);
+        return true;
+    }
+    static bool do_loop_closure(std::vector<CloudStampRot>& ori_rots, const std::vector<CloudStampRot>& opt_rots) {
+        if (opt_rots.empty()) return false;
+        std::vector<double> a = detail::pack_rots(ori_rots), b = detail::pack_rots(opt_rots);
+        std::vector<uint64_t> sa(ori_rots.size()), sb(opt_rots.size());
+        for (size_t i = 0; i < ori_rots.size(); i++) sa[i] = ori_rots[i]._stamp;
+        for (size_t i = 0; i < opt_rots.size(); i++) sb[i] = opt_rots[i]._stamp;
+        if (pcp_pose_loop_closure(a.data(), sa.data(), (int64_t)sa.size(), b.data(), sb.data(), (int64_t)sb.size(),
+                                  400) != PCP_OK)
+            return false;  // "cannot find stamp in rots" / "rots count not equal"
+        detail::unpack_rots(a, ori_rots);
+        return true;
+    }
+};
+
 }  // namespace cloud_blend_double
 
 #endif  // PCP_PCL_HPP

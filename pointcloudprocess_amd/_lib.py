@@ -58,6 +58,9 @@ SIGNATURES = [
     ("pcp_centroid_concat_aos48", _i32, [_vp, _vp, _i64, _vp, _i64, _i32, _P(_f64), _P(_u32)]),
     ("pcp_transform_aos48", _i32, [_vp, _vp, _vp, _i64, _i32, _P(_f64)]),
     ("pcp_voxel_filter", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _i32, _vp, _P(_i64), _vp]),
+    ("pcp_pose_interpolate", _i32, [_vp, _i64, _i64, _i64]),
+    ("pcp_pose_lum_elch", _i32, [_vp, _i64, _i64, _i64, _vp]),
+    ("pcp_pose_loop_closure", _i32, [_vp, _vp, _i64, _vp, _vp, _i64, _i64]),
     ("pcp_remove_duplicate", _i32, [_vp, _vp, _i64, _i32, _f32, _vp, _P(_i64)]),
     ("pcp_normals_knn", _i32, [_vp, _vp, _i32, _vp, _i64]),
     ("pcp_icp_create", _i32, [_vp, _vp, _vp, _sz, _i64, _P(_vp)]),

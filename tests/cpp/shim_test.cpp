@@ -237,7 +237,31 @@ static void test_features_and_icp() {
     CHECK(PointCloudHelper::get_rot_icp(src, tmp, Ra, false, true) < 0, "do_affine -> err < 0");
 }
 
+static void test_pose_lines() {  // main_blend.cpp:934-980, point_cloud_closure.cpp:194-276
+    std::vector<CloudStampRot> line(12);
+    for (int i = 0; i < 12; i++) {
+        line[i]._stamp = 100 + i;
+        line[i]._rot = Mat4d::Identity();
+        line[i]._rot(0, 3) = 2.0 * i;
+    }
+    std::vector<CloudStampRot> ori = line;
+    Mat4d loop = Mat4d::Identity();
+    loop(0, 1) = -0.01; loop(1, 0) = 0.01; loop(2, 3) = 0.3;  // a small yaw + lift
+    CHECK(PointCloudClosure::do_lum_elch(line, 2, 9, loop), "do_lum_elch");
+    CHECK(line[2]._rot(2, 3) == 0.0 && std::fabs(line[9]._rot(2, 3) - 0.3) < 1e-12, "lum_elch ends %g %g",
+          line[2]._rot(2, 3), line[9]._rot(2, 3));
+    CHECK(std::fabs(line[5]._rot(2, 3) - 0.3 * 3.0 / 7.0) < 1e-12, "lum_elch weight 3/7: %g", line[5]._rot(2, 3));
+    std::vector<CloudStampRot> opt(ori.begin() + 6, ori.begin() + 9);
+    for (auto& o : opt) o._rot(1, 3) = 0.5;
+    CHECK(PointCloudClosure::do_loop_closure(ori, opt), "do_loop_closure");
+    CHECK(ori[7]._rot(1, 3) == 0.5 && std::fabs(ori[11]._rot(1, 3) - 0.5) < 1e-12, "loop closure splice/carry");
+    CHECK(PointCloudClosure::get_index_from_rots(ori, 104) == 4, "get_index_from_rots");
+    do_transform_interpolation(ori, 0, 11);
+    CHECK(std::fabs(ori[0]._rot(0, 3)) < 1e-12 && std::fabs(ori[11]._rot(1, 3) - 0.5) < 1e-9, "interpolation ends");
+}
+
 int main() {
+    test_pose_lines();
     test_voxel_grid();
     test_kd_tree();
     test_knn_radius_vs_oracle();
