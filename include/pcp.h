@@ -328,6 +328,35 @@ int pcp_pose_lum_elch(double* rots_host, int64_t n, int64_t start, int64_t end, 
 int pcp_pose_loop_closure(double* ori_host, const uint64_t* ori_stamps_host, int64_t n_ori, const double* opt_host,
                           const uint64_t* opt_stamps_host, int64_t n_opt, int64_t window);
 
+/* ----------------------------------------------------------------------- CloudGrid
+ * The map cache that builds every ICP target (cloud_grid.h:37-88; callers main_blend.cpp:263,
+ * 471, 792-795, 1027): 1 m cells keyed by ((int)x, (int)y), each holding the points kept by
+ * add_cloud_internal's sequential 4 cm de-duplication, replayed exactly per cell on the GPU.
+ * Clouds are device AoS48 records.
+ *
+ * pcp_grid_add_cloud: CloudGrid::add_cloud_internal (cloud_grid.cpp:34-78).
+ * pcp_grid_clear: CloudGrid::clear (:218-224).
+ * pcp_grid_points: get_grid_cloud(CloudPtr&) (:150-158): every kept point, cells in
+ * ((int)x, (int)y) order (the reference's is its hash map's), kept order within a cell.
+ * pcp_grid_box: get_cloud_with_pos (:84-131): cells i in [i0, i1), j in [j0, j1) in the
+ * reference's loop order (the shim derives the ranges from min/max or the pose as it does);
+ * out_dev NULL = count only.
+ * pcp_grid_match: get_grid_cloud(src, src_out, dst, dis) (:160-216): src points with a grid
+ * point of their cell within Chebyshev `dis` (cells spanning < 1.5 m in z skipped) and those
+ * grid points once each, in the reference's push order; cap >= pcp_grid_size suffices. */
+typedef struct pcp_grid pcp_grid;
+int pcp_grid_create(pcp_ctx* ctx, pcp_grid** out);
+int pcp_grid_destroy(pcp_grid* grid);
+int pcp_grid_clear(pcp_ctx* ctx, pcp_grid* grid);
+int pcp_grid_add_cloud(pcp_ctx* ctx, pcp_grid* grid, const void* cloud_dev, int64_t n);
+int64_t pcp_grid_size(const pcp_grid* grid);
+int64_t pcp_grid_cells(const pcp_grid* grid);
+int pcp_grid_points(pcp_ctx* ctx, const pcp_grid* grid, void* out_dev, int64_t cap, int64_t* n_out);
+int pcp_grid_box(pcp_ctx* ctx, const pcp_grid* grid, int i0, int i1, int j0, int j1, void* out_dev, int64_t cap,
+                 int64_t* n_out);
+int pcp_grid_match(pcp_ctx* ctx, const pcp_grid* grid, const void* src_dev, int64_t n_src, float dis,
+                   void* src_out_dev, int64_t* n_src_out, void* dst_dev, int64_t cap, int64_t* n_dst);
+
 #ifdef __cplusplus
 }
 #endif

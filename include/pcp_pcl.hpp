@@ -748,6 +748,79 @@ public:
     std::string _time_stamp_str;
 };
 
+// ------------------------------------------------------------------ CloudGrid (map cache)
+// cloud_grid.h:37-88: the reference's singleton over a boost hash map of 1 m cells; here the
+// cells and their de-duplicated points live on the device (pcp_grid_*, cloudgrid.hip) and the
+// members below stage clouds through the C-ABI.  Output clouds are filled in the reference's
+// order (get_grid_cloud(CloudPtr&): cell key order instead of the hash map's).
+class CloudGrid {
+public:
+    static const int MAX_DIS = 60;
+    static CloudGrid& instance() {
+        static CloudGrid g;
+        return g;
+    }
+    void clear() { detail::check(pcp_grid_clear(ctx(), g_), ctx(), "CloudGrid::clear"); }
+    void add_cloud_internal(CloudPtr newpoint) {  // cloud_grid.cpp:34-78
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        const size_t n = newpoint->points.size();
+        detail::DevBuf in;
+        in.upload(newpoint->points.data(), n * sizeof(PointXYZRGBA));
+        detail::check(pcp_grid_add_cloud(ctx(), g_, in.ptr(), (int64_t)n), ctx(), "CloudGrid::add_cloud_internal");
+    }
+    template <class M>
+    void get_cloud_with_pos(CloudPtr& cloud_cache, const M& cur_rot, int dis = MAX_DIS) {  // :84-108
+        const int irow = (int)(float)cur_rot(0, 3), icol = (int)(float)cur_rot(1, 3);  // Matrix4f entries
+        box(cloud_cache, irow - dis, irow + dis, icol - dis, icol + dis);
+    }
+    void get_cloud_with_pos(CloudPtr& cloud_cache, const PointXYZRGBA& min_xyz, const PointXYZRGBA& max_xyz) {
+        // for (int i = min_xyz.x; i < max_xyz.x; i++) (:118-119)
+        box(cloud_cache, (int)min_xyz.x, (int)std::ceil(max_xyz.x), (int)min_xyz.y, (int)std::ceil(max_xyz.y));
+    }
+    void get_grid_cloud(CloudPtr& cloud) {  // :150-158
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        int64_t n = pcp_grid_size(g_);
+        detail::DevBuf out;
+        out.reserve((size_t)n * sizeof(PointXYZRGBA));
+        detail::check(pcp_grid_points(ctx(), g_, out.ptr(), n, &n), ctx(), "CloudGrid::get_grid_cloud");
+        cloud->points.resize((size_t)n);
+        out.download(cloud->points.data(), (size_t)n * sizeof(PointXYZRGBA));
+    }
+    void get_grid_cloud(CloudPtr src_cloud, CloudPtr src_cloud_out, CloudPtr dst_cloud, float dis_threshold) {
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());  // :160-216
+        const size_t n = src_cloud->points.size();
+        const int64_t cap = pcp_grid_size(g_);
+        detail::DevBuf in, so, dst;
+        in.upload(src_cloud->points.data(), n * sizeof(PointXYZRGBA));
+        so.reserve(n * sizeof(PointXYZRGBA));
+        dst.reserve((size_t)cap * sizeof(PointXYZRGBA));
+        int64_t ns = 0, nd = 0;
+        detail::check(pcp_grid_match(ctx(), g_, in.ptr(), (int64_t)n, dis_threshold, so.ptr(), &ns, dst.ptr(), cap, &nd),
+                      ctx(), "CloudGrid::get_grid_cloud");
+        dst_cloud->points.resize((size_t)nd);
+        dst.download(dst_cloud->points.data(), (size_t)nd * sizeof(PointXYZRGBA));
+        std::vector<PointXYZRGBA> tmp((size_t)ns);
+        so.download(tmp.data(), (size_t)ns * sizeof(PointXYZRGBA));
+        src_cloud_out->points.swap(tmp);
+    }
+    ~CloudGrid() { pcp_grid_destroy(g_); }
+
+private:
+    CloudGrid() { detail::check(pcp_grid_create(ctx(), &g_), ctx(), "CloudGrid"); }
+    static pcp_ctx* ctx() { return detail::Device::get().ctx(); }
+    void box(CloudPtr& cache, int i0, int i1, int j0, int j1) {
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        int64_t n = 0;
+        detail::check(pcp_grid_box(ctx(), g_, i0, i1, j0, j1, nullptr, 0, &n), ctx(), "CloudGrid::get_cloud_with_pos");
+        detail::DevBuf out;
+        out.reserve((size_t)n * sizeof(PointXYZRGBA));
+        if (n) detail::check(pcp_grid_box(ctx(), g_, i0, i1, j0, j1, out.ptr(), n, &n), ctx(), "CloudGrid::box");
+        cache->points.resize((size_t)n);
+        out.download(cache->points.data(), (size_t)n * sizeof(PointXYZRGBA));
+    }
+    pcp_grid* g_ = nullptr;
+};
+
 // pose lines: the reference's Eigen composition restated in libpcp (pcp_pose_*, host-only)
 namespace detail {
 inline std::vector<double> pack_rots(const std::vector<CloudStampRot>& r) {

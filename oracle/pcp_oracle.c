@@ -1059,3 +1059,171 @@ float ora_get_rot_icp(const ora_point48* src, int ns, int src_dense, const ora_p
     free(fs); free(ft);
     return (float)err;
 }
+
+
+/* ======================================================================= CloudGrid
+ * cloud_grid.cpp:34-78 (add_cloud_internal), :110-131 (box), :160-216 (get_grid_cloud). */
+typedef struct {
+    uint64_t key;
+    int ix, iy;
+    int n, cap;
+    ora_point48* p;
+} ora_gcell;
+struct ora_grid {
+    ora_gcell* cells;
+    int ncell, ccap;
+    int* slot;  /* open addressing: cell index or -1 */
+    int nslot;
+};
+
+static uint64_t g_key(int ix, int iy) {
+    return ((uint64_t)((uint32_t)ix ^ 0x80000000u) << 32) | (uint64_t)((uint32_t)iy ^ 0x80000000u);
+}
+static uint32_t g_hash(uint64_t k) { return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32); }
+
+ora_grid* ora_grid_create(void) {
+    ora_grid* g = (ora_grid*)calloc(1, sizeof(ora_grid));
+    g->nslot = 1 << 16;
+    g->slot = (int*)malloc(sizeof(int) * g->nslot);
+    for (int i = 0; i < g->nslot; i++) g->slot[i] = -1;
+    return g;
+}
+void ora_grid_free(ora_grid* g) {
+    if (!g) return;
+    for (int c = 0; c < g->ncell; c++) free(g->cells[c].p);
+    free(g->cells);
+    free(g->slot);
+    free(g);
+}
+static int g_find(const ora_grid* g, uint64_t k) {
+    uint32_t h = g_hash(k) & (uint32_t)(g->nslot - 1);
+    while (g->slot[h] >= 0) {
+        if (g->cells[g->slot[h]].key == k) return g->slot[h];
+        h = (h + 1) & (uint32_t)(g->nslot - 1);
+    }
+    return -1;
+}
+static void g_rehash(ora_grid* g) {
+    free(g->slot);
+    g->nslot *= 2;
+    g->slot = (int*)malloc(sizeof(int) * g->nslot);
+    for (int i = 0; i < g->nslot; i++) g->slot[i] = -1;
+    for (int c = 0; c < g->ncell; c++) {
+        uint32_t h = g_hash(g->cells[c].key) & (uint32_t)(g->nslot - 1);
+        while (g->slot[h] >= 0) h = (h + 1) & (uint32_t)(g->nslot - 1);
+        g->slot[h] = c;
+    }
+}
+static void g_push(ora_gcell* c, const ora_point48* p) {
+    if (c->n == c->cap) {
+        c->cap = c->cap ? 2 * c->cap : 16;
+        c->p = (ora_point48*)realloc(c->p, sizeof(ora_point48) * c->cap);
+    }
+    c->p[c->n++] = *p;
+}
+/* is_2point_high_x (cloud_grid.h:79-84) */
+static int g_high_x(const ora_point48* a, const ora_point48* b, double x) {
+    return fabs(a->x - b->x) > x || fabs(a->y - b->y) > x || fabs(a->z - b->z) > x;
+}
+/* dis_two_point returns float (cloud_grid.h:73-77) */
+static float g_dis2(const ora_point48* a, const ora_point48* b) {
+    return (float)((a->x - b->x) * (a->x - b->x) + (a->y - b->y) * (a->y - b->y) + (a->z - b->z) * (a->z - b->z));
+}
+void ora_grid_add_cloud(ora_grid* g, const ora_point48* in, int n) {
+    const double X = 0.04, X2 = X * X;  /* MAX_DIS_2POINT_X, MAX_DIS_2POINT (cloud_grid.cpp:11-12) */
+    for (int i = 0; i < n; i++) {
+        const int irow = (int)in[i].x, icol = (int)in[i].y;
+        const uint64_t k = g_key(irow, icol);
+        const int c = g_find(g, k);
+        if (c < 0) {
+            if (g->ncell == g->ccap) {
+                g->ccap = g->ccap ? 2 * g->ccap : 1024;
+                g->cells = (ora_gcell*)realloc(g->cells, sizeof(ora_gcell) * g->ccap);
+            }
+            ora_gcell* cell = &g->cells[g->ncell];
+            memset(cell, 0, sizeof(*cell));
+            cell->key = k;
+            cell->ix = irow;
+            cell->iy = icol;
+            g_push(cell, &in[i]);
+            g->ncell++;
+            if (2 * g->ncell > g->nslot) g_rehash(g);
+            else {
+                uint32_t h = g_hash(k) & (uint32_t)(g->nslot - 1);
+                while (g->slot[h] >= 0) h = (h + 1) & (uint32_t)(g->nslot - 1);
+                g->slot[h] = g->ncell - 1;
+            }
+        } else {
+            ora_gcell* cell = &g->cells[c];
+            int mindis = 1;
+            for (int q = 0; q < cell->n; q++) {
+                if (g_high_x(&cell->p[q], &in[i], X)) continue;
+                if ((double)g_dis2(&cell->p[q], &in[i]) < X2) {
+                    mindis = 0;
+                    break;
+                }
+            }
+            if (mindis) g_push(cell, &in[i]);
+        }
+    }
+}
+int ora_grid_size(const ora_grid* g) {
+    int s = 0;
+    for (int c = 0; c < g->ncell; c++) s += g->cells[c].n;
+    return s;
+}
+static int g_cmp(const void* a, const void* b) {
+    const uint64_t x = ((const ora_gcell*)a)->key, y = ((const ora_gcell*)b)->key;
+    return x < y ? -1 : (x > y ? 1 : 0);
+}
+int ora_grid_points(const ora_grid* g, ora_point48* out) {
+    ora_gcell* cs = (ora_gcell*)malloc(sizeof(ora_gcell) * (g->ncell ? g->ncell : 1));
+    memcpy(cs, g->cells, sizeof(ora_gcell) * g->ncell);
+    qsort(cs, g->ncell, sizeof(ora_gcell), g_cmp);
+    int m = 0;
+    for (int c = 0; c < g->ncell; c++)
+        for (int q = 0; q < cs[c].n; q++) out[m++] = cs[c].p[q];
+    free(cs);
+    return m;
+}
+int ora_grid_box(const ora_grid* g, int i0, int i1, int j0, int j1, ora_point48* out) {
+    int m = 0;
+    for (int i = i0; i < i1; i++)
+        for (int j = j0; j < j1; j++) {
+            const int c = g_find(g, g_key(i, j));
+            if (c < 0) continue;
+            for (int q = 0; q < g->cells[c].n; q++) out[m++] = g->cells[c].p[q];
+        }
+    return m;
+}
+int ora_grid_match(const ora_grid* g, const ora_point48* src, int nsrc, float dis, ora_point48* src_out,
+                   int* n_src_out, ora_point48* dst) {
+    /* grid_index_map: per cell, the set of indices already emitted */
+    unsigned char** used = (unsigned char**)calloc(g->ncell ? g->ncell : 1, sizeof(unsigned char*));
+    int ns = 0, nd = 0;
+    for (int i = 0; i < nsrc; i++) {
+        const int c = g_find(g, g_key((int)src[i].x, (int)src[i].y));
+        if (c < 0) continue;
+        const ora_gcell* cell = &g->cells[c];
+        double min_z = DBL_MAX, max_z = DBL_MIN;  /* numeric_limits<double>::min() (:185-186) */
+        for (int k = 0; k < cell->n; k++) {
+            min_z = min_z < cell->p[k].z ? min_z : cell->p[k].z;
+            max_z = max_z > cell->p[k].z ? max_z : cell->p[k].z;
+        }
+        if (max_z - min_z < 1.5) continue;
+        int is_find = 0;
+        for (int k = 0; k < cell->n; k++) {
+            if (g_high_x(&cell->p[k], &src[i], (double)dis)) continue;
+            is_find = 1;
+            if (!used[c]) used[c] = (unsigned char*)calloc(cell->n, 1);
+            if (used[c][k]) continue;
+            used[c][k] = 1;
+            dst[nd++] = cell->p[k];
+        }
+        if (is_find) src_out[ns++] = src[i];
+    }
+    for (int c = 0; c < g->ncell; c++) free(used[c]);
+    free(used);
+    *n_src_out = ns;
+    return nd;
+}

@@ -174,6 +174,24 @@ double ora_icp(const float* tgt, int nt, const float* q, int nq, double T[16], f
 float ora_get_rot_icp(const ora_point48* src, int ns, int src_dense, const ora_point48* tmp, int nt, int tmp_dense,
                       double mat_rot[16], float rmax, int iters, int do_scale, int nthreads);
 
+
+/* CloudGrid (cloud_grid.cpp): a grid of 1 m cells keyed by ((int)x, (int)y), each holding
+ * the points kept by add_cloud_internal's sequential 4 cm de-duplication (:34-78).  The
+ * restatement keeps the cells in a hash map (as the reference) and reports them in key order
+ * ((int)x, then (int)y) where the reference's order is the hash map's (get_grid_cloud). */
+typedef struct ora_grid ora_grid;
+ora_grid* ora_grid_create(void);
+void ora_grid_free(ora_grid* g);
+void ora_grid_add_cloud(ora_grid* g, const ora_point48* in, int n);          /* :34-78 */
+int ora_grid_size(const ora_grid* g);
+/* all kept points, cells in key order, kept order within a cell */
+int ora_grid_points(const ora_grid* g, ora_point48* out);
+/* get_cloud_with_pos over the cells i in [i0, i1), j in [j0, j1) in loop order (:110-131) */
+int ora_grid_box(const ora_grid* g, int i0, int i1, int j0, int j1, ora_point48* out);
+/* get_grid_cloud(src, src_out, dst, dis) (:160-216): returns the dst count, *n_src_out */
+int ora_grid_match(const ora_grid* g, const ora_point48* src, int nsrc, float dis, ora_point48* src_out,
+                   int* n_src_out, ora_point48* dst);
+
 #ifdef __cplusplus
 }
 #endif

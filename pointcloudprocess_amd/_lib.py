@@ -59,6 +59,15 @@ SIGNATURES = [
     ("pcp_transform_aos48", _i32, [_vp, _vp, _vp, _i64, _i32, _P(_f64)]),
     ("pcp_voxel_filter", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _i32, _vp, _P(_i64), _vp]),
     ("pcp_pose_interpolate", _i32, [_vp, _i64, _i64, _i64]),
+    ("pcp_grid_create", _i32, [_vp, _P(_vp)]),
+    ("pcp_grid_destroy", _i32, [_vp]),
+    ("pcp_grid_clear", _i32, [_vp, _vp]),
+    ("pcp_grid_add_cloud", _i32, [_vp, _vp, _vp, _i64]),
+    ("pcp_grid_size", _i64, [_vp]),
+    ("pcp_grid_cells", _i64, [_vp]),
+    ("pcp_grid_points", _i32, [_vp, _vp, _vp, _i64, _P(_i64)]),
+    ("pcp_grid_box", _i32, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _P(_i64)]),
+    ("pcp_grid_match", _i32, [_vp, _vp, _vp, _i64, _f32, _vp, _P(_i64), _vp, _i64, _P(_i64)]),
     ("pcp_pose_lum_elch", _i32, [_vp, _i64, _i64, _i64, _vp]),
     ("pcp_pose_loop_closure", _i32, [_vp, _vp, _i64, _vp, _vp, _i64, _i64]),
     ("pcp_remove_duplicate", _i32, [_vp, _vp, _i64, _i32, _f32, _vp, _P(_i64)]),

@@ -260,8 +260,37 @@ static void test_pose_lines() {  // main_blend.cpp:934-980, point_cloud_closure.
     CHECK(std::fabs(ori[0]._rot(0, 3)) < 1e-12 && std::fabs(ori[11]._rot(1, 3) - 0.5) < 1e-9, "interpolation ends");
 }
 
+static void test_cloud_grid() {  // cloud_grid.cpp:34-216 through the shim vs the C restatement
+    CloudPtr base = random_cloud(30000, 21, 5.0);
+    CloudPtr more = random_cloud(10000, 22, 5.0);
+    CloudGrid& g = CloudGrid::instance();
+    g.clear();
+    g.add_cloud_internal(base);
+    g.add_cloud_internal(more);
+    ora_grid* og = ora_grid_create();
+    ora_grid_add_cloud(og, (const ora_point48*)base->points.data(), (int)base->size());
+    ora_grid_add_cloud(og, (const ora_point48*)more->points.data(), (int)more->size());
+    CloudPtr all(new Cloud());
+    g.get_grid_cloud(all);
+    std::vector<ora_point48> ea(ora_grid_size(og));
+    const int na = ora_grid_points(og, ea.data());
+    CHECK((int)all->size() == na && std::memcmp(all->points.data(), ea.data(), na * sizeof(ora_point48)) == 0,
+          "CloudGrid points %zu vs %d", all->size(), na);
+    PointXYZRGBA mn{}, mx{};
+    mn.x = -2.5; mn.y = -1.2; mx.x = 3.5; mx.y = 2.0;
+    CloudPtr box(new Cloud());
+    g.get_cloud_with_pos(box, mn, mx);
+    std::vector<ora_point48> eb(ea.size());
+    const int nb = ora_grid_box(og, -2, 4, -1, 2, eb.data());
+    CHECK((int)box->size() == nb && std::memcmp(box->points.data(), eb.data(), nb * sizeof(ora_point48)) == 0,
+          "CloudGrid box %zu vs %d", box->size(), nb);
+    ora_grid_free(og);
+    g.clear();
+}
+
 int main() {
     test_pose_lines();
+    test_cloud_grid();
     test_voxel_grid();
     test_kd_tree();
     test_knn_radius_vs_oracle();

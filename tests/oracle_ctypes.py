@@ -75,6 +75,13 @@ def load():
     lib.ora_get_rot_icp.restype = C.c_float
     lib.ora_get_rot_icp.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.c_float,
                                     C.c_int, C.c_int, C.c_int]
+    lib.ora_grid_create.restype = vp
+    lib.ora_grid_free.argtypes = [vp]
+    lib.ora_grid_add_cloud.argtypes = [vp, vp, C.c_int]
+    lib.ora_grid_size.argtypes = [vp]
+    lib.ora_grid_points.argtypes = [vp, vp]
+    lib.ora_grid_box.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+    lib.ora_grid_match.argtypes = [vp, vp, C.c_int, C.c_float, vp, vp, vp]
     _lib = lib
     return lib
 
@@ -307,3 +314,43 @@ def get_rot_icp(src, tmp, rmax, iters, do_scale=False, nthreads=0, src_dense=Tru
                               int(tmp_dense), M.ctypes.data, float(rmax), int(iters), int(do_scale),
                               nthreads)
     return float(err), M.reshape(4, 4)
+
+
+class Grid:
+    """CloudGrid restatement (ora_grid_*, cloud_grid.cpp)."""
+
+    def __init__(self):
+        self.lib = load()
+        self.h = self.lib.ora_grid_create()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.ora_grid_free(self.h)
+            self.h = None
+
+    def add_cloud(self, cloud):
+        cloud = np.ascontiguousarray(cloud)
+        self.lib.ora_grid_add_cloud(self.h, cloud.ctypes.data, len(cloud))
+
+    @property
+    def size(self):
+        return self.lib.ora_grid_size(self.h)
+
+    def points(self):
+        out = np.zeros(max(self.size, 1), dtype=POINT48)
+        m = self.lib.ora_grid_points(self.h, out.ctypes.data)
+        return out[:m]
+
+    def box(self, i0, i1, j0, j1):
+        out = np.zeros(max(self.size, 1), dtype=POINT48)
+        m = self.lib.ora_grid_box(self.h, int(i0), int(i1), int(j0), int(j1), out.ctypes.data)
+        return out[:m]
+
+    def match(self, src, dis):
+        src = np.ascontiguousarray(src)
+        so = np.zeros(max(len(src), 1), dtype=POINT48)
+        dst = np.zeros(max(self.size, 1), dtype=POINT48)
+        ns = C.c_int(0)
+        nd = self.lib.ora_grid_match(self.h, src.ctypes.data, len(src), C.c_float(dis), so.ctypes.data,
+                                     C.byref(ns), dst.ctypes.data)
+        return so[:ns.value], dst[:nd]
