@@ -357,6 +357,22 @@ int pcp_grid_box(pcp_ctx* ctx, const pcp_grid* grid, int i0, int i1, int j0, int
 int pcp_grid_match(pcp_ctx* ctx, const pcp_grid* grid, const void* src_dev, int64_t n_src, float dis,
                    void* src_out_dev, int64_t* n_src_out, void* dst_dev, int64_t cap, int64_t* n_dst);
 
+/* ----------------------------------------------------------------------- PCD / LZF I/O
+ * Host-only (caller buffers; pinned host memory then stages to the device in one copy).
+ * pcp_pcd_write: io::savePCDFile / savePCDFileBinary -> PCDWriter::writeBinary
+ * (pcd_helper.h:489-610) or writeBinaryCompressed (:628-790) of n PointXYZRGBA records:
+ * the header of generateHeader (:321-371; fields x y z rgba stamp_id, point_type.h:326-332),
+ * then packed records, or SoA planes LZF-compressed behind (compressed, uncompressed) u32
+ * sizes.  width/height <= 0: n x 1.  PCP_ERR_EMPTY for n == 0 (the reference throws).
+ * pcp_pcd_read: io::loadPCDFile (pcd_helper.h:1374-1378 -> PCDReader, pcd_helper.cpp:71-1395)
+ * of DATA ascii / binary / binary_compressed; out_host NULL = size query (*n_out = POINTS).
+ * pcp_lzf_compress / pcp_lzf_decompress: lzfCompress / lzfDecompress (lzf.cpp:86-415);
+ * return the output size, 0 on failure. */
+int pcp_pcd_write(const char* path, const void* pts_host, int64_t n, int64_t width, int64_t height, int compressed);
+int pcp_pcd_read(const char* path, void* out_host, int64_t cap, int64_t* n_out);
+size_t pcp_lzf_compress(const void* in_host, size_t in_len, void* out_host, size_t out_len);
+size_t pcp_lzf_decompress(const void* in_host, size_t in_len, void* out_host, size_t out_len);
+
 #ifdef __cplusplus
 }
 #endif

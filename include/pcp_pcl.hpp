@@ -821,6 +821,35 @@ private:
     pcp_grid* g_ = nullptr;
 };
 
+// ------------------------------------------------------------------ PCD I/O (pcd_helper.h)
+namespace io {
+// io::loadPCDFile (pcd_helper.h:1374-1378): ascii / binary / binary_compressed; 0 or -1
+inline int loadPCDFile(const std::string& file_name, Cloud& cloud) {
+    int64_t n = 0;
+    if (pcp_pcd_read(file_name.c_str(), nullptr, 0, &n) != PCP_OK) return -1;
+    cloud.points.resize((size_t)n);
+    if (pcp_pcd_read(file_name.c_str(), cloud.points.data(), n, &n) != PCP_OK) return -1;
+    return 0;
+}
+// io::savePCDFile(binary_mode = true) / savePCDFileBinary -> writeBinary (:489-610); the
+// reference throws IOException on an empty cloud or an I/O error
+inline int savePCDFileBinary(const std::string& file_name, const Cloud& cloud) {
+    const int rc = pcp_pcd_write(file_name.c_str(), cloud.points.data(), (int64_t)cloud.points.size(), 0, 0, 0);
+    if (rc != PCP_OK) throw PCLException("[pcl::PCDWriter::writeBinary] " + file_name);
+    return 0;
+}
+inline int savePCDFile(const std::string& file_name, const Cloud& cloud, bool binary_mode = true) {
+    if (!binary_mode) throw PCLException("savePCDFile: ASCII output is not provided by this build");
+    return savePCDFileBinary(file_name, cloud);
+}
+// PCDWriter::writeBinaryCompressed (:628-790)
+inline int savePCDFileBinaryCompressed(const std::string& file_name, const Cloud& cloud) {
+    const int rc = pcp_pcd_write(file_name.c_str(), cloud.points.data(), (int64_t)cloud.points.size(), 0, 0, 1);
+    if (rc != PCP_OK) throw PCLException("[pcl::PCDWriter::writeBinaryCompressed] " + file_name);
+    return 0;
+}
+}  // namespace io
+
 // pose lines: the reference's Eigen composition restated in libpcp (pcp_pose_*, host-only)
 namespace detail {
 inline std::vector<double> pack_rots(const std::vector<CloudStampRot>& r) {

@@ -288,7 +288,26 @@ static void test_cloud_grid() {  // cloud_grid.cpp:34-216 through the shim vs th
     g.clear();
 }
 
+static void test_pcd_io() {  // pcd_helper.h writeBinary / writeBinaryCompressed / loadPCDFile
+    CloudPtr c = random_cloud(2000, 31, 20.0);
+    for (int compressed = 0; compressed < 2; compressed++) {
+        const std::string path = compressed ? "/tmp/pcp_shim_test_c.pcd" : "/tmp/pcp_shim_test_b.pcd";
+        if (compressed) io::savePCDFileBinaryCompressed(path, *c);
+        else io::savePCDFileBinary(path, *c);
+        Cloud back;
+        CHECK(io::loadPCDFile(path, back) == 0 && back.size() == c->size(), "pcd read %d", compressed);
+        bool same = back.size() == c->size();
+        for (size_t i = 0; same && i < back.size(); i++)
+            same = back.points[i].x == c->points[i].x && back.points[i].y == c->points[i].y &&
+                   back.points[i].z == c->points[i].z && back.points[i].rgba == c->points[i].rgba &&
+                   back.points[i].stamp_id == c->points[i].stamp_id;
+        CHECK(same, "pcd round trip %d", compressed);
+        std::remove(path.c_str());
+    }
+}
+
 int main() {
+    test_pcd_io();
     test_pose_lines();
     test_cloud_grid();
     test_voxel_grid();

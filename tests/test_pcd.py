@@ -1,0 +1,90 @@
+"""PCD v0.7 / LZF I/O (libpcp pcp_pcd_*, host-only) against the pure-Python restatement of
+the reference's writers and codec (oracle/pcd_oracle.py): byte-identical files (binary and
+binary_compressed), byte-identical LZF streams on varied inputs, round trips, and reading
+files with other field sets / types / ascii data the reference's reader accepts."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import oracle_ctypes as ora  # noqa: E402
+import pcd_oracle as po  # noqa: E402
+from pointcloudprocess_amd import pcd  # noqa: E402
+
+
+def cloud(n, seed):
+    rng = np.random.default_rng(seed)
+    xyz = np.round(rng.uniform(-50, 50, (n, 3)), 3)  # quantised (compressible), like voxelised maps
+    xyz[: n // 3] = np.round(xyz[: n // 3], 1)
+    return ora.make_cloud(xyz, rgba=rng.integers(0, 4, n).astype(np.uint32) * 0x01010101,
+                          stamp=(np.arange(n) // 97).astype(np.uint32))
+
+
+@pytest.mark.parametrize("data", [b"", b"a", b"ab", b"abc", b"abcabcabcabc" * 3, bytes(range(256)) * 5,
+                                  b"\x00" * 300, b"xyzxyz" * 20 + b"q" * 17])
+def test_lzf_matches_restatement(data):
+    cap = int(len(data) * 1.5) + 16
+    got = pcd.lzf_compress(data, cap)
+    exp = po.lzf_compress(data, cap)
+    assert got == exp
+    if got:
+        assert pcd.lzf_decompress(got, len(data)) == data
+        assert po.lzf_decompress(got, len(data)) == data
+
+
+def test_lzf_random_blocks():
+    rng = np.random.default_rng(3)
+    for t in range(6):
+        n = int(rng.integers(1000, 40000))
+        alphabet = int(rng.integers(2, 256))
+        data = rng.integers(0, alphabet, n).astype(np.uint8).tobytes() + bytes(rng.integers(0, 4, 300).astype(np.uint8))
+        cap = int(n * 1.5) + 16
+        got = pcd.lzf_compress(data, cap)
+        assert got == po.lzf_compress(data, cap)
+        assert pcd.lzf_decompress(got, len(data)) == data
+
+
+@pytest.mark.parametrize("compressed", [False, True])
+def test_pcd_write_bytes_and_round_trip(tmp_path, compressed):
+    c = cloud(5000, 1)
+    p = tmp_path / "c.pcd"
+    pcd.save_pcd(p, c, compressed=compressed)
+    assert p.read_bytes() == po.pcd_bytes(c, compressed)
+    back = pcd.load_pcd(p)
+    for f in ("x", "y", "z", "rgba", "stamp_id"):
+        assert np.array_equal(back[f], c[f])
+    assert (back["w"] == 1.0).all()  # PointXYZRGBA() data[3] = 1 (point_type.h:86-91)
+
+
+def test_pcd_empty_cloud_rejected(tmp_path):
+    with pytest.raises(Exception):
+        pcd.save_pcd(tmp_path / "e.pcd", cloud(0, 2))
+
+
+def test_pcd_read_other_layouts(tmp_path):
+    # float xyz + packed float rgb, ascii and binary, extra fields ignored
+    n = 50
+    rng = np.random.default_rng(4)
+    xyz = rng.uniform(-5, 5, (n, 3)).astype(np.float32)
+    rgb = rng.integers(0, 2**24, n).astype(np.uint32)
+    inten = rng.uniform(0, 1, n).astype(np.float32)
+    head = ("# .PCD v0.7\nVERSION 0.7\nFIELDS x y z intensity rgb\nSIZE 4 4 4 4 4\nTYPE F F F F F\nCOUNT 1 1 1 1 1\n"
+            "WIDTH {n}\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS {n}\nDATA {d}\n")
+    rec = np.zeros(n, dtype=[("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("i", "<f4"), ("rgb", "<u4")])
+    rec["x"], rec["y"], rec["z"], rec["i"], rec["rgb"] = xyz[:, 0], xyz[:, 1], xyz[:, 2], inten, rgb
+    p = tmp_path / "b.pcd"
+    p.write_bytes(head.format(n=n, d="binary").encode() + rec.tobytes())
+    b = pcd.load_pcd(p)
+    assert np.array_equal(b["x"], xyz[:, 0].astype(np.float64)) and np.array_equal(b["rgba"], rgb)
+    assert (b["stamp_id"] == 0).all()
+    lines = [f"{x!r} {y!r} {z!r} {i!r} {float(np.uint32(c).view(np.float32))!r}" for (x, y, z), i, c in
+             zip(xyz.tolist(), inten.tolist(), rgb)]
+    p2 = tmp_path / "a.pcd"
+    p2.write_text(head.format(n=n, d="ascii") + "\n".join(lines) + "\n")
+    a = pcd.load_pcd(p2)
+    assert np.allclose(a["x"], xyz[:, 0], rtol=0, atol=1e-6) and np.array_equal(a["rgba"], rgb)
