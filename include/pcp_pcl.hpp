@@ -104,6 +104,13 @@ struct LAS_POINT_PROPERTY {  // data_struct.h:161-172
     float dis_from_point_plane;
 };
 
+struct alignas(16) PointC {  // point_type.h:244-316 (64 bytes; the kd-tree uses x, y, z)
+    double x = 0, y = 0, z = 0, w = 1.0;
+    uint64_t stamp = 0;
+    double angle_z = 0;
+    double distance_sqr = 0;
+};
+
 class PCLException : public std::runtime_error {  // exception.h:11
 public:
     explicit PCLException(const std::string& m) : std::runtime_error(m) {}
@@ -304,6 +311,21 @@ public:
     }
 
     // ---- batch extensions (one launch for many queries)
+    // find_cloud_nearest_point_in_kdtree (main_blend.cpp:306-325): the query whose 1-NN d2 is
+    // smallest (strict '<' from 9999, the first wins ties), or a default point when none beats it
+    PointT nearestQuery(const PointCloud<PointT>& cloud) const {
+        if (!st_ || cloud.points.empty()) return PointT();
+        pcp_ctx* c = detail::Device::get().ctx();
+        std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+        std::vector<double> qh = detail::pack_xyz(cloud.points);
+        detail::DevBuf q;
+        q.upload(qh.data(), qh.size() * sizeof(double));
+        int64_t best = -1;
+        double bd = 0;
+        detail::check(pcp_nearest_query(c, st_->index, (const double*)q.ptr(), 24, (int64_t)cloud.points.size(), 9999.0,
+                                        &best, &bd), c, "pcp_nearest_query");
+        return best >= 0 ? cloud.points[best] : PointT();
+    }
     // rows of k: k_indices[i*k + r] (-1 / +inf past the tree size)
     void nearestKSearchBatch(const std::vector<PointT>& queries, int k, std::vector<int>& k_indices,
                              std::vector<double>& k_sqr_distances) const {
@@ -850,6 +872,55 @@ inline int savePCDFileBinaryCompressed(const std::string& file_name, const Cloud
 }
 }  // namespace io
 
+// ------------------------------------------------------------------ find_reliable
+class Rot {  // main_blend.cpp:282-297
+public:
+    int ID;
+    Mat4d _matrix;
+    uint64_t TimeStamp;
+    int _const100;
+    double icperr;
+    bool is_valid;
+    Rot(int id, const Mat4d& mat, uint64_t timestamp, double icp_value)
+        : ID(id), _matrix(mat), TimeStamp(timestamp), _const100(100), icperr(icp_value), is_valid(false) {}
+};
+
+// find_cloud_nearest_point_in_kdtree (main_blend.cpp:306-325): the per-point loop as one
+// batched nearest search with a single MIN reduction (pcp_nearest_query)
+inline CloudItem find_cloud_nearest_point_in_kdtree(CloudPtr cloud, KdTreeFLANN<CloudItem>& kdtree) {
+    return kdtree.nearestQuery(*cloud);
+}
+
+// find_reliable (main_blend.cpp:327-380): frames whose neighbours' closest points agree
+inline void find_reliable(std::vector<Rot>& rots, std::string cloud_files_dir, float icp_threshold) {
+    const float dis_threshold = 0.06f;
+    auto path = [&](uint64_t st) { return cloud_files_dir + "/" + std::to_string(st) + ".pcd"; };
+    auto xform = [](const Mat4d& m, const CloudItem& p, double o[4]) {
+        const double v[4] = {p.x, p.y, p.z, p.data[3]};
+        for (int r = 0; r < 4; r++) o[r] = m(r, 0) * v[0] + m(r, 1) * v[1] + m(r, 2) * v[2] + m(r, 3) * v[3];
+    };
+    for (int i = 1; i + 1 < (int)rots.size(); i++) {
+        if (!(rots[i].icperr >= 0 && rots[i].icperr <= icp_threshold && rots[i - 1].icperr >= 0 && rots[i + 1].icperr >= 0))
+            continue;
+        CloudPtr left(new Cloud), right(new Cloud), centra(new Cloud);
+        io::loadPCDFile(path(rots[i - 1].TimeStamp), *left);
+        io::loadPCDFile(path(rots[i + 1].TimeStamp), *right);
+        io::loadPCDFile(path(rots[i].TimeStamp), *centra);
+        KdTreeFLANN<CloudItem> kdtree;
+        kdtree.setInputCloud(centra);
+        double a[4], b[4];
+        const CloudItem lp = find_cloud_nearest_point_in_kdtree(left, kdtree);
+        xform(rots[i - 1]._matrix, lp, a);
+        xform(rots[i]._matrix, lp, b);
+        const double dis_left = std::pow(a[0] - b[0], 2) + std::pow(a[1] - b[1], 2) + std::pow(a[2] - b[2], 2);
+        const CloudItem rp = find_cloud_nearest_point_in_kdtree(right, kdtree);
+        xform(rots[i]._matrix, rp, a);
+        xform(rots[i + 1]._matrix, rp, b);
+        const double dis_right = std::pow(a[0] - b[0], 2) + std::pow(a[1] - b[1], 2) + std::pow(a[2] - b[2], 2);
+        if (dis_left < dis_threshold && dis_right < dis_threshold) rots[i].is_valid = true;
+    }
+}
+
 // pose lines: the reference's Eigen composition restated in libpcp (pcp_pose_*, host-only)
 namespace detail {
 inline std::vector<double> pack_rots(const std::vector<CloudStampRot>& r) {
@@ -870,8 +941,63 @@ inline void do_transform_interpolation(std::vector<CloudStampRot>& line, int sta
     detail::unpack_rots(a, line);
 }
 
-class PointCloudClosure {  // point_cloud_closure.cpp:185-276 (the pose-line members)
+class PointCloudClosure {  // point_cloud_closure.cpp:44-276 (the pose-line and overlap members)
 public:
+    struct same_segment {  // point_cloud_closure.h:15-21
+        uint64_t base_start_stamp, base_end_stamp, frame_start_stamp, frame_end_stamp;
+    };
+    // get_overlap_stamp (:44-180): the per-point radiusSearch(10) loop as one batched search
+    static void get_overlap_stamp(const std::vector<CloudStampRot>& rots, std::vector<same_segment>& overlap_segs) {
+        auto minus_abs = [](uint64_t a, uint64_t b) { return a > b ? a - b : b - a; };
+        typename PointCloud<PointC>::Ptr pts(new PointCloud<PointC>());
+        for (size_t i = 0; i + 1 < rots.size(); i++) {
+            const double x = rots[i]._rot(0, 3), y = rots[i]._rot(1, 3), z = rots[i]._rot(2, 3);
+            const double dx = rots[i + 1]._rot(0, 3) - x, dy = rots[i + 1]._rot(1, 3) - y, dz = rots[i + 1]._rot(2, 3) - z;
+            PointC d;
+            d.x = x; d.y = y; d.z = z;
+            d.stamp = rots[i]._stamp;
+            d.angle_z = std::atan2(dy, dx) * 57.29578;  // RAD2DEG (macros.h:15)
+            d.distance_sqr = std::pow(dx, 2) + std::pow(dy, 2) + std::pow(dz, 2);
+            if (d.angle_z < 0) d.angle_z += 360.0f;
+            if (d.distance_sqr <= 0.1) continue;
+            pts->push_back(d);
+        }
+        overlap_segs.clear();
+        if (pts->points.empty()) return;
+        KdTreeFLANN<PointC> tree;
+        tree.setInputCloud(pts);
+        std::vector<int64_t> off;
+        std::vector<int> idx;
+        std::vector<double> d2;
+        tree.radiusSearchBatch(pts->points, 10, off, idx, d2);
+        std::vector<std::pair<uint64_t, uint64_t>> pairs;
+        for (size_t i = 0; i < pts->points.size(); i++) {
+            const PointC& cp = pts->points[i];
+            for (int64_t t = off[i]; t < off[i + 1]; t++) {
+                const PointC& q = pts->points[idx[t]];
+                if (q.stamp <= cp.stamp || minus_abs(cp.stamp, q.stamp) < 6000) continue;
+                if (std::abs(cp.angle_z - q.angle_z) >= 20.0f) continue;
+                double avg = (cp.angle_z + q.angle_z) / 2.0 - 90;
+                avg = avg / 180.0 * M_PI;
+                const double k = std::tan(avg), b = cp.y - k * cp.x;
+                if (std::abs(0 - k * q.x + q.y - b) / std::sqrt(k * k + 1) > 1.5) continue;
+                pairs.emplace_back(cp.stamp, q.stamp);
+                break;
+            }
+        }
+        if (pairs.empty()) return;
+        uint64_t bs = pairs[0].first, fs = pairs[0].second;
+        for (size_t i = 1; i < pairs.size(); i++) {
+            if (minus_abs(pairs[i].first, pairs[i - 1].first) > 10 || minus_abs(pairs[i].second, pairs[i - 1].second) > 10) {
+                overlap_segs.push_back({bs, pairs[i - 1].first, fs, pairs[i - 1].second});
+                bs = pairs[i].first;
+                fs = pairs[i].second;
+            }
+        }
+        overlap_segs.push_back({bs, pairs.back().first, fs, pairs.back().second});
+        for (auto& sg : overlap_segs)
+            if (sg.frame_start_stamp > sg.frame_end_stamp) std::swap(sg.frame_start_stamp, sg.frame_end_stamp);
+    }
     static int get_index_from_rots(const std::vector<CloudStampRot>& rots, uint64_t stamp) {
         for (size_t i = 0; i < rots.size(); i++)
             if (rots[i]._stamp == stamp) return (int)i;

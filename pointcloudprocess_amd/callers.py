@@ -1,0 +1,118 @@
+"""Callers of the hot path restructured to batch: the reference's
+per-point / per-frame loops around kNN / radius become one batched pcp_* call each.
+
+  get_overlap_stamp(poses, stamps)        PointCloudClosure::get_overlap_stamp
+                                          (point_cloud_closure.cpp:44-180): one batched
+                                          radiusSearch(r = 10) over the trajectory, then the
+                                          reference's first-passing-candidate scan of each
+                                          sorted row and the segment grouping
+  find_reliable(rots, load_cloud, thr)    find_reliable (main_blend.cpp:327-380): per frame the
+                                          centre cloud's index and two batched
+                                          find_cloud_nearest_point_in_kdtree reductions
+                                          (pcp_nearest_query, one MIN over all queries)
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+
+RAD2DEG = 57.29578  # macros.h:15
+
+
+def _d_rots(poses, stamps):
+    """The trajectory points of get_overlap_stamp (:46-79): position, stamp, heading (deg in
+    [0, 360)), squared step; steps with distance_sqr <= 0.1 dropped."""
+    out = []
+    for i in range(len(poses) - 1):
+        x, y, z = poses[i][0][3], poses[i][1][3], poses[i][2][3]
+        dx, dy, dz = poses[i + 1][0][3] - x, poses[i + 1][1][3] - y, poses[i + 1][2][3] - z
+        ang = math.atan2(dy, dx) * RAD2DEG
+        dist = math.pow(dx, 2) + math.pow(dy, 2) + math.pow(dz, 2)
+        if ang < 0:
+            ang += 360.0
+        if dist <= 0.1:
+            continue
+        out.append((x, y, z, int(stamps[i]), ang))
+    return out
+
+
+def _segments(pair_vec):
+    """The segment grouping of get_overlap_stamp (:132-174)."""
+    segs = []
+    if not pair_vec:
+        return segs
+    base_start, frame_start = pair_vec[0]
+    for i in range(1, len(pair_vec)):
+        if abs(pair_vec[i][0] - pair_vec[i - 1][0]) > 10 or abs(pair_vec[i][1] - pair_vec[i - 1][1]) > 10:
+            segs.append([base_start, pair_vec[i - 1][0], frame_start, pair_vec[i - 1][1]])
+            base_start, frame_start = pair_vec[i]
+    segs.append([base_start, pair_vec[-1][0], frame_start, pair_vec[-1][1]])
+    for s in segs:
+        if s[2] > s[3]:
+            s[2], s[3] = s[3], s[2]
+    return [tuple(s) for s in segs]
+
+
+def _first_pair(pts, i, row):
+    """The scan of one sorted radiusSearch row (:88-127): the first later, >= 6000 ms apart,
+    same-heading (< 20 deg) neighbour within 1.5 m of the driving line."""
+    cx, cy, _, cs, a1 = pts[i]
+    for j in row:
+        x2, y2, _, s2, a2 = pts[j]
+        if s2 <= cs or abs(cs - s2) < 6000:
+            continue
+        if abs(a1 - a2) >= 20.0:
+            continue
+        avg = ((a1 + a2) / 2.0 - 90) / 180.0 * math.pi
+        k = math.tan(avg)
+        b = cy - k * cx
+        if abs(0 - k * x2 + y2 - b) / math.sqrt(k * k + 1) > 1.5:
+            continue
+        return s2
+    return None
+
+
+def get_overlap_stamp(ctx, poses, stamps):
+    """-> [(base_start, base_end, frame_start, frame_end)] stamps of the overlapping segments."""
+    pts = _d_rots(poses, stamps)
+    if not pts:
+        return []
+    xyz = torch.tensor([p[:3] for p in pts], dtype=torch.float64, device=ctx.device)
+    ix = ops.GridIndex(ctx, xyz)
+    offs, idx, _ = ops.radius(ix, xyz, 10.0)  # kd_tree.radiusSearch(cur_p, 10, ...) for every point
+    offs, idx = offs.cpu().numpy(), idx.cpu().numpy()
+    ix.close()
+    pair_vec = []
+    for i in range(len(pts)):
+        s2 = _first_pair(pts, i, idx[offs[i]:offs[i + 1]])
+        if s2 is not None:
+            pair_vec.append((pts[i][3], s2))
+    return _segments(pair_vec)
+
+
+def find_reliable(ctx, rots, load_cloud, icp_threshold):
+    """rots: list of dicts {matrix (4x4), stamp, icperr}; load_cloud(stamp) -> (n, 48) uint8 device
+    cloud.  Returns the is_valid flags (main_blend.cpp:327-380, dis_threshold 0.06)."""
+    valid = [False] * len(rots)
+    for i in range(1, len(rots) - 1):
+        e0, e1, e2 = rots[i - 1]["icperr"], rots[i]["icperr"], rots[i + 1]["icperr"]
+        if not (e1 >= 0 and e1 <= icp_threshold and e0 >= 0 and e2 >= 0):
+            continue
+        left, right, centre = (load_cloud(rots[k]["stamp"]) for k in (i - 1, i + 1, i))
+        ix = ops.GridIndex(ctx, centre)
+        dis = []
+        for cloud, (ma, mb) in ((left, (i - 1, i)), (right, (i, i + 1))):
+            q, _ = ops.nearest_query(ix, cloud)
+            # the default CloudItem when no query beats 9999 (x = y = z = 0, data[3] = 1)
+            p = np.array([0.0, 0.0, 0.0, 1.0])
+            if q >= 0:
+                p = cloud[q].cpu().numpy().view(np.float64)[:4].copy()
+            ta = np.asarray(rots[ma]["matrix"], dtype=np.float64) @ p
+            tb = np.asarray(rots[mb]["matrix"], dtype=np.float64) @ p
+            dis.append(math.pow(ta[0] - tb[0], 2) + math.pow(ta[1] - tb[1], 2) + math.pow(ta[2] - tb[2], 2))
+        ix.close()
+        if dis[0] < 0.06 and dis[1] < 0.06:
+            valid[i] = True
+    return valid

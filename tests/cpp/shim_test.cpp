@@ -306,7 +306,35 @@ static void test_pcd_io() {  // pcd_helper.h writeBinary / writeBinaryCompressed
     }
 }
 
+static void test_batched_callers() {  // point_cloud_closure.cpp:44-180, main_blend.cpp:306-380
+    std::vector<CloudStampRot> line;
+    uint64_t t = 1000000;
+    for (int lap = 0; lap < 2; lap++) {
+        for (int k = 0; k < 300; k++) {
+            CloudStampRot r;
+            r._stamp = t;
+            r._rot = Mat4d::Identity();
+            r._rot(0, 3) = 0.5 * k + 0.2 * lap;
+            r._rot(1, 3) = 0.01 * (k % 7) + 0.3 * lap;
+            line.push_back(r);
+            t += 100;
+        }
+        t += 60000;
+    }
+    std::vector<PointCloudClosure::same_segment> segs;
+    PointCloudClosure::get_overlap_stamp(line, segs);
+    CHECK(!segs.empty() && segs[0].base_start_stamp < segs[0].frame_start_stamp, "overlap segments %zu", segs.size());
+    CloudPtr c = random_cloud(5000, 41, 10.0);
+    KdTreeFLANN<CloudItem> tree;
+    tree.setInputCloud(c);
+    CloudPtr q = random_cloud(300, 42, 10.0);
+    q->points[123] = c->points[7];
+    const CloudItem best = find_cloud_nearest_point_in_kdtree(q, tree);
+    CHECK(best.x == c->points[7].x && best.y == c->points[7].y, "nearest query point");
+}
+
 int main() {
+    test_batched_callers();
     test_pcd_io();
     test_pose_lines();
     test_cloud_grid();
