@@ -104,7 +104,7 @@ const void* pcp_index_sorted_points(const pcp_index* index);
 /* Batch KdTreeFLANN::nearestKSearch (kd_tree.h:814-845), exact fp64: k clamped to the
  * index size, rows ascending by (d2, internal j), d2 = ((0+d0^2)+d1^2)+d2^2 (FLANN
  * L2_Simple<double>), indices mapped through index_mapping_.  Outputs are nq*k; entries
- * past the clamped k are -1 / +inf.  Per-query output count in out_n_dev (optional). */
+ * past the clamped k are -1 / +inf.  out_d2_dev may be NULL (indices only). */
 int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_stride_bytes,
             int64_t nq, int k, int32_t* out_idx_dev, double* out_d2_dev);
 
@@ -219,6 +219,18 @@ int pcp_normals_rpca(pcp_ctx* ctx, const double* xyz_dev, size_t stride_bytes, i
 int pcp_plane_fit_segments(pcp_ctx* ctx, const double* xyz_dev, size_t stride_bytes,
                            const int64_t* offsets_dev, const int32_t* idx_dev, int64_t nseg,
                            pcp_plane* out_dev);
+
+/* Region growing over rpca planes: TreeExtration::region_growning (extraction_tree.cpp:66-272,
+ * live body :177-271) as point_segment calls it (static.cpp:8-21).  index: fp64 index over the
+ * n points of xyz_dev (kdtree.setInputCloud(Cloud)); props_dev: the n records of
+ * pcp_normals_rpca, whose segment_id is rewritten (-1 = UNSEGMENTATION).  Kept segments, in
+ * label order: segment s = seg_points_host[seg_offsets_host[s] .. seg_offsets_host[s+1]) in
+ * the reference's push order, seeded by point seg_seeds_host[s] (its normal and Distance are
+ * the PlanSegment's).  Buffers: seg_offsets n+1, seg_points n, seg_seeds n (host). */
+int pcp_region_growing(pcp_ctx* ctx, const pcp_index* index, const double* xyz_dev, size_t stride_bytes, int64_t n,
+                       pcp_point_property* props_dev, double distance_t, double cosfa_t,
+                       int64_t* seg_offsets_host, int32_t* seg_points_host, int32_t* seg_seeds_host,
+                       int64_t* n_seg);
 
 /* ----------------------------------------------------------------------- I: ICP */
 /* ICP correspondence/transform loop (point_cloud_helper.cpp:75-166 get_rot_icp ->

@@ -752,6 +752,102 @@ private:
     }
 };
 
+// ------------------------------------------------------------------ F: TreeExtration (region growing)
+class TreeExtration {  // extraction_tree.h (the region-growing members)
+public:
+    // extraction_tree.cpp:36-44 (float arithmetic, cmath's float sqrt)
+    float compute_included_angle_between_vector(float vx1, float vy1, float vz1, float vx2, float vy2, float vz2) {
+        const float n_n1 = vx1 * vx2 + vy1 * vy2 + vz1 * vz2;
+        const float n_n = std::sqrt(vx1 * vx1 + vy1 * vy1 + vz1 * vz1);
+        const float n1_n1 = std::sqrt(vx2 * vx2 + vy2 * vy2 + vz2 * vz2);
+        return std::abs(n_n1 / (n_n * n1_n1));
+    }
+    // extraction_tree.cpp:47-64
+    float compute_distance_from_point_to_plane(const CloudItem* a_point, float a, float b, float c, float d) {
+        const float x1 = (float)a_point->x, y1 = (float)a_point->y, z1 = (float)a_point->z;
+        const double g = std::sqrt(a * a + b * b + c * c);
+        const double f1 = a * x1, f2 = b * y1, f3 = c * z1, f4 = d;
+        return (float)(std::abs(f1 + f2 + f3 + f4) / g);
+    }
+    // extraction_tree.cpp:66-272 through pcp_region_growing (kNN(50) graph and the plane test on
+    // the GPU, the sequential seed walk on the host).  PointProperty's SegmentID is rewritten,
+    // as in the reference (shared array).  radius is unused, as in the reference.
+    std::vector<PlanSegment> region_growning(std::shared_ptr<LAS_POINT_PROPERTY> PointProperty, CloudPtr& Cloud,
+                                             double distanceT, double /*radius*/, double cosfaT) {
+        std::vector<PlanSegment> out;
+        const size_t n = Cloud ? Cloud->points.size() : 0;
+        if (!n) return out;
+        KdTreeFLANN<CloudItem> tree;
+        tree.setInputCloud(Cloud);
+        std::vector<int64_t> off(n + 1);
+        std::vector<int32_t> pts(n), seeds(n);
+        int64_t nseg = 0;
+        {
+            pcp_ctx* c = detail::Device::get().ctx();
+            std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
+            detail::DevBuf props;
+            props.upload(PointProperty.get(), n * sizeof(LAS_POINT_PROPERTY));
+            detail::check(pcp_region_growing(c, tree.index(), tree.device_cloud(), sizeof(CloudItem), (int64_t)n,
+                                             (pcp_point_property*)props.ptr(), distanceT, cosfaT, off.data(),
+                                             pts.data(), seeds.data(), &nseg),
+                          c, "pcp_region_growing");
+            props.download(PointProperty.get(), n * sizeof(LAS_POINT_PROPERTY));
+        }
+        out.resize((size_t)nseg);
+        for (int64_t s = 0; s < nseg; s++) {
+            PlanSegment& t = out[s];
+            const LAS_POINT_PROPERTY& sp = PointProperty.get()[seeds[s]];
+            t.SegmentID = (unsigned short)s;
+            t.PointID.assign(pts.begin() + off[s], pts.begin() + off[s + 1]);
+            t.normal_x = sp.normal_x;
+            t.normal_y = sp.normal_y;
+            t.normal_z = sp.normal_z;
+            t.Distance = (float)sp.Distance;
+        }
+        return out;
+    }
+};
+
+// static.cpp:8-21
+inline void point_segment(CloudPtr src_cloud, std::vector<PlanSegment>& Segment, uint64_t seed = 0) {
+    const double radius = 0.15, cosfa_t = 0.940, distance_t = 0.5, radius_in_growning = 0.2;
+    const float pr = 0.99f, epi = 0.5f;
+    CalculateFeature Feature;
+    std::shared_ptr<LAS_POINT_PROPERTY> PointProperty = Feature.calculate_plan_parameter_rpca(src_cloud, radius, pr,
+                                                                                               epi, seed);
+    TreeExtration Tree;
+    Segment = Tree.region_growning(PointProperty, src_cloud, distance_t, radius_in_growning, cosfa_t);
+}
+// static.cpp:24-36
+inline void tree_filter(CloudPtr src_cloud, CloudPtr dst_cloud) {
+    std::vector<PlanSegment> Segment;
+    point_segment(src_cloud, Segment);
+    for (const PlanSegment& s : Segment)
+        if (s.PointID.size() > 50)
+            for (int j : s.PointID) dst_cloud->push_back(src_cloud->points[j]);
+}
+// static.cpp:37-52
+inline void shaft_filter(CloudPtr src_cloud, CloudPtr dst_cloud) {
+    std::vector<PlanSegment> Segment;
+    point_segment(src_cloud, Segment);
+    Cloud tmp;
+    for (const PlanSegment& s : Segment)
+        if (std::abs(s.normal_z) < 0.30)
+            for (int j : s.PointID) tmp.push_back(src_cloud->points[j]);
+    *dst_cloud = tmp;
+}
+// static.cpp:55-79
+inline void ground_filter(CloudPtr src_cloud, CloudPtr dst_cloud) {
+    std::vector<PlanSegment> Segment;
+    point_segment(src_cloud, Segment);
+    std::vector<uint8_t> ground(src_cloud->points.size(), 0);
+    for (const PlanSegment& s : Segment)
+        if (std::abs(s.normal_z) > 0.9)
+            for (int j : s.PointID) ground[j] = 1;
+    for (size_t k = 0; k < src_cloud->points.size(); k++)
+        if (!ground[k]) dst_cloud->push_back(src_cloud->points[k]);
+}
+
 // ------------------------------------------------------------------ I4: CloudStampRot
 class CloudStampRot {  // cloud_stamp_rot.h:7-39 (pose record; composition stays on the host)
 public:

@@ -52,6 +52,7 @@ SIGNATURES = [
     ("pcp_nearest_query", _i32, [_vp, _vp, _vp, _sz, _i64, _f64, _vp, _vp]),
     ("pcp_normals_rpca", _i32, [_vp, _vp, _sz, _i64, _vp, _i32, _f32, _f32, C.c_uint64, _vp]),
     ("pcp_plane_fit_segments", _i32, [_vp, _vp, _sz, _vp, _vp, _i64, _vp]),
+    ("pcp_region_growing", _i32, [_vp, _vp, _vp, _sz, _i64, _vp, _f64, _f64, _vp, _vp, _vp, _P(_i64)]),
     ("pcp_knn_lod", _i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp]),
     ("pcp_minmax_aos48", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _P(_f64)]),
     ("pcp_centroid_aos48", _i32, [_vp, _vp, _i64, _i32, _P(_f64), _P(_u32)]),

@@ -6,6 +6,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
+#include <set>
 #include <random>
 #include <vector>
 
@@ -333,7 +335,85 @@ static void test_batched_callers() {  // point_cloud_closure.cpp:44-180, main_bl
     CHECK(best.x == c->points[7].x && best.y == c->points[7].y, "nearest query point");
 }
 
+// extraction_tree.cpp:177-271 restated literally over the shim's single-query nearestKSearch:
+// the batched region_growning must produce the same segments, order and SegmentIDs
+static void test_region_growing() {
+    CloudPtr c(new Cloud);
+    std::mt19937 rng(77);
+    std::uniform_real_distribution<double> u(0.0, 4.0), e(-0.004, 0.004);
+    for (int i = 0; i < 2500; i++) {  // ground, a wall and a scatter of clutter, interleaved
+        CloudItem p{};
+        const int kind = i % 5;
+        if (kind < 3) { p.x = u(rng); p.y = u(rng); p.z = e(rng); }
+        else if (kind == 3) { p.x = 4.0 + e(rng); p.y = u(rng); p.z = u(rng) * 0.5; }
+        else { p.x = u(rng); p.y = u(rng); p.z = 0.3 + u(rng) * 0.3; }
+        c->push_back(p);
+    }
+    CalculateFeature F;
+    std::shared_ptr<LAS_POINT_PROPERTY> props = F.calculate_plan_parameter_rpca(c, 0.15, 0.99f, 0.5f, 5);
+    const size_t n = c->points.size();
+    std::vector<LAS_POINT_PROPERTY> ref(props.get(), props.get() + n);
+    TreeExtration T;
+    std::vector<PlanSegment> got = T.region_growning(props, c, 0.5, 0.2, 0.94);
+
+    KdTreeFLANN<CloudItem> tree;
+    tree.setInputCloud(c);
+    std::vector<PlanSegment> want;
+    std::set<int> unseg;
+    for (size_t i = 0; i < n; i++) { unseg.insert((int)i); ref[i].SegmentID = -1; }
+    std::deque<int> seed;
+    int label = 0;
+    std::vector<int> ki;
+    std::vector<double> kd;
+    while (!unseg.empty()) {
+        const int m = *unseg.begin();
+        unseg.erase(m);
+        if (!(ref[m].curvature < 0.005)) continue;
+        PlanSegment s;
+        ref[m].SegmentID = label;
+        s.PointID.push_back(m);
+        seed.push_back(m);
+        const double nx = ref[m].normal_x, ny = ref[m].normal_y, nz = ref[m].normal_z;
+        while (!seed.empty()) {
+            const int p = seed.front();
+            seed.pop_front();
+            const int N = tree.nearestKSearch(c->points[ref[p].PointID], 50, ki, kd);
+            for (int i = 0; i < N; i++) {
+                if (ref[ki[i]].SegmentID != -1) continue;
+                const float cs = T.compute_included_angle_between_vector(nx, ny, nz, ref[ki[i]].normal_x,
+                                                                         ref[ki[i]].normal_y, ref[ki[i]].normal_z);
+                const float dis = T.compute_distance_from_point_to_plane(&c->points[ki[i]], ref[p].normal_x,
+                                                                         ref[p].normal_y, ref[p].normal_z,
+                                                                         (float)ref[p].Distance);
+                if (cs > 0.94 && dis < 0.5) {
+                    ref[ki[i]].SegmentID = label;
+                    s.PointID.push_back(ki[i]);
+                    unseg.erase(ki[i]);
+                    seed.push_back(ki[i]);
+                }
+            }
+        }
+        if (s.PointID.size() > 5) {
+            s.normal_z = (float)nz;
+            want.push_back(s);
+            label++;
+        } else {
+            for (int j : s.PointID) ref[j].SegmentID = -1;
+        }
+    }
+    CHECK(got.size() == want.size() && !want.empty(), "segments %zu vs %zu", got.size(), want.size());
+    for (size_t s = 0; s < got.size() && s < want.size(); s++)
+        CHECK(got[s].PointID == want[s].PointID && got[s].normal_z == want[s].normal_z, "segment %zu differs", s);
+    int bad = 0;
+    for (size_t i = 0; i < n; i++) bad += props.get()[i].SegmentID != ref[i].SegmentID;
+    CHECK(bad == 0, "%d SegmentIDs differ", bad);
+    CloudPtr ground(new Cloud);
+    ground_filter(c, ground);
+    CHECK(ground->size() < n, "ground_filter kept %zu of %zu", ground->size(), n);
+}
+
 int main() {
+    test_region_growing();
     test_batched_callers();
     test_pcd_io();
     test_pose_lines();
