@@ -19,6 +19,10 @@
 #include "grid.hpp"
 #include "wave_acc.hpp"
 
+#ifndef PCP_OCT_GLIST  // lanes per query of the octant pass over the verify pass's search lists
+#define PCP_OCT_GLIST 0  // 0: by the list's density (octant_lanes)
+#endif
+
 struct pcp_icp {
     pcp_ctx* ctx = nullptr;
     const pcp_index* target = nullptr;
@@ -52,6 +56,8 @@ struct pcp_icp {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-launch timing events (device loop)
     size_t ntev = 0;              // pairs recorded since the last pcp_icp_kernel_ms
     int dbg = 0;                  // PCP_ICP_ABLATE flags (profiling only)
+    int oct_g_first = 1;          // lanes per query of the octant pass: first launch (all queries)
+    int oct_g_list = PCP_OCT_GLIST;  // ... and the verify pass's search lists (PCP_OCT_G=first,list)
     unsigned long long* dbgcnt = nullptr;  // kDbgCount: [candidates, rows, queries]
     uint2* dbgfz = nullptr;       // kDbgCount: per 64-query chunk {slack bits, launch} (freeze model)
     double last_ms = 0.0;
@@ -110,6 +116,7 @@ struct IcpArgs {
     int64_t nseg;       // fallback segments (= waves of the octant kernel)
     int ring_all;       // ring kernel: process every query (sparse grid) instead of the list
     int dbg;            // ablation flags (PCP_ICP_ABLATE, profiling builds of the bench only)
+    int oct_g;          // octant pass lanes per query: 1, 2, 4, 8, or 0 = by the list's density
     const float* pose;  // device poses (current, previous: 24 floats) overriding R/t, Rp/tq, or null
     unsigned long long* dbgcnt;  // kDbgCount counters, or null
     uint2* dbgfz;       // kDbgCount: chunk freeze model state
@@ -804,30 +811,60 @@ struct Top3P {
     }
     // the wave's lists with a uniform trip count (lanes past their own list read the far
     // sentinel: d2 = inf, never kept), U loads per step, the next step's loads issued before
-    // this step's keys are formed (software pipeline: two batches in flight)
+    // this step's keys are formed (software pipeline: two batches in flight).  With G lanes per
+    // query, lane `sub` of the group takes list entries sub, sub + G, sub + 2G, ...: the group's
+    // loads of one step are G consecutive records of a row (one or two cache lines), so a wave
+    // instruction touches ~64 / G lines instead of 64 (what bounds the sparse search lists).
+    template <int G>
     __device__ __forceinline__ void scan4(const float4* pts, uint32_t sent, const uint32_t (&rs)[4],
-                                          const uint32_t (&rn)[4], uint32_t Lw, float qx, float qy, float qz) {
+                                          const uint32_t (&rn)[4], uint32_t Lw, float qx, float qy, float qz,
+                                          uint32_t sub) {
         const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
         const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
-        auto addr = [=](uint32_t v) { return cat_addr_l(v, c1, c2, c3, L, o0, o1, o2, o3, sent); };
+        auto lv = [=](uint32_t v) { return v * G + sub; };  // this lane's v-th list entry
+        auto addr = [=](uint32_t v) { return cat_addr_l(lv(v), c1, c2, c3, L, o0, o1, o2, o3, sent); };
+        const uint32_t Lg = (Lw + G - 1) / G;
         constexpr int U = 4;
         float4 A[U], B[U];
 #pragma unroll
         for (int u = 0; u < U; u++) A[u] = ld16(pts, addr(u));
-        for (uint32_t v = 0; v < Lw; v += 2 * U) {
+        for (uint32_t v = 0; v < Lg; v += 2 * U) {
             // two register sets, no copies: B's loads are in flight while A's keys are formed
 #pragma unroll
             for (int u = 0; u < U; u++) B[u] = ld16(pts, addr(v + U + u));
             __builtin_amdgcn_sched_barrier(0);  // keep B's loads ahead of A's keys
 #pragma unroll
-            for (int u = 0; u < U; u++) consider(qx, qy, qz, A[u], v + u);
-            if (v + U >= Lw) break;
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, A[u], lv(v + u));
+            if (v + U >= Lg) break;
 #pragma unroll
             for (int u = 0; u < U; u++) A[u] = ld16(pts, addr(v + 2 * U + u));
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int u = 0; u < U; u++) consider(qx, qy, qz, B[u], v + U + u);
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, B[u], lv(v + U + u));
         }
+    }
+    // the G lanes of a query merge their 4 smallest keys: per butterfly step the 4 smallest of
+    // two ascending lists are min(t_i, u_{3-i}) (a bitonic sequence), sorted by two stages of
+    // compare-exchange.  Keys of one query are distinct (the list index is in the low byte)
+    // except kKeyMax.  Afterwards every lane of the group holds the group's t0..t3.
+    template <int G>
+    __device__ __forceinline__ void merge_group() {
+#pragma unroll
+        for (int s = 1; s < G; s <<= 1) {
+            const uint32_t u0 = xor_lane(t0, s), u1 = xor_lane(t1, s), u2 = xor_lane(t2, s), u3 = xor_lane(t3, s);
+            const uint32_t c0 = min(t0, u3), c1 = min(t1, u2), c2 = min(t2, u1), c3 = min(t3, u0);
+            const uint32_t l02 = min(c0, c2), h02 = max(c0, c2), l13 = min(c1, c3), h13 = max(c1, c3);
+            t0 = min(l02, l13);
+            t1 = max(l02, l13);
+            t2 = min(h02, h13);
+            t3 = max(h02, h13);
+        }
+    }
+    // lane ^ s inside a quad by DPP quad_perm (s = 1, 2), else a bpermute
+    __device__ __forceinline__ static uint32_t xor_lane(uint32_t v, int s) {
+        if (s == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // [1,0,3,2]
+        if (s == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+        return (uint32_t)__shfl_xor((int)v, s, 64);
     }
 };
 
@@ -867,11 +904,13 @@ __device__ __forceinline__ void take_exact(OctResult& o, const float4 p, uint32_
     o.wz = t ? p.z : o.wz;
 }
 
-// packed-key scan (every lane's list < 256 candidates)
+// packed-key scan (every lane's list < 256 candidates); G lanes per query share its list
+template <int G>
 __device__ __forceinline__ OctResult octant_packed(const IcpArgs& a, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
-                                                   uint32_t Lw, float qx, float qy, float qz) {
+                                                   uint32_t Lw, float qx, float qy, float qz, uint32_t sub) {
     Top3P k;
-    k.scan4(a.tp, a.ntp, rs, rn, Lw, qx, qy, qz);
+    k.scan4<G>(a.tp, a.ntp, rs, rn, Lw, qx, qy, qz, sub);
+    k.merge_group<G>();
     const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
     const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
     OctResult o;
@@ -907,31 +946,37 @@ __device__ __noinline__ OctResult octant_exact(const IcpArgs& a, uint32_t rs0, u
     return o;
 }
 
-__global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a, const int32_t* list,
-                                                                          const uint32_t* list_n) {
-    load_pose(a);
-    constexpr int kW = kIcpBlock / 64;
-    __shared__ double s_acc[kW][kAcc];
+// G lanes per query (G = 1: one query per lane; G > 1: the G lanes of a group split the query's
+// list, merge their keys, and only the group's first lane writes, accumulates and lists).  A
+// chunk is 64 / G queries.  G > 1 serves the sparse search lists of later launches, whose
+// lanes no longer share candidate lines.
+constexpr int kOctW = kIcpBlock / 64;
+template <int G>
+__device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list, int64_t n,
+                                           double (*s_acc)[kAcc]) {
+    constexpr int kW = kOctW;
+    constexpr int QPC = 64 / G;  // queries per chunk
     const GridDesc& g = a.g;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int slot = lane / G;
+    const uint32_t sub = (uint32_t)(lane % G);
+    const bool lead = sub == 0;
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;  // global wave id = fallback segment
-    const int64_t n = list ? (int64_t)*list_n : a.nq;
-    if (lane < kAcc) s_acc[wid][lane] = 0.0;
     uint32_t fbn = 0;  // wave-uniform count of this wave's fallback entries
     const int64_t nwaves = (int64_t)gridDim.x * kW;
     int64_t in_ = 0;
     float4 qn = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (gw * 64 + lane < n) {
-        in_ = list ? (int64_t)list[gw * 64 + lane] : gw * 64 + lane;
+    if (gw * QPC + slot < n) {
+        in_ = list ? (int64_t)list[gw * QPC + slot] : gw * QPC + slot;
         qn = a.q[in_];
     }
-    for (int64_t c = gw; c * 64 < n; c += nwaves) {  // grid-stride (an XCD split measured slower here)
-        const int64_t j = c * 64 + lane;
+    for (int64_t c = gw; c * QPC < n; c += nwaves) {  // grid-stride (an XCD split measured slower here)
+        const int64_t j = c * QPC + slot;
         const bool valid = j < n;
         const int64_t i = in_;
         const float4 qraw = qn;
-        if (j + 64 * nwaves < n) {  // prefetch the next chunk's query
-            in_ = list ? (int64_t)list[j + 64 * nwaves] : j + 64 * nwaves;
+        if (j + QPC * nwaves < n) {  // prefetch the next chunk's query
+            in_ = list ? (int64_t)list[j + QPC * nwaves] : j + QPC * nwaves;
             qn = a.q[in_];
         }
         float qx = 0.f, qy = 0.f, qz = 0.f, fx = 0.f, fy = 0.f, fz = 0.f, dout = 0.f;
@@ -969,11 +1014,11 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         OctResult o;
         if (!(a.dbg & kDbgNoScan)) {
             if (Lw <= kMaxOctList)
-                o = octant_packed(a, rs, rn, Lw, qx, qy, qz);
+                o = octant_packed<G>(a, rs, rn, Lw, qx, qy, qz, sub);
             else
                 o = octant_exact(a, rs[0], rs[1], rs[2], rs[3], rn[0], rn[1], rn[2], rn[3], qx, qy, qz);
         }
-        if (a.dbg & kDbgCount) {
+        if ((a.dbg & kDbgCount) && lead) {
             atomicAdd(a.dbgcnt, (unsigned long long)len);
             atomicAdd(a.dbgcnt + 2, 1ull);
             if (Lw > kMaxOctList) atomicAdd(a.dbgcnt + 3, 1ull);
@@ -1003,10 +1048,10 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             // octant's first uncached d2 instead.
             const float D = outside ? dout * 0.9999f
                                     : (settled ? fminf(sqrtf(o.dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : o.dnext);
-            a.cand[i] = make_uint4(o.c0, o.c1, o.c2, pack_dlb(D, a.launch));
+            if (lead) a.cand[i] = make_uint4(o.c0, o.c1, o.c2, pack_dlb(D, a.launch));
         }
         // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
-        const bool fb = valid && !settled;
+        const bool fb = valid && lead && !settled;
         const uint64_t fbm = __ballot(fb);
         if (fb) {
             const uint32_t pos = fbn + __builtin_amdgcn_mbcnt_hi((uint32_t)(fbm >> 32),
@@ -1014,7 +1059,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
             a.fb[gw * a.fb_seg + pos] = (int32_t)i;
         }
         fbn += (uint32_t)__popcll(fbm);
-        const bool acc_ok = valid && settled && found && !(a.dbg & kDbgNoAccum);
+        const bool acc_ok = valid && lead && settled && found && !(a.dbg & kDbgNoAccum);
         const Best w{o.d0, 0, o.win, o.wx, o.wy, o.wz};
         chunk_accumulate(acc_ok, qx, qy, qz, w, s_acc[wid], lane);
     }
@@ -1023,6 +1068,33 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
         a.fb_off[gw] = fbn;  // scanned in place into the segment offsets
         if (gw == 0) a.fb_off[a.nseg] = 0u;
     }
+}
+
+// Lanes per query by the list's density (measured per launch on the C4 bench registration,
+// tools/gpu_octg_ab.sh): dense lists share candidate lines between neighbouring queries and
+// want one lane each; sparse ones want the group form.
+__device__ __forceinline__ int octant_lanes(int64_t n, int64_t nq) {
+    if (n * 100 > nq * 36) return 1;
+    if (n * 100 > nq * 17) return 2;
+    return 4;
+}
+
+__global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a, const int32_t* list,
+                                                                          const uint32_t* list_n) {
+    load_pose(a);
+    __shared__ double s_acc[kOctW][kAcc];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t n = list ? (int64_t)*list_n : a.nq;
+    if (lane < kAcc) s_acc[wid][lane] = 0.0;
+    const int G = a.oct_g ? a.oct_g : octant_lanes(n, a.nq);  // uniform over the grid
+    if (G == 1)
+        octant_run<1>(a, list, n, s_acc);
+    else if (G == 2)
+        octant_run<2>(a, list, n, s_acc);
+    else if (G == 4)
+        octant_run<4>(a, list, n, s_acc);
+    else
+        octant_run<8>(a, list, n, s_acc);
     write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
 }
 
@@ -1603,9 +1675,12 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
         if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_ver, ctx->stream));
         // 2. octant search of the list (every query at the first launch); unsettled -> fallback list
         a.partials = part_o;
-        hipLaunchKernelGGL(k_icp_octant, dim3(icp->nb_fast), dim3(kIcpBlock), 0, ctx->stream, a,
-                           verify ? (const int32_t*)icp->svc : nullptr,
-                           verify ? (const uint32_t*)(icp->sv_off + a.nseg_v) : nullptr);
+        {
+            const int32_t* lst = verify ? (const int32_t*)icp->svc : nullptr;
+            const uint32_t* lst_n = verify ? (const uint32_t*)(icp->sv_off + a.nseg_v) : nullptr;
+            a.oct_g = verify ? icp->oct_g_list : icp->oct_g_first;
+            hipLaunchKernelGGL(k_icp_octant, dim3(icp->nb_fast), dim3(kIcpBlock), 0, ctx->stream, a, lst, lst_n);
+        }
     } else {
         PCP_HIP(ctx, hipMemsetAsync(part_v, 0, (size_t)(icp->nb_ver + icp->nb_fast) * kAcc * sizeof(double),
                                     ctx->stream));
@@ -1803,6 +1878,14 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
                 hipEventCreate(&icp->ev_mid) != hipSuccess || hipEventCreate(&icp->ev_ver) != hipSuccess))
         rc = pcp::set_error(ctx, PCP_ERR_HIP, "hipEventCreate failed");
     if (const char* ab = std::getenv("PCP_ICP_ABLATE")) icp->dbg = std::atoi(ab);
+    if (const char* og = std::getenv("PCP_OCT_G")) {  // A/B: lanes per query, "first,list"
+        int f = 1, l = 1;
+        if (std::sscanf(og, "%d,%d", &f, &l) == 2) {
+            auto ok = [](int v) { return v == 1 || v == 2 || v == 4 || v == 8; };
+            if (ok(f) || f == 0) icp->oct_g_first = f;
+            if (ok(l) || l == 0) icp->oct_g_list = l;
+        }
+    }
     if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgcnt, 32);
     if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgfz, icp->nq / 64 + 2);
     if (!rc && icp->dbgfz && hipMemsetAsync(icp->dbgfz, 0, (icp->nq / 64 + 2) * sizeof(uint2), ctx->stream) != hipSuccess)
