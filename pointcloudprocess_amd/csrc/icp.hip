@@ -415,7 +415,18 @@ __device__ __forceinline__ void write_wave_partials(double (*s_acc)[kAcc], doubl
 // kFlush chunks (and at the end) the wave reduces them with DPP adds and lane 0 un-centres the
 // totals in fp64 into the wave's LDS accumulators.  A stretch is at most kFlush * 64
 // consecutive sorted queries (a few metres), so the centred fp32 products stay small.
-constexpr int kFlush = 32;
+#ifndef PCP_KFLUSH
+#define PCP_KFLUSH 32
+#endif
+constexpr int kFlush = PCP_KFLUSH;
+#ifndef PCP_FLUSH_INLINE  // 1: inline the stretch flush (no call frame spilled to scratch)
+#define PCP_FLUSH_INLINE 1
+#endif
+#if PCP_FLUSH_INLINE
+#define PCP_FLUSH_ATTR __attribute__((always_inline))
+#else
+#define PCP_FLUSH_ATTR __attribute__((noinline))
+#endif
 struct LaneAcc {
     float v[kAcc - 1];  // n, A(3), B(3), AB(9), AA(6), D  (centred on c)
     __device__ __forceinline__ void zero() {
@@ -442,7 +453,7 @@ struct LaneAcc {
     }
     // whole wave (full EXEC): totals -> S (fp64, un-centred by lane 0).  Not inlined: it runs once
     // per kFlush chunks, and its fp64 temporaries would otherwise raise the loop's register count.
-    __device__ __attribute__((noinline)) void flush(double* S, int lane, float cx, float cy, float cz) {
+    __device__ PCP_FLUSH_ATTR void flush(double* S, int lane, float cx, float cy, float cz) {
 #if PCP_WAVE_ACC
         wave_accumulate(v, S, lane, cx, cy, cz);
 #else
