@@ -26,6 +26,12 @@ namespace pcp {
 namespace {
 
 constexpr int kB = 256;
+#ifndef PCP_H16_BATCH  // candidate records loaded per batch in the row passes
+#define PCP_H16_BATCH 4
+#endif
+#ifndef PCP_H16_NOSTORE  // profiling variant: the fill pass without its row stores
+#define PCP_H16_NOSTORE 0
+#endif
 
 __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
     const _Float16 ha = (_Float16)a, hb = (_Float16)b;
@@ -61,10 +67,58 @@ struct H16Args {
 };
 
 // one lane per sorted point; halo points (caller index >= n_owned) are not queries
+// the id each sorted point is reported under (the global id of its caller index, or that index):
+// gathered once per point here instead of once per neighbour in the fill pass
+__global__ void k_h16_ids(const int32_t* mapping, const int32_t* gid, int64_t n, int32_t* out) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t m = mapping[k];
+        out[k] = gid ? gid[m] : m;
+    }
+}
+
+// Row staging for the fill pass.  Lanes are sorted points, whose caller rows lie far apart: a
+// lane-per-row store stream touches 64 lines per instruction and leaves lines half-written
+// in L2 (measured: the stores were 13 of the fill pass's 22 ms at 25M points).  So the fill
+// writes the rows in sorted order (adjacent lanes, adjacent rows), and one copy pass moves them
+// to caller order with full-line writes.
+__global__ void k_h16_sorted_counts(const int32_t* mapping, int64_t n, int64_t n_owned, const int64_t* offsets,
+                                    int32_t* cnt_s, int32_t* inv) {
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t c = mapping[s];
+        const bool own = c < n_owned;
+        cnt_s[s] = own ? (int32_t)((offsets[c + 1] - offsets[c] + 3) & ~3ll) : 0;  // 16-byte aligned rows
+        if (own) inv[c] = (int32_t)s;
+    }
+}
+// one wave per 64 consecutive caller rows: lane r fetches row r's source / destination, then
+// the wave copies the rows one after the other (coalesced reads and writes)
+__global__ __launch_bounds__(kB) void k_h16_rows_to_caller(const int32_t* inv, int64_t n_owned, const int64_t* soff,
+                                                           const int64_t* offsets, const int32_t* tmp,
+                                                           int32_t* out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t w = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); w * 64 < n_owned; w += nw) {
+        const int64_t c = w * 64 + lane;
+        int64_t src = 0, dst = 0, len = 0;
+        if (c < n_owned) {
+            dst = offsets[c];
+            len = offsets[c + 1] - dst;
+            src = soff[inv[c]];
+        }
+        const int rows = (int)min((int64_t)64, n_owned - w * 64);
+        for (int r = 0; r < rows; r++) {
+            const int64_t rs = __shfl(src, r, 64), rd = __shfl(dst, r, 64), rl = __shfl(len, r, 64);
+            for (int64_t t = lane; t < rl; t += 64) out[rd + t] = tmp[rs + t];
+        }
+    }
+}
+
 template <bool FILL>
-__global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, const int64_t* offsets,
-                                                   const int32_t* gid, int32_t* out_idx, pcp_plane* out_nrm) {
+__global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, const int64_t* __restrict__ offsets,
+                                                   const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
+                                                   pcp_plane* __restrict__ out_nrm) {
     const GridDesc& g = a.g;
+    const uint2* __restrict__ rec = a.rec;
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < a.n; s += (int64_t)gridDim.x * blockDim.x) {
         const int32_t caller = a.mapping[s];
         if (caller >= a.n_owned) continue;
@@ -79,8 +133,9 @@ __global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, co
         const float gyl = fmaxf(qy, 0.f), gyr = fmaxf(a.hf - qy, 0.f);
         const float gzl = fmaxf(qz, 0.f), gzr = fmaxf(a.hf - qz, 0.f);
         int64_t o = 0;
-        if (FILL) o = offsets[caller];
+        if (FILL) o = offsets[s];  // the sorted-order staging rows
         uint32_t cnt = 0;
+        int32_t sink = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
         float S0 = 0.f, S1 = 0.f, S2 = 0.f, S00 = 0.f, S01 = 0.f, S02 = 0.f, S11 = 0.f, S12 = 0.f, S22 = 0.f;
         for (int dz = -1; dz <= 1; dz++) {
             const int z = cz + dz;
@@ -98,26 +153,53 @@ __global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, co
                 const uint32_t k0 = g.cstart[c0], k1 = g.cstart[c0 + (xb - xa + 1)];
                 const uint32_t b1 = g.cstart[cq], b2 = g.cstart[cq + 1];  // the query's x column
                 const float ey = (float)dy * a.hf - qy, ez = (float)dz * a.hf - qz;
-                for (uint32_t k = k0; k < k1; k++) {
-                    const uint2 pr = a.rec[k];
-                    const float dxc = k < b1 ? -a.hf : (k < b2 ? 0.f : a.hf);
-                    const float dx = dxc + (h_lo(pr.x) - qx);
-                    const float dy_ = ey + h_hi(pr.x);
-                    const float dz_ = ez + h_lo(pr.y);
-                    const float d2 = __fmaf_rn(dz_, dz_, __fmaf_rn(dy_, dy_, dx * dx));
-                    if (d2 < a.r2) {
-                        if (FILL) {
-                            const int32_t m = a.mapping[k];
-                            out_idx[o + cnt] = gid ? gid[m] : m;
-                            S0 += dx; S1 += dy_; S2 += dz_;
-                            S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy_, S01); S02 = __fmaf_rn(dx, dz_, S02);
-                            S11 = __fmaf_rn(dy_, dy_, S11); S12 = __fmaf_rn(dy_, dz_, S12); S22 = __fmaf_rn(dz_, dz_, S22);
+                // batches of NB candidates: the loads are issued together (the hit path's stores
+                // would otherwise order every later load behind them)
+                constexpr int NB = PCP_H16_BATCH;
+                for (uint32_t k = k0; k < k1; k += NB) {
+                    uint2 pr[NB];
+                    int32_t idv[NB];
+#pragma unroll
+                    for (int u = 0; u < NB; u++) {
+                        const uint32_t kk = min(k + (uint32_t)u, k1 - 1u);
+                        pr[u] = rec[kk];
+                        if (FILL) idv[u] = ids[kk];
+                    }
+#pragma unroll
+                    for (int u = 0; u < NB; u++) {
+                        const uint32_t kk = k + (uint32_t)u;
+                        const float dxc = kk < b1 ? -a.hf : (kk < b2 ? 0.f : a.hf);
+                        const float dx = dxc + (h_lo(pr[u].x) - qx);
+                        const float dy_ = ey + h_hi(pr[u].x);
+                        const float dz_ = ez + h_lo(pr[u].y);
+                        const float d2 = __fmaf_rn(dz_, dz_, __fmaf_rn(dy_, dy_, dx * dx));
+                        if (kk < k1 && d2 < a.r2) {
+                            if (FILL) {
+#if PCP_H16_NOSTORE
+                                sink ^= idv[u];
+#else
+                                // four hits per 16-byte store (the staging rows are padded to 4)
+                                const int32_t id = idv[u];
+                                const uint32_t slot = cnt & 3u;
+                                w0 = slot == 0 ? id : w0;
+                                w1 = slot == 1 ? id : w1;
+                                w2 = slot == 2 ? id : w2;
+                                w3 = slot == 3 ? id : w3;
+                                if (slot == 3) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
+#endif
+                                S0 += dx; S1 += dy_; S2 += dz_;
+                                S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy_, S01); S02 = __fmaf_rn(dx, dz_, S02);
+                                S11 = __fmaf_rn(dy_, dy_, S11); S12 = __fmaf_rn(dy_, dz_, S12); S22 = __fmaf_rn(dz_, dz_, S22);
+                            }
+                            cnt++;
                         }
-                        cnt++;
                     }
                 }
+
             }
         }
+        if (PCP_H16_NOSTORE && FILL && sink == 0x7fffffff) out_idx[o] = sink;
+        if (!PCP_H16_NOSTORE && FILL && (cnt & 3u)) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
         if (!FILL) {
             count[caller] = (int32_t)cnt;
         } else if (out_nrm) {
@@ -232,8 +314,30 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
                            n_owned);
     if (ix->n == 0) return PCP_OK;
     const H16Args a = make_args(ix, radius, n_owned);
+    int64_t total = 0;
+    PCP_HIP(ctx, hipMemcpyAsync(&total, offsets_dev + n_owned, sizeof(total), hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    int32_t *ids = nullptr, *cnt_s = nullptr, *inv = nullptr, *tmp = nullptr;
+    int64_t* soff = nullptr;
+    struct Free {
+        pcp_ctx* c; int32_t **a, **b, **d, **e; int64_t** f;
+        ~Free() { dfree(c, *a); dfree(c, *b); dfree(c, *d); dfree(c, *e); dfree(c, *f); }
+    } fr{ctx, &ids, &cnt_s, &inv, &tmp, &soff};
+    PCP_TRY(dmalloc(ctx, &ids, (size_t)ix->n));
+    PCP_TRY(dmalloc(ctx, &cnt_s, (size_t)ix->n));
+    PCP_TRY(dmalloc(ctx, &inv, (size_t)n_owned));
+    PCP_TRY(dmalloc(ctx, &soff, (size_t)ix->n + 1));
+    PCP_TRY(dmalloc(ctx, &tmp, (size_t)total + 3 * (size_t)n_owned + 4));  // rows padded to 4
+    hipLaunchKernelGGL(k_h16_ids, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, (const int32_t*)ix->mapping,
+                       global_id_dev, ix->n, ids);
+    hipLaunchKernelGGL(k_h16_sorted_counts, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream,
+                       (const int32_t*)ix->mapping, ix->n, n_owned, offsets_dev, cnt_s, inv);
+    PCP_LAUNCH_CHECK(ctx);
+    PCP_TRY(scan_i32_to_i64(ctx, cnt_s, ix->n, soff, nullptr));
     hipLaunchKernelGGL(k_h16_radius<true>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, (int32_t*)nullptr,
-                       offsets_dev, global_id_dev, idx_dev, normals_dev);
+                       (const int64_t*)soff, (const int32_t*)ids, tmp, normals_dev);
+    hipLaunchKernelGGL(k_h16_rows_to_caller, dim3(grid_for(n_owned, kB, 1 << 16)), dim3(kB), 0, ctx->stream,
+                       (const int32_t*)inv, n_owned, (const int64_t*)soff, offsets_dev, (const int32_t*)tmp, idx_dev);
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }
