@@ -42,6 +42,7 @@ struct pcp_icp {
     uint32_t* sv_off = nullptr;
     int32_t* svc = nullptr;       // compacted search list
     int64_t sv_seg = 0;
+    int64_t nseg_v = 0;           // verify list segments: one per wave, or one per chunk (XCD split)
     int nb_ver = 0;
     int32_t* fb = nullptr;        // fallback lists: one segment of fb_seg entries per octant WG
     uint32_t* fb_count = nullptr; // per octant wave: entries in its segment
@@ -51,6 +52,7 @@ struct pcp_icp {
     double* partials = nullptr;   // (nb_ver + nb_fast + nb_ring) * 24
     double* acc = nullptr;        // 24 (scratch for pcp_icp_run)
     int nb_fast = 0, nb_ring = 0;
+    int nb_fast_l = 0;            // octant grid of the list launches (<= nb_fast)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr, ev_ver = nullptr;
     float* pose_dev = nullptr;    // 24 floats: this launch's pose (R row-major, t), then the previous one
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-launch timing events (device loop)
@@ -70,6 +72,9 @@ namespace pcp {
 namespace {
 
 constexpr int kIcpBlock = 256;
+#ifndef PCP_OCT_WAVES_LIST  // the octant pass over the verify pass's lists: more registers, fewer waves
+#define PCP_OCT_WAVES_LIST 4
+#endif
 #ifndef PCP_OCT_WAVES
 #define PCP_OCT_WAVES 6
 #endif
@@ -415,8 +420,12 @@ __device__ __forceinline__ void write_wave_partials(double (*s_acc)[kAcc], doubl
 // kFlush chunks (and at the end) the wave reduces them with DPP adds and lane 0 un-centres the
 // totals in fp64 into the wave's LDS accumulators.  A stretch is at most kFlush * 64
 // consecutive sorted queries (a few metres), so the centred fp32 products stay small.
-#ifndef PCP_KFLUSH
+#ifndef PCP_KFLUSH  // chunks per accumulator stretch (XCD split: a wave's chunks are far apart)
+#if PCP_VER_XCD
+#define PCP_KFLUSH 8
+#else
 #define PCP_KFLUSH 32
+#endif
 #endif
 constexpr int kFlush = PCP_KFLUSH;
 #ifndef PCP_FLUSH_INLINE  // 1: inline the stretch flush (no call frame spilled to scratch)
@@ -654,10 +663,26 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             const bool srch = valid && !ok;
             const uint64_t msk = __ballot(srch);
             if (srch) {
+#if PCP_VER_XCD
+                // one 64-entry segment per chunk: the compacted list keeps query order whatever
+                // the work split
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+                a.sv[(cstart_ + k * cstep) * 64 + pos] = (int32_t)i;
+#else
                 const uint32_t pos = svn + __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32),
                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
                 a.sv[gw * a.sv_seg + pos] = (int32_t)i;
+#endif
             }
+#if PCP_VER_XCD
+            if (lane == 0) {
+                const int64_t ch = cstart_ + k * cstep;
+                a.sv_count[ch] = (uint32_t)__popcll(msk);
+                a.sv_off[ch] = (uint32_t)__popcll(msk);  // scanned in place into the segment offsets
+                if (ch == 0) a.sv_off[a.nseg_v] = 0u;
+            }
+#endif
             svn += (uint32_t)__popcll(msk);
             if ((a.dbg & kDbgCount) && valid) {
                 // why queries are searched: reason and where the winner sits relative to D
@@ -723,9 +748,11 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
         acc.flush(s_acc[wid], lane, ccx, ccy, ccz);
     }
     if (lane == 0) {
+#if !PCP_VER_XCD
         a.sv_count[gw] = svn;
         a.sv_off[gw] = svn;  // scanned in place into the segment offsets
         if (gw == 0) a.sv_off[a.nseg_v] = 0u;
+#endif
     }
     write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
 }
@@ -1090,8 +1117,12 @@ __device__ __forceinline__ int octant_lanes(int64_t n, int64_t nq) {
     return 4;
 }
 
-__global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs a, const int32_t* list,
-                                                                          const uint32_t* list_n) {
+// MINW: the first (dense) launch runs at PCP_OCT_WAVES waves/SIMD; the search lists of later
+// launches at PCP_OCT_WAVES_LIST, whose larger register budget measured faster on them.  A grid
+// smaller than the partial rows / list segments sized for the first launch zeroes the rest.
+template <int MINW>
+__global__ void __launch_bounds__(kIcpBlock, MINW) k_icp_octant(IcpArgs a, const int32_t* list,
+                                                                 const uint32_t* list_n) {
     load_pose(a);
     __shared__ double s_acc[kOctW][kAcc];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1107,6 +1138,15 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_OCT_WAVES) k_icp_octant(IcpArgs
     else
         octant_run<8>(a, list, n, s_acc);
     write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
+    for (int64_t r = gridDim.x + blockIdx.x; r < a.nb_fast; r += gridDim.x)
+        if (threadIdx.x < kAcc) a.partials[r * kAcc + threadIdx.x] = 0.0;
+    if (lane == 0) {
+        const int64_t nw = (int64_t)gridDim.x * kOctW;
+        for (int64_t sg = nw + (int64_t)blockIdx.x * kOctW + wid; sg < a.nseg; sg += nw) {
+            a.fb_count[sg] = 0u;
+            a.fb_off[sg] = 0u;
+        }
+    }
 }
 
 // Fallback / general pass: exact box search (dense or sparse grid), starting from the
@@ -1638,7 +1678,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.sv_count = icp->sv_count;
     a.sv_off = icp->sv_off;
     a.sv_seg = icp->sv_seg;
-    a.nseg_v = (int64_t)icp->nb_ver * (kIcpBlock / 64);
+    a.nseg_v = icp->nseg_v;
     a.fb = icp->fb;
     a.fb_count = icp->fb_count;
     a.fb_off = icp->fb_off;
@@ -1690,7 +1730,12 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
             const int32_t* lst = verify ? (const int32_t*)icp->svc : nullptr;
             const uint32_t* lst_n = verify ? (const uint32_t*)(icp->sv_off + a.nseg_v) : nullptr;
             a.oct_g = verify ? icp->oct_g_list : icp->oct_g_first;
-            hipLaunchKernelGGL(k_icp_octant, dim3(icp->nb_fast), dim3(kIcpBlock), 0, ctx->stream, a, lst, lst_n);
+            if (verify)
+                hipLaunchKernelGGL(k_icp_octant<PCP_OCT_WAVES_LIST>, dim3(icp->nb_fast_l), dim3(kIcpBlock), 0,
+                                   ctx->stream, a, lst, lst_n);
+            else
+                hipLaunchKernelGGL(k_icp_octant<PCP_OCT_WAVES>, dim3(icp->nb_fast), dim3(kIcpBlock), 0, ctx->stream,
+                                   a, lst, lst_n);
         }
     } else {
         PCP_HIP(ctx, hipMemsetAsync(part_v, 0, (size_t)(icp->nb_ver + icp->nb_fast) * kAcc * sizeof(double),
@@ -1848,20 +1893,20 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
         dev_cus = prop.multiProcessorCount;
     const int64_t want = (icp->nq + pcp::kIcpBlock - 1) / pcp::kIcpBlock;
     icp->nb_fast = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_OCT_WAVES));
+    icp->nb_fast_l = (int)std::max<int64_t>(1, std::min<int64_t>(icp->nb_fast, (int64_t)dev_cus * PCP_OCT_WAVES_LIST));
     icp->nb_ring = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_RING_WAVES));
     const int64_t nwaves = (int64_t)icp->nb_fast * (pcp::kIcpBlock / 64);
+    const int64_t nwaves_l = (int64_t)icp->nb_fast_l * (pcp::kIcpBlock / 64);  // the smaller grid: larger segments
     const int64_t nchunks64 = (icp->nq + 63) / 64;
-    icp->fb_seg = ((nchunks64 + nwaves - 1) / nwaves) * 64;
+    icp->fb_seg = ((nchunks64 + nwaves_l - 1) / nwaves_l) * 64;
     icp->nb_ver = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_VER_WAVES));
     const int64_t nwaves_v = (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64);
 #if PCP_VER_XCD
-    {  // XCD-blocked split: a part of ceil(nch / np) chunks over floor(grid / np) * 4 waves
-        const int64_t np = std::min<int64_t>(8, icp->nb_ver);
-        const int64_t part = (nchunks64 + np - 1) / np, nw = (icp->nb_ver / np) * (pcp::kIcpBlock / 64);
-        icp->sv_seg = ((part + nw - 1) / nw) * 64;
-    }
+    icp->sv_seg = 64;  // one segment per chunk
+    icp->nseg_v = nchunks64;
 #else
     icp->sv_seg = ((nchunks64 + nwaves_v - 1) / nwaves_v) * 64;  // contiguous ranges: <= this per wave
+    icp->nseg_v = nwaves_v;
 #endif
     int rc = pcp::dmalloc(ctx, &icp->partials, (size_t)(icp->nb_ver + icp->nb_fast + icp->nb_ring) * pcp::kAcc);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->acc, pcp::kAcc);
@@ -1876,9 +1921,9 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
                 hipMemsetAsync(icp->pose_hist, 0, pcp::kHist * 12 * sizeof(float), ctx->stream) != hipSuccess ||
                 hipMemsetAsync(icp->pose_dev, 0, 24 * sizeof(float), ctx->stream) != hipSuccess))
         rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv, (size_t)nwaves_v * icp->sv_seg + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_count, (size_t)nwaves_v);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_off, (size_t)nwaves_v + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv, (size_t)icp->nseg_v * icp->sv_seg + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_count, (size_t)icp->nseg_v);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_off, (size_t)icp->nseg_v + 1);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->svc, icp->nq + 1);
 
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fb, (size_t)nwaves * icp->fb_seg + 1);
@@ -1952,7 +1997,7 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
     PCP_HIP(ctx, hipMemcpyAsync(&fbn, acc_dev + 23, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     uint32_t nsv = (uint32_t)icp->nq;  // sparse grid / first launch: every query is searched
     if (icp->last_verified)
-        PCP_HIP(ctx, hipMemcpyAsync(&nsv, icp->sv_off + (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64), sizeof(nsv),
+        PCP_HIP(ctx, hipMemcpyAsync(&nsv, icp->sv_off + icp->nseg_v, sizeof(nsv),
                                     hipMemcpyDeviceToHost, ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     icp->last_fallback = (uint32_t)fbn;
