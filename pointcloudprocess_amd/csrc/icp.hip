@@ -1113,7 +1113,7 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
 // want one lane each; sparse ones want the group form.
 __device__ __forceinline__ int octant_lanes(int64_t n, int64_t nq) {
     if (n * 100 > nq * 36) return 1;
-    if (n * 100 > nq * 17) return 2;
+    if (n * 100 > nq * 8) return 2;
     return 4;
 }
 
