@@ -35,6 +35,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "pcp.h"
@@ -1015,6 +1016,107 @@ inline void find_reliable(std::vector<Rot>& rots, std::string cloud_files_dir, f
         const double dis_right = std::pow(a[0] - b[0], 2) + std::pow(a[1] - b[1], 2) + std::pow(a[2] - b[2], 2);
         if (dis_left < dis_threshold && dis_right < dis_threshold) rots[i].is_valid = true;
     }
+}
+
+// PointCloudHelper::change_cloud_rgb (point_cloud_helper.cpp:178-186)
+inline void change_cloud_rgb(CloudPtr cloud_src, int r, int g, int b) {
+    const uint32_t rgb = (uint32_t)r << 16 | (uint32_t)g << 8 | (uint32_t)b;
+    for (CloudItem& p : cloud_src->points) p.rgba = rgb;
+}
+
+// do_mul_frame_icp (main_blend.cpp:641-931) over the device path: the pose line and the
+// threshold the reference reads from g_status are parameters; the map cache is
+// CloudGrid::instance().  Frames are loaded in the reference's order (the frames between the two
+// ends, then the walk back from start_index and the walk forward from end_index until valid_count
+// consecutive frames have 0 < icp value < min_icp_threshold), concatenated, recoloured,
+// de-duplicated (4 cm) and optionally shaft-filtered; the map cache around them (+-30 m box, or
+// get_grid_cloud at 1 m) registers them with get_rot_icp(do_scale); with is_do_sep_icp each frame
+// is then registered against its own +-3 m box.  Every loaded frame's pose is set in `line`.
+inline float do_mul_frame_icp(std::vector<CloudStampRot>& line, double min_icp_threshold,
+                              const std::unordered_map<uint64_t, std::string>& stamp_filename_map, int start_index,
+                              int end_index, int valid_count, bool is_do_sep_icp, bool is_mul_seg,
+                              bool is_shaft_filter) {
+    std::vector<uint64_t> stamps;
+    std::vector<std::string> files;
+    auto take = [&](int i) {
+        const auto it = stamp_filename_map.find(line[i]._stamp);
+        if (it == stamp_filename_map.end()) return;
+        files.push_back(it->second);
+        stamps.push_back(line[i]._stamp);
+    };
+    for (int i = start_index + 1; i < end_index; i++) take(i);
+    const int size = (int)line.size();
+    int k = 0, l = start_index, last = -1;
+    do {  // (:684-712); (size_t)last < size is false for the unset -1
+        if (l < 0) break;
+        const float v = (float)line[l]._value_icp;
+        if (v > 0 && v < min_icp_threshold) {
+            k++;
+            if (last >= 0 && last < size && last != l + 1) k = 0;
+            last = l;
+        }
+        take(l--);
+    } while (k < valid_count);
+    k = 0, l = end_index, last = -1;
+    do {  // (:717-745)
+        if (l >= size) break;
+        const float v = (float)line[l]._value_icp;
+        if (v > 0 && v < min_icp_threshold) {
+            k++;
+            if (last >= 0 && last != l - 1) k = 0;
+            last = l;
+        }
+        take(l++);
+    } while (k < valid_count);
+    std::vector<CloudPtr> clouds(files.size());
+    CloudPtr frame(new Cloud);
+    for (size_t i = 0; i < files.size(); i++) {
+        clouds[i].reset(new Cloud);
+        io::loadPCDFile(files[i], *clouds[i]);
+        frame->points.insert(frame->points.end(), clouds[i]->points.begin(), clouds[i]->points.end());
+        frame->is_dense = frame->is_dense && clouds[i]->is_dense;
+    }
+    frame->width = (uint32_t)frame->points.size();
+    frame->height = 1;
+    change_cloud_rgb(frame, 255, 0, 0);
+    PointCloudHelper::remove_duplicate(frame, 0.04f);
+    if (is_shaft_filter) shaft_filter(frame, frame);
+    CloudPtr cache(new Cloud);
+    if (!is_mul_seg) {
+        CloudItem mn, mx;
+        PointCloudHelper::getMinMax3D(*frame, mn, mx);
+        const float d = 30;
+        mn.x -= d; mn.y -= d; mn.z -= d;
+        mx.x += d; mx.y += d; mx.z += d;
+        CloudGrid::instance().get_cloud_with_pos(cache, mn, mx);
+    } else {
+        CloudGrid::instance().get_grid_cloud(frame, frame, cache, 1.0f);
+    }
+    Mat4d rot = Mat4d::Identity();
+    const float dis = PointCloudHelper::get_rot_icp(cache, frame, rot, true, false);
+    for (size_t i = 0; i < stamps.size(); i++) {
+        Mat4d final_rot = rot;
+        if (is_do_sep_icp) {
+            CloudPtr moved(new Cloud);
+            PointCloudHelper::transformPointCloud(*clouds[i], *moved, rot);
+            CloudItem mn, mx;
+            PointCloudHelper::getMinMax3D(*moved, mn, mx);
+            const float d = 3;
+            mn.x -= d; mn.y -= d; mn.z -= d;
+            mx.x += d; mx.y += d; mx.z += d;
+            CloudPtr cache_t(new Cloud);
+            CloudGrid::instance().get_cloud_with_pos(cache_t, mn, mx);
+            Mat4d rot_split = Mat4d::Identity();
+            if (cache_t->size() > 0) PointCloudHelper::get_rot_icp(cache_t, moved, rot_split, false, false);
+            final_rot = rot_split * rot;
+        }
+        for (CloudStampRot& r : line)  // get_cloud_rot_with_stamp: the first entry of the stamp
+            if (r._stamp == stamps[i]) {
+                r._rot = final_rot;
+                break;
+            }
+    }
+    return dis;
 }
 
 // pose lines: the reference's Eigen composition restated in libpcp (pcp_pose_*, host-only)

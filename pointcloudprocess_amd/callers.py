@@ -116,3 +116,89 @@ def find_reliable(ctx, rots, load_cloud, icp_threshold):
         if dis[0] < 0.06 and dis[1] < 0.06:
             valid[i] = True
     return valid
+
+
+# ---------------------------------------------------------------- do_mul_frame_icp
+def _frame_walk(line, start, step, valid_count, min_icp_threshold, stamp_file, stamps_out):
+    """The front / back walks of do_mul_frame_icp (main_blend.cpp:684-745): collect frames from
+    `start` outwards until valid_count consecutive frames have 0 < icp value < threshold.  The
+    reference's consecutiveness tests differ by direction, and both are kept: walking back it
+    is `(size_t)last_valid_index < size && last_valid_index != l + 1` (the unset -1 compares
+    as SIZE_MAX), walking forward `last_valid_index >= 0 && last_valid_index != l - 1`; a
+    gap resets k to 0 after the increment, so the frame that ends the gap does not count."""
+    k, l, last = 0, start, -1
+    n = len(line)
+    while True:
+        if (step < 0 and l < 0) or (step > 0 and l >= n):
+            break
+        v = float(np.float32(line[l]["icperr"]))  # const float icp_value = ..._value_icp
+        if v > 0 and v < min_icp_threshold:
+            k += 1
+            gap = (last >= 0 and last < n and last != l + 1) if step < 0 else (last >= 0 and last != l - 1)
+            if gap:
+                k = 0
+            last = l
+        st = line[l]["stamp"]
+        l += step
+        if st in stamp_file:
+            stamps_out.append((st, stamp_file[st]))
+        if not k < valid_count:
+            break
+
+
+def _box_pad(ctx, cloud, pad):
+    """getMinMax3D(cloud, PointT&, PointT&) (point_cloud_helper.h:22-57) widened by `pad`."""
+    mn, mx = ops.minmax(ctx, cloud, True)
+    return (mn[0] - pad, mn[1] - pad, mn[2] - pad), (mx[0] + pad, mx[1] + pad, mx[2] + pad)
+
+
+def do_mul_frame_icp(ctx, line, stamp_file, start_index, end_index, grid, valid_count, min_icp_threshold,
+                     is_do_sep_icp=False, is_mul_seg=False, is_shaft_filter=False, load_cloud=None):
+    """do_mul_frame_icp (main_blend.cpp:641-931) on the device path.  line: the pose line, a list
+    of dicts {stamp, matrix (4x4), icperr} (g_status._clouds_stamp_rot_line; matrices are
+    updated in place, at the first entry of each stamp as get_cloud_rot_with_stamp does);
+    stamp_file: stamp -> PCD path; grid: the CloudGrid map cache.  load_cloud(path) -> (n, 48)
+    uint8 device records (default: pcd.load_pcd).  Returns (dis, rot) of the joint registration."""
+    import torch
+    from . import pcd as _pcd
+    from . import segments as _seg
+    if load_cloud is None:
+        def load_cloud(path):
+            return torch.from_numpy(_pcd.load_pcd(path).view(np.uint8).reshape(-1, 48).copy()).to(ctx.device)
+    frames = []  # (stamp, path) in frame_files order
+    for i in range(start_index + 1, end_index):  # the frames between the two ends (:662-679)
+        st = line[i]["stamp"]
+        if st in stamp_file:
+            frames.append((st, stamp_file[st]))
+    _frame_walk(line, start_index, -1, valid_count, min_icp_threshold, stamp_file, frames)
+    _frame_walk(line, end_index, +1, valid_count, min_icp_threshold, stamp_file, frames)
+    clouds = [load_cloud(p) for _, p in frames]  # (:754-765)
+    frame = torch.cat(clouds) if clouds else torch.empty((0, 48), dtype=torch.uint8, device=ctx.device)
+    frame = frame.clone()
+    frame[:, 32:36] = torch.tensor([0, 0, 255, 0], dtype=torch.uint8, device=ctx.device)  # change_cloud_rgb 255,0,0
+    dense = bool(torch.isfinite(frame[:, :24].contiguous().view(torch.float64)).all()) if frame.shape[0] else True
+    frame = ops.remove_duplicate(ctx, frame, 0.04, is_dense=dense)
+    if is_shaft_filter:
+        frame = _seg.shaft_filter(ctx, frame)
+    if not is_mul_seg:  # (:779-790): the map cache around the frames' box +- 30 m
+        lo, hi = _box_pad(ctx, frame, 30.0)
+        cache = grid.get_cloud_with_pos(lo, hi)
+    else:  # get_grid_cloud(frame_cloud, frame_cloud, cache_cloud, 1.0) (:792): frame <- its matched part
+        frame, cache = grid.get_grid_cloud_match(frame, 1.0)
+    dis, rot = ops.get_rot_icp(ctx, cache, frame, 0.25, do_scale=True)  # get_rot_icp(cache, frame, rot, true)
+    by_stamp = {}
+    for i, e in enumerate(line):
+        by_stamp.setdefault(e["stamp"], i)
+    for (st, _), cloud in zip(frames, clouds):  # (:839-904)
+        final = rot
+        if is_do_sep_icp:
+            moved = ops.transform(ctx, cloud, rot)
+            lo, hi = _box_pad(ctx, moved, 3.0)
+            cache_t = grid.get_cloud_with_pos(lo, hi)
+            rot_split = np.eye(4)
+            if cache_t.shape[0] > 0:
+                _, rot_split = ops.get_rot_icp(ctx, cache_t, moved, 0.25, do_scale=False)
+            final = rot_split @ rot
+        if st in by_stamp:
+            line[by_stamp[st]]["matrix"] = np.array(final)
+    return dis, rot

@@ -9,6 +9,7 @@
 #include <deque>
 #include <set>
 #include <random>
+#include <unordered_map>
 #include <vector>
 
 #include "pcp_pcl.hpp"
@@ -412,7 +413,44 @@ static void test_region_growing() {
     CHECK(ground->size() < n, "ground_filter kept %zu of %zu", ground->size(), n);
 }
 
+// do_mul_frame_icp (main_blend.cpp:641-931): frames saved as PCD files, the map in
+// CloudGrid::instance(); every selected frame's pose is set, the walks stop at valid_count
+// consecutive valid frames, and the joint pose equals a direct get_rot_icp of the same clouds
+static void test_mul_frame_icp() {
+    CloudPtr map = random_cloud(40000, 91, 10.0, 300.0);
+    CloudGrid::instance().clear();
+    CloudGrid::instance().add_cloud_internal(map);
+    std::vector<CloudStampRot> line;
+    std::unordered_map<uint64_t, std::string> files;
+    const double errs[8] = {0.05, 0.05, 0.2, 0.05, 0.05, 0.05, 0.0, 0.05};
+    for (int i = 0; i < 8; i++) {
+        CloudStampRot r;
+        r._stamp = 700 + i;
+        r._value_icp = errs[i];
+        line.push_back(r);
+        CloudPtr f(new Cloud);
+        for (size_t j = i; j < map->size(); j += 8) {
+            CloudItem p = map->points[j];
+            p.x += 0.01; p.y -= 0.02;
+            f->push_back(p);
+        }
+        const std::string path = "/tmp/pcp_shim_frame_" + std::to_string(i) + ".pcd";
+        io::savePCDFileBinary(path, *f);
+        files[700 + i] = path;
+    }
+    const float dis = do_mul_frame_icp(line, 0.1, files, 3, 5, 2, false, false, false);
+    // middle 4; back from 3: 3, 2 (invalid: k stays), 1, 0 -> k = 1 after 1 (gap at 2 resets), 2 after 0;
+    // forward from 5: 5 (k 1), 6 (invalid), 7 (gap: k = 0) -> end of line
+    int set = 0;
+    for (int i = 0; i < 8; i++) set += line[i]._rot(0, 3) != 0.0;
+    CHECK(dis > 0 && set == 8, "mul-frame icp dis %g, poses set %d", dis, set);
+    CHECK(std::fabs(line[0]._rot(0, 3) + 0.01) < 2e-3 && std::fabs(line[0]._rot(1, 3) - 0.02) < 2e-3,
+          "mul-frame pose t = (%g, %g)", line[0]._rot(0, 3), line[0]._rot(1, 3));
+    CloudGrid::instance().clear();
+}
+
 int main() {
+    test_mul_frame_icp();
     test_region_growing();
     test_batched_callers();
     test_pcd_io();

@@ -102,3 +102,136 @@ def test_gpu_find_reliable():
         exp[i] = dis[0] < 0.06 and dis[1] < 0.06
     assert got == exp and any(exp) and not all(exp[1:-1])
     ctx.close()
+
+
+# ---------------------------------------------------------------- do_mul_frame_icp
+def select_frames_reference(line, stamp_file, start, end, valid_count, thr):
+    """main_blend.cpp:662-745 as written (C++ int / size_t comparisons spelled out)."""
+    out = [line[i]["stamp"] for i in range(start + 1, end) if line[i]["stamp"] in stamp_file]
+    size = len(line)
+    k, l, last = 0, start, -1
+    while True:  # do { ... } while (k < valid_count)
+        if l < 0:
+            break
+        v = float(np.float32(line[l]["icperr"]))
+        if v > 0 and v < thr:
+            k += 1
+            last_as_size_t = last if last >= 0 else 2 ** 64 - 1
+            if last_as_size_t < size and last != l + 1:
+                k = 0
+            last = l
+        st = line[l]["stamp"]
+        l -= 1
+        if st in stamp_file:
+            out.append(st)
+        if not k < valid_count:
+            break
+    k, l, last = 0, end, -1
+    while True:
+        if l >= size:
+            break
+        v = float(np.float32(line[l]["icperr"]))
+        if v > 0 and v < thr:
+            k += 1
+            if last >= 0 and last != l - 1:
+                k = 0
+            last = l
+        st = line[l]["stamp"]
+        l += 1
+        if st in stamp_file:
+            out.append(st)
+        if not k < valid_count:
+            break
+    return out
+
+
+def test_frame_selection_walks():
+    rng = np.random.default_rng(9)
+    for trial in range(200):
+        n = int(rng.integers(3, 30))
+        line = [{"stamp": 100 + i, "icperr": float(rng.choice([0.0, 0.05, 0.2, -1.0])), "matrix": np.eye(4)}
+                for i in range(n)]
+        stamp_file = {100 + i: f"f{i}" for i in range(n) if rng.random() < 0.8}
+        s = int(rng.integers(0, n - 1))
+        e = int(rng.integers(s + 1, n))
+        vc = int(rng.integers(1, 4))
+        frames = []
+        for i in range(s + 1, e):
+            if line[i]["stamp"] in stamp_file:
+                frames.append((line[i]["stamp"], stamp_file[line[i]["stamp"]]))
+        callers._frame_walk(line, s, -1, vc, 0.1, stamp_file, frames)
+        callers._frame_walk(line, e, +1, vc, 0.1, stamp_file, frames)
+        assert [f[0] for f in frames] == select_frames_reference(line, stamp_file, s, e, vc, 0.1), trial
+
+
+def mul_frame_reference(line, frames_xyz, map_cloud, start, end, valid_count, thr, sep, mul_seg):
+    """The same composition over the oracle: selection, concatenation, change_cloud_rgb,
+    remove_duplicate(0.04), the map cache box (+-30 m) or get_grid_cloud(1.0), get_rot_icp
+    (do_scale), and per frame the +-3 m box and a second get_rot_icp."""
+    stamp_file = {st: st for st in frames_xyz}
+    sel = select_frames_reference(line, stamp_file, start, end, valid_count, thr)
+    clouds = [ora.make_cloud(frames_xyz[st]) for st in sel]
+    frame = np.concatenate(clouds)
+    frame["rgba"] = 0x00FF0000
+    frame = ora.remove_duplicate(frame, 0.04)
+    g = ora.Grid()
+    g.add_cloud(map_cloud)
+    if not mul_seg:
+        mn, mx = ora.minmax(frame)
+        cache = g.box(int(mn[0] - 30.0), math.ceil(mx[0] + 30.0), int(mn[1] - 30.0), math.ceil(mx[1] + 30.0))
+    else:
+        frame, cache = g.match(frame, 1.0)
+    dis, rot = ora.get_rot_icp(cache, frame, 0.25, 20, do_scale=True)
+    finals = {}
+    for st, cloud in zip(sel, clouds):
+        final = rot
+        if sep:
+            moved = ora.transform(cloud, rot)
+            mn, mx = ora.minmax(moved)
+            c2 = g.box(int(mn[0] - 3.0), math.ceil(mx[0] + 3.0), int(mn[1] - 3.0), math.ceil(mx[1] + 3.0))
+            rs = np.eye(4)
+            if len(c2):
+                _, rs = ora.get_rot_icp(c2, moved, 0.25, 20, do_scale=False)
+            final = rs @ rot
+        finals[st] = final
+    return sel, dis, rot, finals
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sep,mul_seg", [(False, False), (True, False), (False, True)])
+def test_gpu_do_mul_frame_icp(tmp_path, sep, mul_seg):
+    """main_blend.cpp:641-931 through the device path (PCD files, CloudGrid, remove_duplicate,
+    get_rot_icp) against the oracle composition: the same frames, poses within 1e-5."""
+    import torch
+    from pointcloudprocess_amd import cloudgrid, ops, pcd, synth
+    ctx = ops.Context(0)
+    T_true = synth.rigid(0.3, 0.1, -0.1, (0.06, -0.04, 0.02))
+    tgt, q = synth.icp_pair(60_000, 60_000, 81, 82, T_true, extent=(40.0, 40.0))
+    off = np.array([3512.25, -1801.5, 40.0])
+    map_cloud = ora.make_cloud(tgt.double().numpy() + off)
+    qx = q.double().numpy() + off
+    order = np.argsort(qx[:, 0], kind="stable")  # frames = consecutive strips along x
+    nfr = 10
+    frames_xyz, stamp_file = {}, {}
+    for i in range(nfr):
+        st = 5000 + 10 * i
+        frames_xyz[st] = qx[order[i::nfr][: len(order) // nfr]]
+        path = tmp_path / f"{st}.pcd"
+        pcd.save_pcd(str(path), ora.make_cloud(frames_xyz[st]))
+        stamp_file[st] = str(path)
+    errs = [0.05, 0.2, 0.05, 0.05, 0.0, 0.05, 0.3, 0.05, 0.05, 0.05]
+    line = [{"stamp": 5000 + 10 * i, "icperr": errs[i], "matrix": np.eye(4)} for i in range(nfr)]
+    grid = cloudgrid.CloudGrid(ctx)
+    grid.add_cloud_internal(ops.cloud_to_device(map_cloud, ctx.device))
+    dis, rot = callers.do_mul_frame_icp(ctx, line, stamp_file, 4, 6, grid, 2, 0.1, is_do_sep_icp=sep,
+                                        is_mul_seg=mul_seg)
+    sel, edis, erot, finals = mul_frame_reference(
+        [dict(e) for e in line], frames_xyz, map_cloud, 4, 6, 2, 0.1, sep, mul_seg)
+    assert dis > 0 and edis > 0 and abs(dis - edis) <= 1e-5
+    assert np.abs(rot - erot).max() <= 1e-5 * np.abs(off).max()
+    got = {e["stamp"]: e["matrix"] for e in line if not np.array_equal(e["matrix"], np.eye(4))}
+    assert sorted(got) == sorted(finals) and len(finals) >= 5
+    for st in finals:
+        assert np.abs(got[st] - finals[st]).max() <= 1e-5 * np.abs(off).max(), st
+    grid.close()
+    ctx.close()
