@@ -289,3 +289,36 @@ def test_slab_guard_device(ctx):
     T[0, 3] = 1.5
     ops.slab_guard(ctx, torch.from_numpy(T.reshape(16).copy()).to(ctx.device), box, -1.0, 11.0, flag)
     assert flag.item() == 1
+
+
+@pytest.mark.parametrize("gs", ["2,2", "4,4", "8,8", "1,0"])
+def test_octant_lane_groups_exact(ctx, gs, monkeypatch):
+    """G lanes per query in the octant pass (PCP_OCT_G="first,list"; 0 = by density): the
+    group merge, the per-group cache write and the > 256-candidate compare-swap path must give
+    the oracle's correspondences over a registration, on lattice ties and a dense cluster."""
+    from pointcloudprocess_amd import ops, synth
+    monkeypatch.setenv("PCP_OCT_G", gs)
+    T_true = synth.rigid()
+    tgt, q = _pair(120_000, 51, T_true)
+    rng = np.random.default_rng(52)
+    c0 = tgt[0].numpy()
+    cluster = (c0 + rng.uniform(-0.02, 0.02, (3000, 3))).astype(np.float32)  # >256 points per cell
+    lat = np.stack(np.meshgrid(np.arange(6), np.arange(6), np.arange(3), indexing="ij"), -1).reshape(-1, 3)
+    lat = (lat * 0.1 + np.array([5.0, 5.0, 20.0])).astype(np.float32)       # exact ties
+    tgt = torch.from_numpy(np.concatenate([tgt.numpy(), cluster, lat]))
+    qn = np.concatenate([q.numpy(), cluster[:500] + 0.003, (lat + 0.05).astype(np.float32)])
+    q = torch.from_numpy(qn.astype(np.float32))
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+    icp = ops.ICP(index, q.to(ctx.device))
+    oi = ora.F32Index(tgt.numpy())
+    T = np.eye(4)
+    for it in range(6):
+        acc, ci, cd = icp.step(T, 0.25, corr=True)
+        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+        ei, ed = oi.correspond(q.numpy(), R, t, 0.25)
+        gi = ci.cpu().numpy()
+        assert np.array_equal(gi, ei), f"G {gs} iter {it}: {(gi != ei).sum()} mismatching correspondences"
+        assert np.array_equal(cd.cpu().numpy()[ei >= 0], ed[ei >= 0])
+        rc, dT = ops.icp_solve(acc.cpu().numpy())
+        assert rc == 0
+        T = dT @ T
