@@ -171,8 +171,29 @@ __device__ double global_kth(const TopK<K>& top, int kk, int lane) {
     return kth;
 }
 
+// An upper bound on the wave's exact k-th d2, cheap enough to refresh inside a shell: the
+// kk-th smallest of the lanes' own best d2 (a subset of the union, so its kk-th smallest is at
+// least the union's), by a 64-lane bitonic sort; +inf until kk lanes hold a point.
 template <int K>
-__device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int lane, int kk) {
+__device__ double wave_kth_of_bests(const TopK<K>& top, int kk, int lane) {
+    double x = INFINITY;
+#pragma unroll
+    for (int i = 0; i < K; i++)
+        if (i == kk - 1) x = top.d[i];
+#pragma unroll
+    for (int k2 = 2; k2 <= 64; k2 <<= 1)
+#pragma unroll
+        for (int j = k2 >> 1; j > 0; j >>= 1) {
+            const double y = __shfl_xor(x, j, 64);
+            const bool up = (lane & k2) == 0, lower = (lane & j) == 0;
+            x = (lower == up) ? fmin(x, y) : fmax(x, y);
+        }
+    return __shfl(x, kk - 1, 64);
+}
+
+template <int K>
+__device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int lane, int kk,
+                            int* shells = nullptr, long long* tk = nullptr) {
     const double fx = cell_f<double>(g, v.qx, 0), fy = cell_f<double>(g, v.qy, 1), fz = cell_f<double>(g, v.qz, 2);
     const int cx = (int)floor(fx), cy = (int)floor(fy), cz = (int)floor(fz);
     const double lx = fx - cx, ly = fy - cy, lz = fz - cz;
@@ -226,8 +247,12 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     farb = max(farb, max(bz - (g.nb[2] - 1), -bz));
     const int sbmax = farb + max(g.nb[0], max(g.nb[1], g.nb[2]));
     // rings closer than `farb` lie wholly outside the grid (a query far away from it)
+    if (tk) tk[0] = clock64();
     for (int sb = farb; sb <= sbmax; sb++) {
+        if (shells) (*shells)++;
+        const long long c0 = tk ? (long long)clock64() : 0;
         v.shared = global_kth<K>(v.top, kk, lane);
+        if (tk) tk[1] += (long long)clock64() - c0;
         if (sb > 0) {
             const double rmin = (double)(4 * (sb - 1)) + bdmin - mc;
             if (rmin > 0 && rmin * rmin * h2 > v.ubound()) return;
@@ -258,38 +283,76 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
             }
         }
         const int64_t total = area[0] + area[1] + area[2] + area[3] + area[4] + area[5];
-        for (int64_t t = lane; t < total; t += 64) {
-            int f = 0;
-            int64_t r = t;
-            while (r >= area[f]) { r -= area[f]; f++; }
-            int xb, yb, zb;
-            if (f < 2) {
-                xb = X0 + (int)(r % nx); yb = Y0 + (int)(r / nx); zb = fixc[f];
-            } else if (f < 4) {
-                xb = X0 + (int)(r % nx); zb = Zi0 + (int)(r / nx); yb = fixc[f];
-            } else {
-                yb = Yi0 + (int)(r % nyi); zb = Zi0 + (int)(r / nyi); xb = fixc[f];
+        // bricks t = lane + 64 u: the occupancy words of a batch are loaded together (mostly
+        // empty bricks around isolated queries: one dependent load each would serialise)
+        constexpr int kBB = 8;
+        for (int64_t base = 0; base < total; base += 64 * kBB) {  // wave-uniform trip count
+            const int64_t t0 = base + lane;
+            int bxs[kBB], bys[kBB], bzs[kBB];
+            int32_t occ[kBB];
+#pragma unroll
+            for (int u = 0; u < kBB; u++) {
+                const int64_t t = t0 + 64 * u;
+                int xb = 0, yb = 0, zb = 0;
+                bool live = t < total;
+                if (live) {
+                    int f = 0;
+                    int64_t r = t;
+                    while (r >= area[f]) { r -= area[f]; f++; }
+                    if (f < 2) {
+                        xb = X0 + (int)(r % nx); yb = Y0 + (int)(r / nx); zb = fixc[f];
+                    } else if (f < 4) {
+                        xb = X0 + (int)(r % nx); zb = Zi0 + (int)(r / nx); yb = fixc[f];
+                    } else {
+                        yb = Yi0 + (int)(r % nyi); zb = Zi0 + (int)(r / nyi); xb = fixc[f];
+                    }
+                    const double gz = zb < bz ? (oz + 4.0 * (bz - zb - 1)) : (zb > bz ? (4.0 - oz + 4.0 * (zb - bz - 1)) : 0.0);
+                    const double gy = yb < by ? (oy + 4.0 * (by - yb - 1)) : (yb > by ? (4.0 - oy + 4.0 * (yb - by - 1)) : 0.0);
+                    const double gx = xb < bx ? (ox + 4.0 * (bx - xb - 1)) : (xb > bx ? (4.0 - ox + 4.0 * (xb - bx - 1)) : 0.0);
+                    live = (sq_gap(gz, mc) + sq_gap(gy, mc) + sq_gap(gx, mc)) * h2 <= v.bound();
+                }
+                bxs[u] = xb; bys[u] = yb; bzs[u] = zb;
+                occ[u] = live ? g.brick[((int64_t)zb * g.nb[1] + yb) * g.nb[0] + xb] : -1;
             }
-            const double gz = zb < bz ? (oz + 4.0 * (bz - zb - 1)) : (zb > bz ? (4.0 - oz + 4.0 * (zb - bz - 1)) : 0.0);
-            const double gy = yb < by ? (oy + 4.0 * (by - yb - 1)) : (yb > by ? (4.0 - oy + 4.0 * (yb - by - 1)) : 0.0);
-            const double gx = xb < bx ? (ox + 4.0 * (bx - xb - 1)) : (xb > bx ? (4.0 - ox + 4.0 * (xb - bx - 1)) : 0.0);
-            if ((sq_gap(gz, mc) + sq_gap(gy, mc) + sq_gap(gx, mc)) * h2 > v.bound()) continue;
-            if (g.brick[((int64_t)zb * g.nb[1] + yb) * g.nb[0] + xb] < 0) continue;  // empty brick
-            for (int z = 4 * zb; z < min(4 * zb + 4, g.n[2]); z++) {
-                const double cz2 = sq_gap(axis_gap<double>(z, cz, lz), mc);
-                const bool zin = abs(z - cz) <= kCellRings;
-                for (int y = 4 * yb; y < min(4 * yb + 4, g.n[1]); y++) {
-                    const double cyz2 = cz2 + sq_gap(axis_gap<double>(y, cy, ly), mc);
-                    if (cyz2 * h2 > v.bound()) continue;
-                    const bool yzin = zin && abs(y - cy) <= kCellRings;
-                    for (int x = 4 * xb; x < min(4 * xb + 4, g.n[0]); x++) {
-                        if (yzin && abs(x - cx) <= kCellRings) continue;
-                        if ((cyz2 + sq_gap(axis_gap<double>(x, cx, lx), mc)) * h2 > v.bound()) continue;
-                        uint32_t st, en;
-                        if (cell_range(g, x, y, z, st, en)) v.visit(st, en);
+#pragma unroll 1
+            for (int u = 0; u < kBB; u++) {
+                if (occ[u] < 0) continue;  // empty or pruned brick
+                const int xb = bxs[u], yb = bys[u], zb = bzs[u];
+                // the brick's rows of 4 cells are contiguous point ranges (x fastest, dense or
+                // brick-slot layout): one range per row run instead of one per cell
+                const int xc0 = 4 * xb, xc1 = min(4 * xb + 3, g.n[0] - 1);
+                const int64_t rowbase = g.dense ? 0 : (int64_t)occ[u] * 64;
+                for (int z = 4 * zb; z < min(4 * zb + 4, g.n[2]); z++) {
+                    const double cz2 = sq_gap(axis_gap<double>(z, cz, lz), mc);
+                    const bool zin = abs(z - cz) <= kCellRings;
+                    for (int y = 4 * yb; y < min(4 * yb + 4, g.n[1]); y++) {
+                        const double cyz2 = cz2 + sq_gap(axis_gap<double>(y, cy, ly), mc);
+                        if (cyz2 * h2 > v.bound()) continue;
+                        const bool yzin = zin && abs(y - cy) <= kCellRings;
+                        // cells within the bound form an interval around cx; phase 1's cells
+                        // (|x - cx| <= kCellRings on this row) are cut out of it
+                        int xa = xc0, xe = xc1;
+                        while (xa <= xe && (cyz2 + sq_gap(axis_gap<double>(xa, cx, lx), mc)) * h2 > v.bound()) xa++;
+                        while (xe >= xa && (cyz2 + sq_gap(axis_gap<double>(xe, cx, lx), mc)) * h2 > v.bound()) xe--;
+                        if (xa > xe) continue;
+                        const int64_t r0 = g.dense ? dense_id(g, 0, y, z) : rowbase + local_of(0, y, z);
+                        auto run = [&](int x0, int x1) {  // cells [x0, x1] of this row
+                            if (x0 > x1) return;
+                            const int64_t c0 = g.dense ? r0 + x0 : r0 + (x0 & 3);
+                            const uint32_t st = g.cstart[c0], en = g.cstart[c0 + (x1 - x0) + 1];
+                            if (en > st) v.visit(st, en);
+                        };
+                        if (yzin) {
+                            run(xa, min(xe, cx - kCellRings - 1));
+                            run(max(xa, cx + kCellRings + 1), xe);
+                        } else {
+                            run(xa, xe);
+                        }
                     }
                 }
             }
+            // tighten the shared bound mid-shell (the exact k-th is refreshed per shell)
+            if (kk <= 64) v.shared = fmin(v.shared, wave_kth_of_bests<K>(v.top, kk, lane));
         }
     }
 }
@@ -346,7 +409,8 @@ __global__ __launch_bounds__(kB) void k_knn_coop(GridDesc g, const double4* pts,
 template <int K>
 __global__ __launch_bounds__(kB) void k_normals_coop(GridDesc g, const double4* pts, const int32_t* mapping,
                                                      int identity, const int32_t* pos_of_j, int kk, double mc,
-                                                     pcp_plane* out, int64_t n_out, FarList far) {
+                                                     pcp_plane* out, int64_t n_out, FarList far,
+                                                     unsigned long long* dbg = nullptr) {
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64), cnt = *far.count;
     for (int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6); w < cnt; w += nwaves) {
@@ -356,25 +420,45 @@ __global__ __launch_bounds__(kB) void k_normals_coop(GridDesc g, const double4* 
         v.pts = pts;
         v.qx = qp.x; v.qy = qp.y; v.qz = qp.z;
         v.top.init(kk);
-        coop_search<K>(g, mc, v, lane, kk);
+        int shells = 0;
+        const long long t0 = dbg ? (long long)clock64() : 0;
+        long long tk[2] = {t0, 0};
+        coop_search<K>(g, mc, v, lane, kk, dbg ? &shells : nullptr, dbg ? tk : nullptr);
+        if (dbg && lane == 0) {  // PCP_KNN_DEBUG: shells walked and cycles per deferred query
+            const unsigned long long dt = (unsigned long long)((long long)clock64() - t0);
+            atomicAdd(dbg + 0, 1ull);
+            atomicAdd(dbg + 1, (unsigned long long)shells);
+            atomicMax(dbg + 2, (unsigned long long)shells);
+            atomicAdd(dbg + 3, dt);
+            atomicMax(dbg + 4, dt);
+            atomicAdd(dbg + 9, (unsigned long long)(tk[0] - t0));  // ring phase
+            atomicAdd(dbg + 10, (unsigned long long)tk[1]);        // global_kth in the shells
+            if (dt >= dbg[4]) {  // the slowest query's coordinates (racy, debugging only)
+                dbg[5] = (unsigned long long)__double_as_longlong(qp.x);
+                dbg[6] = (unsigned long long)__double_as_longlong(qp.y);
+                dbg[7] = (unsigned long long)__double_as_longlong(qp.z);
+                dbg[8] = (unsigned long long)__double_as_longlong(v.shared);
+            }
+        }
         double md;
         int mj;
         coop_merge<K>(v, kk, lane, md, mj);
         const int jq = (int)qp.w;
         const int64_t oi = identity ? jq : mapping[jq];
         if (oi >= n_out) continue;
-        // mean and X X^T, sequential in kNN order (calculate_feature.cpp:131-164), wave-uniform
+        // mean and X X^T, sequential in kNN order (calculate_feature.cpp:131-164), wave-uniform;
+        // lane r fetches the r-th neighbour once (all loads in flight together), the sums then
+        // walk the lanes in order through shuffles
+        double4 pr = make_double4(0.0, 0.0, 0.0, 0.0);
+        if (lane < kk && mj != INT_MAX) pr = pts[pos_of_j[mj]];
         double xa = 0, ya = 0, za = 0;
         for (int r = 0; r < kk; r++) {
-            const int j = __shfl(mj, r, 64);
-            const double4 p = pts[pos_of_j[j]];
-            xa += p.x; ya += p.y; za += p.z;
+            xa += __shfl(pr.x, r, 64); ya += __shfl(pr.y, r, 64); za += __shfl(pr.z, r, 64);
         }
         xa /= kk; ya /= kk; za /= kk;
         double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
         for (int r = 0; r < kk; r++) {
-            const int j = __shfl(mj, r, 64);
-            const double4 p = pts[pos_of_j[j]];
+            const double4 p = make_double4(__shfl(pr.x, r, 64), __shfl(pr.y, r, 64), __shfl(pr.z, r, 64), 0.0);
             const double x0 = p.x - xa, x1 = p.y - ya, x2 = p.z - za;
             c00 += x0 * x0; c01 += x0 * x1; c02 += x0 * x2;
             c11 += x1 * x1; c12 += x1 * x2; c22 += x2 * x2;
@@ -1217,8 +1301,8 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
     if (ix->g.dense && tile_R > 0) {
         unsigned long long* st = nullptr;
         if (getenv("PCP_KNN_DEBUG")) {
-            PCP_TRY(dmalloc(ctx, &st, 4));
-            PCP_HIP(ctx, hipMemsetAsync(st, 0, 4 * sizeof(unsigned long long), ctx->stream));
+            PCP_TRY(dmalloc(ctx, &st, 16));
+            PCP_HIP(ctx, hipMemsetAsync(st, 0, 16 * sizeof(unsigned long long), ctx->stream));
         }
         const unsigned nbt = (unsigned)std::min<int64_t>((ix->n + 63) / 64, 1 << 20);
         // brick order of the queries: (brick key, sorted position) radix-sorted
@@ -1251,7 +1335,7 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         hipLaunchKernelGGL((k_normals<KV, false>), dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts,   \
                            ix->mapping, ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb2.f, fb.f);       \
         hipLaunchKernelGGL((k_normals_coop<KV>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts,            \
-                           ix->mapping, ix->identity, ix->pos_of_j, kk, mc, out, n_out, fb2.f)
+                           ix->mapping, ix->identity, ix->pos_of_j, kk, mc, out, n_out, fb2.f, st ? st + 4 : nullptr)
         switch (K) {
             case 1: case 4: LAUNCH_TILE(4); break;
             case 8: LAUNCH_TILE(8); break;
@@ -1268,6 +1352,18 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
             unsigned c2 = 0;
             hipMemcpy(&c2, fb2.f.count, 4, hipMemcpyDeviceToHost);
             fprintf(stderr, "pcp_normals_knn tile: the near pass deferred %u to the brick search\n", c2);
+            unsigned long long cd[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            hipMemcpy(cd, st + 4, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+            double qd[4];
+            hipMemcpy(qd, st + 9, sizeof(qd), hipMemcpyDeviceToHost);
+            unsigned long long ph[2] = {0, 0};
+            hipMemcpy(ph, st + 13, sizeof(ph), hipMemcpyDeviceToHost);
+            fprintf(stderr, "pcp_normals_knn coop: cycles per query: ring phase %.0f, global_kth in shells %.0f\n",
+                    cd[0] ? (double)ph[0] / cd[0] : 0.0, cd[0] ? (double)ph[1] / cd[0] : 0.0);
+            fprintf(stderr, "pcp_normals_knn coop: the slowest query at (%.3f, %.3f, %.3f), last k-th d2 %.4f; grid o (%.2f %.2f %.2f) h %.4f n %d %d %d\n",
+                    qd[0], qd[1], qd[2], qd[3], ix->g.o[0], ix->g.o[1], ix->g.o[2], ix->g.h, ix->g.n[0], ix->g.n[1], ix->g.n[2]);
+            fprintf(stderr, "pcp_normals_knn coop: queries %llu, brick shells mean %.2f max %llu, cycles mean %.0f max %llu\n",
+                    cd[0], cd[0] ? (double)cd[1] / cd[0] : 0.0, cd[2], cd[0] ? (double)cd[3] / cd[0] : 0.0, cd[4]);
             fprintf(stderr, "pcp_normals_knn tile: k=%d R=%d n=%lld uncertified lanes: by the list bound %llu, by the "
                     "box %llu; oversized-wave lanes: rows %llu, points %llu; deferred %u\n", k, tile_R,
                     (long long)ix->n, h[0], h[2], h[1], h[3], c);
