@@ -31,6 +31,9 @@ struct pcp_icp {
     float4* q = nullptr;          // sorted queries {x,y,z,bits(original index)}
     uint4* cand = nullptr;        // per sorted query: sorted-target positions of its kCache nearest targets
                                   // at its last search (~0u = empty slot); the winner is always among them
+    float4* hot = nullptr;        // per sorted query (PCP_VER_HOT): 2 records {x,y,z,dlb word}, {x,y,z,0}:
+                                  // the two nearest of cand (the winner among them) with D folded
+                                  // down to the third's distance -- all the verify pass reads
     uint32_t* dlb = nullptr;      // per sorted query: (float bits of D) & ~0xff | s, where s = the launch
                                   // (mod 256) of its last search and D a lower bound (m) on the distance
                                   // from the query, at that launch's pose, to every target NOT in cand
@@ -88,6 +91,9 @@ constexpr int kIcpBlock = 256;
 #ifndef PCP_RING_WAVES
 #define PCP_RING_WAVES 8
 #endif
+#ifndef PCP_VER_HOT  // verify reads per-query hot records (positions inline) instead of gathering
+#define PCP_VER_HOT 0
+#endif
 constexpr int kAcc = 24;
 
 struct IcpArgs {
@@ -104,6 +110,7 @@ struct IcpArgs {
     float mc;           // cell-unit margin for pruning
     double* partials;
     uint4* cand;
+    float4* hot;
     uint32_t* dlb;
     const float* pose_hist;
     uint32_t launch;    // this launch's index (mod 2^32)
@@ -580,6 +587,26 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     LaneAcc acc;
     acc.zero();
     const float r2m = a.r2 * 1.0003f;
+#if PCP_VER_HOT
+    // software pipeline: the query and its two hot cache records two chunks ahead (plain
+    // coalesced streams, no gathers)
+    const float4 far4 = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+    auto raw = [&](int64_t k, float4& q, float4& h0, float4& h1) {
+        const int64_t i = (cstart_ + k * cstep) * 64 + lane;
+        if (k < nsteps && i < a.nq) {
+            q = a.q[i];
+            h0 = a.hot[2 * i];
+            h1 = a.hot[2 * i + 1];
+        } else {
+            q = make_float4(0.f, 0.f, 0.f, 0.f);
+            h0 = far4;
+            h1 = far4;
+        }
+    };
+    float4 q1, q2, a1, a2, b1, b2;
+    raw(0, q1, a1, b1);
+    raw(1, q2, a2, b2);
+#else
     // software pipeline: the query, cache and bound words two chunks ahead, the cached points'
     // gathers one chunk ahead (this chunk's were issued during the previous one)
     const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -609,6 +636,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     raw(0, q1, c1_, D1);
     raw(1, q2, c2_, D2);
     gather(c1_, g0, g1, g2, g3);
+#endif
     for (int64_t k0 = 0; k0 < nsteps; k0 += kFlush) {  // stretches of kFlush chunks
         const int64_t k1 = min(k0 + (int64_t)kFlush, nsteps);
         // centre: the stretch's first query under the current pose (wave-uniform)
@@ -621,6 +649,14 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             const int64_t i = (cstart_ + k * cstep) * 64 + lane;
             const bool valid = i < a.nq;
             const float4 qq = q1;
+#if PCP_VER_HOT
+            const float4 p0 = a1, p1 = b1, p2 = far4;
+            const uint32_t Dw = valid ? __float_as_uint(a1.w) : 0u;
+            q1 = q2;
+            a1 = a2;
+            b1 = b2;
+            raw(k + 2, q2, a2, b2);
+#else
             const uint32_t Dw = valid ? D1 : 0u;
             const float4 p0 = g0, p1 = g1, p2 = g2, p3 = g3;
             // issue chunk c+1's gathers and chunk c+2's words before using chunk c's
@@ -629,8 +665,24 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             c1_ = c2_;
             D1 = D2;
             raw(k + 2, q2, c2_, D2);
+#endif
             float qx, qy, qz;
             xform(a, qq, qx, qy, qz);
+#if PCP_VER_HOT
+            // winner of the two hot points by d2; an exact tie within rmax (the index decides,
+            // which the hot records do not carry) is searched
+            float m = icp_d2(qx, qy, qz, p0), px = p0.x, py = p0.y, pz = p0.z;
+            bool tie;
+            {
+                const float e = icp_d2(qx, qy, qz, p1);
+                tie = e == m && e <= a.r2;
+                const bool t = e < m;
+                m = t ? e : m;
+                px = t ? p1.x : px;
+                py = t ? p1.y : py;
+                pz = t ? p1.z : pz;
+            }
+#else
             // winner among the cached points by (d2, target index); an empty slot never wins
             float m = INFINITY, px = 0.f, py = 0.f, pz = 0.f;
             int mj = 0x7fffffff;
@@ -648,6 +700,8 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             take(p1);
             take(p2);
             if (!PCP_CACHE3) take(p3);
+            const bool tie = false;
+#endif
             // the query at the pose of its last search
             const uint32_t sl = Dw & 0xffu;
             const float4 A = s_pose[sl][0], B = s_pose[sl][1], C = s_pose[sl][2];
@@ -658,7 +712,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             const float lb = __uint_as_float(Dw & ~0xffu) * 0.99998f - delta;  // every uncached point is >= lb
             // the nearest cached point is the exact 1-NN (it beats lb), or nothing is within rmax
             const float thr = fminf(m * 1.0003f, r2m);
-            bool ok = valid && ((a.launch - Dw) & 0xffu) < kMaxAge && lb > 0.f && thr + 1e-12f < lb * lb;
+            bool ok = valid && !tie && ((a.launch - Dw) & 0xffu) < kMaxAge && lb > 0.f && thr + 1e-12f < lb * lb;
             ok = ok && !(a.dbg & kDbgNoVerify);
             const bool srch = valid && !ok;
             const uint64_t msk = __ballot(srch);
@@ -927,7 +981,23 @@ struct OctResult {
     float wx = 0.f, wy = 0.f, wz = 0.f;
     uint32_t c0 = ~0u, c1 = ~0u, c2 = ~0u;  // the cache: positions of the 3 kept points
     float dnext = INFINITY;    // lower bound on the d2 of every scanned point not kept
+    float4 h0 = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h1 = h0;  // the hot pair: the kept points less the last by (d2, index)
+    float edrop = INFINITY;    // exact d2 of the dropped (third) kept point
 };
+
+// the hot pair of the 3 kept points: drop the largest by (d2, index), so the winner stays
+__device__ __forceinline__ void hot_pair(OctResult& o, const float4 p0, const float4 p1, const float4 p2, float qx,
+                                         float qy, float qz) {
+    const float e0 = icp_d2(qx, qy, qz, p0), e1 = icp_d2(qx, qy, qz, p1), e2 = icp_d2(qx, qy, qz, p2);
+    const int i0 = __float_as_int(p0.w), i1 = __float_as_int(p1.w), i2 = __float_as_int(p2.w);
+    const bool d1 = e1 > e0 || (e1 == e0 && i1 > i0);  // p1 above p0
+    const float em = d1 ? e1 : e0;
+    const int im = d1 ? i1 : i0;
+    const bool d2 = e2 > em || (e2 == em && i2 > im);  // p2 is the largest
+    o.edrop = d2 ? e2 : em;
+    o.h0 = d2 || d1 ? p0 : p1;
+    o.h1 = d2 ? p1 : p2;
+}
 
 __device__ __forceinline__ void take_exact(OctResult& o, const float4 p, uint32_t pos, float qx, float qy, float qz,
                                            int& wj) {
@@ -960,6 +1030,7 @@ __device__ __forceinline__ OctResult octant_packed(const IcpArgs& a, const uint3
     take_exact(o, p0, o.c0, qx, qy, qz, wj);
     take_exact(o, p1, o.c1, qx, qy, qz, wj);
     take_exact(o, p2, o.c2, qx, qy, qz, wj);
+    if (PCP_VER_HOT) hot_pair(o, p0, p1, p2, qx, qy, qz);
     o.dnext = k.t3 == kKeyMax ? INFINITY : __uint_as_float(k.t3 & ~0xffu);
     return o;
 }
@@ -980,6 +1051,7 @@ __device__ __noinline__ OctResult octant_exact(const IcpArgs& a, uint32_t rs0, u
     take_exact(o, p0, o.c0, qx, qy, qz, wj);
     take_exact(o, p1, o.c1, qx, qy, qz, wj);
     take_exact(o, p2, o.c2, qx, qy, qz, wj);
+    if (PCP_VER_HOT) hot_pair(o, p0, p1, p2, qx, qy, qz);
     o.dnext = b.d3;
     return o;
 }
@@ -1087,6 +1159,15 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
             const float D = outside ? dout * 0.9999f
                                     : (settled ? fminf(sqrtf(o.dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : o.dnext);
             if (lead) a.cand[i] = make_uint4(o.c0, o.c1, o.c2, pack_dlb(D, a.launch));
+#if PCP_VER_HOT
+            // the verify pass's records: D folded down to the dropped point's distance (0 when
+            // unsettled: the fallback pass rewrites them)
+            if (lead) {
+                const float Dh = settled ? fminf(D, sqrtf(o.edrop) * 0.9999f) : 0.f;
+                a.hot[2 * i] = make_float4(o.h0.x, o.h0.y, o.h0.z, __uint_as_float(pack_dlb(Dh, a.launch)));
+                a.hot[2 * i + 1] = make_float4(o.h1.x, o.h1.y, o.h1.z, 0.f);
+            }
+#endif
         }
         // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
         const bool fb = valid && lead && !settled;
@@ -1240,6 +1321,8 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
             // no bound kept: the next launch searches it again
 #if PCP_CACHE3
             a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, pack_dlb(0.f, a.launch));
+            if (PCP_VER_HOT)
+                a.hot[2 * i] = make_float4(INFINITY, INFINITY, INFINITY, __uint_as_float(pack_dlb(0.f, a.launch)));
 #else
             a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, ~0u);
             a.dlb[i] = pack_dlb(0.f, a.launch);
@@ -1670,6 +1753,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     const double rr = (0.5 - (double)a.mc) * a.g.h;
     a.cert2 = (float)(rr * rr * (1.0 - 1e-5));
     a.cand = icp->cand;
+    a.hot = icp->hot;
     a.dlb = icp->dlb;
     a.pose_hist = icp->pose_hist;
     a.launch = (uint32_t)icp->launches;
@@ -1913,8 +1997,11 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_dev, 24);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->cand, icp->nq + 1);
     if (!rc && !PCP_CACHE3) rc = pcp::dmalloc(ctx, &icp->dlb, icp->nq + 1);  // else packed in cand.w
+    if (!rc && PCP_VER_HOT) rc = pcp::dmalloc(ctx, &icp->hot, 2 * (icp->nq + 1));
     if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_hist, pcp::kHist * 12);
     if (!rc && (hipMemsetAsync(icp->cand, 0xff, (size_t)(icp->nq + 1) * sizeof(uint4), ctx->stream) != hipSuccess ||
+                (icp->hot && hipMemsetAsync(icp->hot, 0, (size_t)2 * (icp->nq + 1) * sizeof(float4), ctx->stream) !=
+                                 hipSuccess) ||
 
                 (icp->dlb && hipMemsetAsync(icp->dlb, 0, (size_t)(icp->nq + 1) * sizeof(uint32_t), ctx->stream) !=
                                  hipSuccess) ||
@@ -1961,6 +2048,7 @@ int pcp_icp_destroy(pcp_icp* icp) {
     pcp::dfree(icp->ctx, icp->partials);
     pcp::dfree(icp->ctx, icp->acc);
     pcp::dfree(icp->ctx, icp->cand);
+    pcp::dfree(icp->ctx, icp->hot);
     pcp::dfree(icp->ctx, icp->dlb);
     pcp::dfree(icp->ctx, icp->pose_hist);
     pcp::dfree(icp->ctx, icp->sv);
