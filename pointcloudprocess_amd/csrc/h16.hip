@@ -90,26 +90,47 @@ __global__ void k_h16_sorted_counts(const int32_t* mapping, int64_t n, int64_t n
         if (own) inv[c] = (int32_t)s;
     }
 }
-// one wave per 64 consecutive caller rows: lane r fetches row r's source / destination, then
-// the wave copies the rows one after the other (coalesced reads and writes)
+// one wave per 64 consecutive caller rows.  Their destination is one contiguous span of the
+// caller CSR, so the wave walks it flat: lane t copies span elements t, t + 64, ... (full-line
+// writes every instruction), each finding its row from the 64 row starts staged in LDS (rows
+// are ~n-bar long, so a lane advances about one row per step).  The per-row form (the wave
+// copying one row after another) left a dependent load->store per row and lanes idle past
+// each row's end.
 __global__ __launch_bounds__(kB) void k_h16_rows_to_caller(const int32_t* inv, int64_t n_owned, const int64_t* soff,
-                                                           const int64_t* offsets, const int32_t* tmp,
-                                                           int32_t* out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t w = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); w * 64 < n_owned; w += nw) {
-        const int64_t c = w * 64 + lane;
-        int64_t src = 0, dst = 0, len = 0;
-        if (c < n_owned) {
-            dst = offsets[c];
-            len = offsets[c + 1] - dst;
-            src = soff[inv[c]];
-        }
+                                                           const int64_t* offsets, const int32_t* __restrict__ tmp,
+                                                           int32_t* __restrict__ out) {
+    constexpr int kW = kB / 64;
+    __shared__ int64_t s_dst[kW][65];
+    __shared__ int64_t s_src[kW][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t nw = (int64_t)gridDim.x * kW;
+    for (int64_t w = blockIdx.x * (int64_t)kW + wid; w * 64 < n_owned; w += nw) {
         const int rows = (int)min((int64_t)64, n_owned - w * 64);
-        for (int r = 0; r < rows; r++) {
-            const int64_t rs = __shfl(src, r, 64), rd = __shfl(dst, r, 64), rl = __shfl(len, r, 64);
-            for (int64_t t = lane; t < rl; t += 64) out[rd + t] = tmp[rs + t];
+        const int64_t c = w * 64 + lane;
+        if (lane < rows) {
+            s_dst[wid][lane] = offsets[c];
+            s_src[wid][lane] = soff[inv[c]];
         }
+        if (lane == 0) s_dst[wid][rows] = offsets[w * 64 + rows];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t d0 = s_dst[wid][0], d1 = s_dst[wid][rows];
+        int r = 0;
+        int64_t rd = d0, rn = s_dst[wid][1], rs = s_src[wid][0];
+        for (int64_t p = d0 + lane; p < d1; p += 64) {
+            while (p >= rn) {  // empty rows are skipped too
+                r++;
+                rd = rn;
+                rn = s_dst[wid][r + 1];
+                rs = s_src[wid][r];
+            }
+            out[p] = tmp[rs + (p - rd)];
+        }
+        // the LDS rows are rewritten by the wave's next group
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
