@@ -89,7 +89,7 @@ constexpr int kIcpBlock = 256;
 #endif
 
 #ifndef PCP_RING_WAVES
-#define PCP_RING_WAVES 8
+#define PCP_RING_WAVES 6
 #endif
 #ifndef PCP_VER_HOT  // verify reads per-query hot records (positions inline) instead of gathering
 #define PCP_VER_HOT 0
@@ -254,6 +254,78 @@ struct Best {
             consider(qx, qy, qz, pts[k], k);
         }
     }
+    // G lanes per query: lane `sub` of the group takes entries sub, sub + G, ... of the same
+    // ranges (strided scan / scan_rows), then merge_group() gives every lane of the group the
+    // group's (d2, index) winner.  A lane prunes with its own bound, which is never below the
+    // group's, so nothing the group's winner needs is skipped.
+    template <int G, typename P>
+    __device__ __forceinline__ void scan_g(const P* pts, uint32_t s, uint32_t e, float qx, float qy, float qz,
+                                           uint32_t sub) {
+        if (G == 1) {
+            scan(pts, s, e, qx, qy, qz);
+            return;
+        }
+        uint32_t k = s + sub;
+        for (; k + 3 * G < e; k += 4 * G) {
+            const float4 p0 = pts[k], p1 = pts[k + G], p2 = pts[k + 2 * G], p3 = pts[k + 3 * G];
+            consider(qx, qy, qz, p0, k);
+            consider(qx, qy, qz, p1, k + G);
+            consider(qx, qy, qz, p2, k + 2 * G);
+            consider(qx, qy, qz, p3, k + 3 * G);
+        }
+        for (; k < e; k += G) consider(qx, qy, qz, pts[k], k);
+    }
+    template <int G, typename P, int NR>
+    __device__ __forceinline__ void scan_rows_g(const P* pts, const uint32_t (&rs)[NR], const uint32_t (&rn)[NR],
+                                                float qx, float qy, float qz, uint32_t sub) {
+        if (G == 1) {
+            scan_rows(pts, rs, rn, qx, qy, qz);
+            return;
+        }
+        static_assert(NR == 3 || NR == 4, "3 or 4 rows");
+        const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = NR == 4 ? c3 + rn[NR - 1] : c3;
+        dbg_len = L;
+        const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[NR - 1] - c3;
+        const uint32_t c3e = NR == 4 ? c3 : 0xffffffffu;
+        auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3e, o0, o1, o2, o3); };
+        uint32_t v = sub;
+        constexpr int U = PCP_SCAN_UNROLL;
+        for (; v + (U - 1) * G < L; v += U * G) {
+            uint32_t k[U];
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) k[u] = addr(v + u * G);
+#pragma unroll
+            for (int u = 0; u < U; u++) p[u] = pts[k[u]];
+#pragma unroll
+            for (int u = 0; u < U; u++) consider(qx, qy, qz, p[u], k[u]);
+        }
+        for (; v < L; v += G) {
+            const uint32_t k = addr(v);
+            consider(qx, qy, qz, pts[k], k);
+        }
+    }
+    template <int G>
+    __device__ __forceinline__ void merge_group() {
+#pragma unroll
+        for (int s = 1; s < G; s <<= 1) {
+            const float od = __shfl_xor(bd, s, 64);
+            const int oj = __shfl_xor(bj, s, 64);
+            const uint32_t ok = (uint32_t)__shfl_xor((int)bk, s, 64);
+#if PCP_TRACK_BEST
+            const float ox = __shfl_xor(px, s, 64), oy = __shfl_xor(py, s, 64), oz = __shfl_xor(pz, s, 64);
+#endif
+            const bool t = od < bd || (od == bd && oj < bj);
+            bd = t ? od : bd;
+            bj = t ? oj : bj;
+            bk = t ? ok : bk;
+#if PCP_TRACK_BEST
+            px = t ? ox : px;
+            py = t ? oy : py;
+            pz = t ? oz : pz;
+#endif
+        }
+    }
     template <typename P>
     __device__ __forceinline__ void fetch(const P* pts) {
         const float4 p = pts[bk];
@@ -266,13 +338,17 @@ struct Best {
 // still within the (shrinking) bound -- one contiguous point range per row on a dense grid.
 // Rows and cells are pruned conservatively (margin mc cells, 2e-5 relative on d2), so the
 // winner equals an exhaustive lexicographic (d2, index) search.
+template <int G = 1>
 __device__ __forceinline__ void box_search(const GridDesc& g, const float4* tp, float qx, float qy,
-                                           float qz, float mc, Best& b) {
+                                           float qz, float mc, Best& b, uint32_t sub = 0) {
     const float fx = cell_f<float>(g, qx, 0), fy = cell_f<float>(g, qy, 1), fz = cell_f<float>(g, qz, 2);
     const int cy = (int)floorf(fy), cz = (int)floorf(fz);
     const float ly = fy - (float)cy, lz = fz - (float)cz;
     const float inv_h2 = g.inv_hf * g.inv_hf;
     const float rc = sqrtf(b.bd * 1.00002f * inv_h2) + mc;  // initial radius in cells
+    // G > 1: rows are pruned by the group's bound as of its last merge (every lane of the group
+    // then cuts the same x-range, so the strided entries still partition it)
+    float gb = b.bd;
     const int ry = (int)ceilf(rc) + 1, rz = ry;
     for (int oz = 0; oz <= 2 * rz; oz++) {
         const int dz = (oz & 1) ? -((oz + 1) >> 1) : (oz >> 1);  // 0, -1, +1, -2, +2, ...
@@ -286,22 +362,25 @@ __device__ __forceinline__ void box_search(const GridDesc& g, const float4* tp, 
             if (y < 0 || y >= g.n[1]) continue;
             const float gy = dy < 0 ? (ly + (float)(-dy - 1)) : (dy > 0 ? (1.f - ly + (float)(dy - 1)) : 0.f);
             const float gyz2 = gz2 + (gy > mc ? (gy - mc) * (gy - mc) : 0.f);
-            const float lim = b.bd * 1.00002f * inv_h2 - gyz2;  // remaining x extent^2 (cells)
+            const float lim = (G == 1 ? b.bd : gb) * 1.00002f * inv_h2 - gyz2;  // remaining x extent^2 (cells)
             if (lim < 0.f) continue;
             const float rx = sqrtf(lim) + mc;
             const int xa = max((int)floorf(fx - rx), 0), xb = min((int)floorf(fx + rx), g.n[0] - 1);
             if (xa > xb) continue;
             if (g.dense) {
                 const int64_t c = dense_id(g, xa, y, z);
-                b.scan(tp, g.cstart[c], g.cstart[c + (xb - xa + 1)], qx, qy, qz);
+                b.scan_g<G>(tp, g.cstart[c], g.cstart[c + (xb - xa + 1)], qx, qy, qz, sub);
             } else {
                 for (int x = xa; x <= xb; x++) {
                     uint32_t s, e;
-                    if (cell_range(g, x, y, z, s, e)) b.scan(tp, s, e, qx, qy, qz);
+                    if (cell_range(g, x, y, z, s, e)) b.scan_g<G>(tp, s, e, qx, qy, qz, sub);
                 }
             }
         }
+        b.merge_group<G>();  // the group's bound prunes the next plane
+        gb = b.bd;
     }
+    b.merge_group<G>();
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -1234,17 +1313,31 @@ __global__ void __launch_bounds__(kIcpBlock, MINW) k_icp_octant(IcpArgs a, const
 // octant pass's provisional winner when it has one.  Queries come from the compacted
 // fallback list (or are all queries when ring_all is set, i.e. on a sparse grid); waves
 // take 64-entry chunks grid-stride and accumulate like the octant pass.
-__global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs a, double* partials,
-                                                                        const int32_t* list, const uint32_t* list_n) {
-    load_pose(a);
+// G lanes per query: the lanes of a query split its rows (Best::scan_rows_g / scan_g) and
+// merge after each plane; the group's first lane writes and accumulates.  Measured per launch
+// (profiles/r02_ring): the short fallback lists of later launches are latency-bound and run
+// ~35 % faster with G = 4, while the long early lists (wide "nothing within rmax" boxes of
+// short rows, whose per-row bookkeeping G lanes would repeat) want one lane per query.
+// PCP_RING_G = 0 picks G on the device from the list's length (ring_lanes), else fixes it.
+#ifndef PCP_RING_G
+#define PCP_RING_G 0
+#endif
+__device__ __forceinline__ int ring_lanes(int64_t n, int64_t nq) {
+    if (n * 1000 > nq) return 1;
+    if (n * 8000 > nq) return 2;
+    return 4;
+}
+template <int G>
+__device__ __forceinline__ void ring_run(IcpArgs& a, double (*s_acc)[kAcc], const int32_t* list, const uint32_t* list_n) {
     constexpr int kW = kIcpBlock / 64;
-    __shared__ double s_acc[kW][kAcc];
+    constexpr int QPC = 64 / G;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane < kAcc) s_acc[wid][lane] = 0.0;
+    const uint32_t sub = (uint32_t)(lane % G);
+    const bool lead = sub == 0;
     const int64_t n = a.ring_all ? a.nq : (int64_t)*list_n;
-    const XcdSplit xs = xcd_split((n + 63) / 64, kW);
+    const XcdSplit xs = xcd_split((n + QPC - 1) / QPC, kW);
     for (int64_t c = xs.c0 + xs.w; c < xs.c1; c += xs.nw) {
-        const int64_t j = c * 64 + lane;
+        const int64_t j = c * QPC + lane / G;
         const bool valid = j < n;
         Best b{a.r2, 0x7fffffff, 0u, 0.f, 0.f, 0.f};
         float qx = 0.f, qy = 0.f, qz = 0.f;
@@ -1304,7 +1397,8 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
                         rs[r] = in ? g.cstart[cc] : 0u;
                         rn[r] = in ? g.cstart[cc + (xhi - xlo + 1)] - rs[r] : 0u;
                     }
-                    b.scan_rows(a.tp, rs, rn, qx, qy, qz);
+                    b.scan_rows_g<G>(a.tp, rs, rn, qx, qy, qz, sub);
+                    b.merge_group<G>();
                 }
                 const float m = fminf(fminf(fminf(fx - (float)(cx - 1), (float)(cx + 2) - fx),
                                             fminf(fy - (float)(cy - 1), (float)(cy + 2) - fy)),
@@ -1314,24 +1408,45 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
                 const bool found = b.bj != 0x7fffffff;
                 done = (found && b.bd <= c2) || (!found && a.r2 <= c2);
             }
-            if ((a.dbg & kDbgCount) && done) atomicAdd(a.dbgcnt + 5, 1ull);
-            if (!done) box_search(a.g, a.tp, qx, qy, qz, a.mc, b);
-            if ((a.dbg & kDbgCount) && b.bj != 0x7fffffff) atomicAdd(a.dbgcnt + 6, 1ull);
+            if ((a.dbg & kDbgCount) && lead && done) atomicAdd(a.dbgcnt + 5, 1ull);
+            if (!done) box_search<G>(a.g, a.tp, qx, qy, qz, a.mc, b, sub);
+            if ((a.dbg & kDbgCount) && lead && b.bj != 0x7fffffff) atomicAdd(a.dbgcnt + 6, 1ull);
             const bool ok = b.bj != 0x7fffffff;
             // no bound kept: the next launch searches it again
+            if (lead) {
 #if PCP_CACHE3
-            a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, pack_dlb(0.f, a.launch));
-            if (PCP_VER_HOT)
-                a.hot[2 * i] = make_float4(INFINITY, INFINITY, INFINITY, __uint_as_float(pack_dlb(0.f, a.launch)));
+                a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, pack_dlb(0.f, a.launch));
+                if (PCP_VER_HOT)
+                    a.hot[2 * i] = make_float4(INFINITY, INFINITY, INFINITY, __uint_as_float(pack_dlb(0.f, a.launch)));
 #else
-            a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, ~0u);
-            a.dlb[i] = pack_dlb(0.f, a.launch);
+                a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, ~0u);
+                a.dlb[i] = pack_dlb(0.f, a.launch);
 #endif
+            }
         }
-        const bool acc_ok = valid && b.bj != 0x7fffffff && !(a.dbg & kDbgNoAccum);
+        const bool acc_ok = valid && lead && b.bj != 0x7fffffff && !(a.dbg & kDbgNoAccum);
         if (acc_ok) b.fetch(a.tp);
         chunk_accumulate(acc_ok, qx, qy, qz, b, s_acc[wid], lane);
     }
+}
+
+__global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs a, double* partials,
+                                                                        const int32_t* list, const uint32_t* list_n) {
+    load_pose(a);
+    constexpr int kW = kIcpBlock / 64;
+    __shared__ double s_acc[kW][kAcc];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane < kAcc) s_acc[wid][lane] = 0.0;
+    const int64_t n = a.ring_all ? a.nq : (int64_t)*list_n;
+    const int G = PCP_RING_G ? PCP_RING_G : (a.ring_all ? 1 : ring_lanes(n, a.nq));  // uniform over the grid
+    if (G == 1)
+        ring_run<1>(a, s_acc, list, list_n);
+    else if (G == 2)
+        ring_run<2>(a, s_acc, list, list_n);
+    else if (G == 4)
+        ring_run<4>(a, s_acc, list, list_n);
+    else
+        ring_run<8>(a, s_acc, list, list_n);
     write_wave_partials(s_acc, partials + (int64_t)blockIdx.x * kAcc);
 }
 
