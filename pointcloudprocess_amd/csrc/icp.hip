@@ -63,6 +63,7 @@ struct pcp_icp {
     int dbg = 0;                  // PCP_ICP_ABLATE flags (profiling only)
     int oct_g_first = 1;          // lanes per query of the octant pass: first launch (all queries)
     int oct_g_list = PCP_OCT_GLIST;  // ... and the verify pass's search lists (PCP_OCT_G=first,list)
+    int ring_g = 0;               // lanes per query of the fallback pass (env PCP_RING_LANES), 0 = by length
     unsigned long long* dbgcnt = nullptr;  // kDbgCount: [candidates, rows, queries]
     uint2* dbgfz = nullptr;       // kDbgCount: per 64-query chunk {slack bits, launch} (freeze model)
     double last_ms = 0.0;
@@ -129,6 +130,7 @@ struct IcpArgs {
     int ring_all;       // ring kernel: process every query (sparse grid) instead of the list
     int dbg;            // ablation flags (PCP_ICP_ABLATE, profiling builds of the bench only)
     int oct_g;          // octant pass lanes per query: 1, 2, 4, 8, or 0 = by the list's density
+    int ring_g;         // fallback pass lanes per query: 1, 2, 4, 8, or 0 = PCP_RING_G / by length
     const float* pose;  // device poses (current, previous: 24 floats) overriding R/t, Rp/tq, or null
     unsigned long long* dbgcnt;  // kDbgCount counters, or null
     uint2* dbgfz;       // kDbgCount: chunk freeze model state
@@ -1438,7 +1440,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
     const int64_t n = a.ring_all ? a.nq : (int64_t)*list_n;
-    const int G = PCP_RING_G ? PCP_RING_G : (a.ring_all ? 1 : ring_lanes(n, a.nq));  // uniform over the grid
+    const int G = a.ring_g ? a.ring_g : PCP_RING_G ? PCP_RING_G : (a.ring_all ? 1 : ring_lanes(n, a.nq));  // uniform
     if (G == 1)
         ring_run<1>(a, s_acc, list, list_n);
     else if (G == 2)
@@ -1948,6 +1950,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     }
     // 3. exact fallback (or every query on a sparse grid)
     a.partials = part_r;
+    a.ring_g = icp->ring_g;
     hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, ctx->stream, a, part_r,
                        (const int32_t*)icp->fbc, (const uint32_t*)(icp->fb_off + a.nseg));
     PCP_HIP(ctx, hipEventRecord(e1, ctx->stream));
@@ -2143,6 +2146,10 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
             if (ok(f) || f == 0) icp->oct_g_first = f;
             if (ok(l) || l == 0) icp->oct_g_list = l;
         }
+    }
+    if (const char* rg = std::getenv("PCP_RING_LANES")) {  // A/B and tests: fallback-pass lanes per query
+        const int g = std::atoi(rg);
+        if (g == 0 || g == 1 || g == 2 || g == 4 || g == 8) icp->ring_g = g;
     }
     if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgcnt, 32);
     if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgfz, icp->nq / 64 + 2);

@@ -322,3 +322,42 @@ def test_octant_lane_groups_exact(ctx, gs, monkeypatch):
         rc, dT = ops.icp_solve(acc.cpu().numpy())
         assert rc == 0
         T = dT @ T
+
+
+@pytest.mark.parametrize("lanes", ["1", "2", "4", "8"])
+def test_fallback_lane_groups_exact(ctx, lanes, monkeypatch):
+    """G lanes per query in the fallback pass (PCP_RING_LANES; the default picks G from the
+    list length): the strided row scans, the per-plane group merge and box_search's group-bound
+    row cuts must give the oracle's correspondences.  Cells of rmax / 2.5 over a sparse scan send many
+    queries through box_search, including "nothing within rmax" boxes; lattice ties and a dense
+    cluster exercise the (d2, index) order."""
+    from pointcloudprocess_amd import ops, synth
+    monkeypatch.setenv("PCP_RING_LANES", lanes)
+    T_true = synth.rigid()
+    tgt, q = _pair(60_000, 61, T_true, extent=(30.0, 30.0))  # a dense cell table
+    rng = np.random.default_rng(62)
+    c0 = tgt[0].numpy()
+    cluster = (c0 + rng.uniform(-0.02, 0.02, (800, 3))).astype(np.float32)
+    lat = np.stack(np.meshgrid(np.arange(6), np.arange(6), np.arange(3), indexing="ij"), -1).reshape(-1, 3)
+    lat = (lat * 0.1 + np.array([5.0, 5.0, 1.0])).astype(np.float32)
+    tgt = torch.from_numpy(np.concatenate([tgt.numpy(), cluster, lat]))
+    qn = np.concatenate([q.numpy(), cluster[:200] + 0.003, (lat + 0.05).astype(np.float32),
+                         (lat + np.array([0.0, 0.0, 0.2], np.float32)).astype(np.float32)])
+    q = torch.from_numpy(qn.astype(np.float32))
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+    icp = ops.ICP(index, q.to(ctx.device))
+    oi = ora.F32Index(tgt.numpy())
+    T = np.eye(4)
+    fallbacks = 0
+    for it in range(5):
+        acc, ci, cd = icp.step(T, 0.25, corr=True)
+        fallbacks += icp.last_fallback()
+        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+        ei, ed = oi.correspond(q.numpy(), R, t, 0.25)
+        gi = ci.cpu().numpy()
+        assert np.array_equal(gi, ei), f"G {lanes} iter {it}: {(gi != ei).sum()} mismatching correspondences"
+        assert np.array_equal(cd.cpu().numpy()[ei >= 0], ed[ei >= 0])
+        rc, dT = ops.icp_solve(acc.cpu().numpy())
+        assert rc == 0
+        T = dT @ T
+    assert fallbacks > 200  # the fallback pass really ran on a list
