@@ -8,6 +8,8 @@
 #include <string>
 #include <unordered_map>
 
+#include <vector>
+
 #include "../../include/pcp.h"
 
 struct pcp_ctx {
@@ -22,6 +24,9 @@ struct pcp_ctx {
     // look-back scan state (scan.hip): per-tile status words tagged with the call's epoch, so
     // no clearing pass is needed per call; [tiles] u64 status, then the tile counter and total
     uint64_t* scan_status = nullptr;
+    // timing events returned by destroyed ICP handles, reused by the next (creating and
+    // destroying ~44 events per registration cost ~0.3 ms of host time)
+    std::vector<hipEvent_t> event_pool;
     int64_t scan_tiles = 0;
     uint32_t scan_epoch = 0;
     // Caching device allocator for the library's internal buffers (index builds, ICP state,
@@ -59,6 +64,9 @@ int scratch(pcp_ctx* ctx, size_t bytes, void** out);
 int cache_alloc(pcp_ctx* ctx, size_t bytes, void** p);
 void dfree(pcp_ctx* ctx, void* p);
 void cache_release(pcp_ctx* ctx);
+// a timing event from ctx's pool (or a new one); event_put returns it to the pool
+hipError_t event_get(pcp_ctx* ctx, hipEvent_t* ev);
+void event_put(pcp_ctx* ctx, hipEvent_t ev);
 
 template <typename T>
 int dmalloc(pcp_ctx* ctx, T** p, size_t count) {

@@ -96,6 +96,19 @@ void dfree(pcp_ctx* ctx, void* p) {
     }
 }
 
+hipError_t event_get(pcp_ctx* ctx, hipEvent_t* ev) {
+    if (!ctx->event_pool.empty()) {
+        *ev = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        return hipSuccess;
+    }
+    return hipEventCreate(ev);
+}
+
+void event_put(pcp_ctx* ctx, hipEvent_t ev) {
+    if (ev) ctx->event_pool.push_back(ev);
+}
+
 void cache_release(pcp_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->free_blocks) {
@@ -138,6 +151,7 @@ int pcp_ctx_destroy(pcp_ctx* ctx) {
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->scan_status) (void)hipFree(ctx->scan_status);
     pcp::cache_release(ctx);
+    for (hipEvent_t ev : ctx->event_pool) (void)hipEventDestroy(ev);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return PCP_OK;

@@ -1897,9 +1897,9 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     if (T_dev) {  // device-resident loop: one event pair per launch, read by pcp_icp_kernel_ms
         if (icp->ntev == icp->tev.size()) {
             std::pair<hipEvent_t, hipEvent_t> pr{nullptr, nullptr};
-            PCP_HIP(ctx, hipEventCreate(&pr.first));
-            if (hipEventCreate(&pr.second) != hipSuccess) {
-                (void)hipEventDestroy(pr.first);
+            PCP_HIP(ctx, pcp::event_get(ctx, &pr.first));
+            if (pcp::event_get(ctx, &pr.second) != hipSuccess) {
+                pcp::event_put(ctx, pr.first);
                 return set_error(ctx, PCP_ERR_HIP, "hipEventCreate");
             }
             icp->tev.push_back(pr);
@@ -2089,10 +2089,10 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     icp->nq = nfin;
     icp->nq_in = nq;
     icp->q = qs;
-    int dev_cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
-        dev_cus = prop.multiProcessorCount;
+    int dev_cus = 256;  // one attribute query (the whole hipDeviceProp_t costs ~0.1 ms per create)
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess && cus > 0)
+        dev_cus = cus;
     const int64_t want = (icp->nq + pcp::kIcpBlock - 1) / pcp::kIcpBlock;
     icp->nb_fast = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_OCT_WAVES));
     icp->nb_fast_l = (int)std::max<int64_t>(1, std::min<int64_t>(icp->nb_fast, (int64_t)dev_cus * PCP_OCT_WAVES_LIST));
@@ -2135,8 +2135,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_count, (size_t)nwaves);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_off, (size_t)nwaves + 1);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fbc, icp->nq + 1);
-    if (!rc && (hipEventCreate(&icp->ev0) != hipSuccess || hipEventCreate(&icp->ev1) != hipSuccess ||
-                hipEventCreate(&icp->ev_mid) != hipSuccess || hipEventCreate(&icp->ev_ver) != hipSuccess))
+    if (!rc && (pcp::event_get(ctx, &icp->ev0) != hipSuccess || pcp::event_get(ctx, &icp->ev1) != hipSuccess ||
+                pcp::event_get(ctx, &icp->ev_mid) != hipSuccess || pcp::event_get(ctx, &icp->ev_ver) != hipSuccess))
         rc = pcp::set_error(ctx, PCP_ERR_HIP, "hipEventCreate failed");
     if (const char* ab = std::getenv("PCP_ICP_ABLATE")) icp->dbg = std::atoi(ab);
     if (const char* og = std::getenv("PCP_OCT_G")) {  // A/B: lanes per query, "first,list"
@@ -2185,13 +2185,13 @@ int pcp_icp_destroy(pcp_icp* icp) {
     pcp::dfree(icp->ctx, icp->fb_off);
     pcp::dfree(icp->ctx, icp->fbc);
     pcp::dfree(icp->ctx, icp->pose_dev);
-    if (icp->ev0) (void)hipEventDestroy(icp->ev0);
-    if (icp->ev1) (void)hipEventDestroy(icp->ev1);
-    if (icp->ev_mid) (void)hipEventDestroy(icp->ev_mid);
-    if (icp->ev_ver) (void)hipEventDestroy(icp->ev_ver);
+    pcp::event_put(icp->ctx, icp->ev0);
+    pcp::event_put(icp->ctx, icp->ev1);
+    pcp::event_put(icp->ctx, icp->ev_mid);
+    pcp::event_put(icp->ctx, icp->ev_ver);
     for (auto& pr : icp->tev) {
-        (void)hipEventDestroy(pr.first);
-        (void)hipEventDestroy(pr.second);
+        pcp::event_put(icp->ctx, pr.first);
+        pcp::event_put(icp->ctx, pr.second);
     }
     delete icp;
     return PCP_OK;

@@ -190,9 +190,10 @@ def run_slab_dev(engine, T0, rmax, iters, guard=None, do_scale=False, exchange=N
             ev[1].record()
             exchange.append(ev)
         engine.solve_dev(acc, T_dev, stats, do_scale)
-    st = stats.cpu().numpy()
-    T = T_dev.cpu().numpy().reshape(4, 4)
-    ok = int(flag.cpu().item()) == 0
+    # one device->host copy (and one sync) for the stats, the pose and the guard flag
+    ns = stats.numel()
+    host = torch.cat([stats.reshape(-1).double(), T_dev.reshape(-1).double(), flag.double()]).cpu().numpy()
+    st, T, ok = host[:ns], host[ns:ns + 16].reshape(4, 4).copy(), bool(host[ns + 16] == 0)
     if out_stats is not None:
         out_stats["fallback"] = float(st[2])  # queries that needed the exact fallback, all iterations
     return (float(st[1]) if st[0] == 0 and st[3] == iters else -1.0), T, ok
