@@ -116,6 +116,7 @@ def pmc_traffic():
 
 
 def cpu_info():
+    """(model, nproc, affinity CPUs, cgroup CPU quota or None)."""
     model = None
     try:
         for line in open("/proc/cpuinfo"):
@@ -131,19 +132,40 @@ def cpu_info():
                 model = line.split(":", 1)[1].strip()
     except (OSError, subprocess.SubprocessError):
         pass
-    return model, os.cpu_count(), len(os.sched_getaffinity(0))
+    quota = None
+    try:  # cgroup v2 cpu.max: "<quota> <period>" or "max <period>"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return model, os.cpu_count(), len(os.sched_getaffinity(0)), quota
+
+
+def native_oracle():
+    """The CPU baseline's oracle: built on THIS host -O3 -march=native -fopenmp (oracle/Makefile
+    `native`); falls back to the portable -O2 parity build if the host compiler fails."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ctypes as ora  # test infrastructure: the checker / baseline only
+    try:
+        path, march = ora.use_native()
+        build = f"gcc -O3 -march=native ({march}) -fopenmp -ffp-contract=off: {os.path.relpath(path, ROOT)}"
+    except (OSError, subprocess.SubprocessError) as e:
+        ora.load()
+        build = f"portable -O2 parity build (native build failed: {e})"
+    return ora, build
 
 
 def cpu_baseline(args, T_true, synth):
     """The oracle's ICP (C restatement: kd-tree + OpenMP correspondences, per-thread
-    accumulators) on bounded samples of the same workload, timed on this host.  The kd-tree
-    build and the 20 iterations are timed separately; `value` is the iteration rate with
-    the process's CPU share (OMP_NUM_THREADS, the threads this box allots to one GPU)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ctypes as ora  # test infrastructure: the checker / baseline only
+    accumulators), built -O3 -march=native on this host, on a bounded sample of the same
+    workload.  The kd-tree build and the iterations are timed separately; `value` is the
+    iteration rate with ALL the process's CPUs (affinity count); the 16-thread share one GPU
+    gets on this box and one core are reported beside it."""
     import numpy as np
-    model, ncpu, naff = cpu_info()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or naff
+    ora, build = native_oracle()
+    model, ncpu, naff, quota = cpu_info()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0")) or naff
 
     n = args.cpu_n
     side = 200.0 * math.sqrt(n / float(args.n))  # same point density as the GPU cloud
@@ -154,26 +176,31 @@ def cpu_baseline(args, T_true, synth):
         err, T, bs, its = ora.icp_timed(tgt, q, np.eye(4), args.rmax, iters, nthreads=nthreads)
         return n * iters / its / 1e6, bs, its
 
-    v_all, b_all, i_all = run(threads, args.iters)
+    v_all, b_all, i_all = run(naff, args.iters)
+    v_sh, b_sh, i_sh = run(share, args.iters) if share != naff else (v_all, b_all, i_all)
     v_1, b_1, i_1 = run(1, args.cpu_iters1)
     return {
         "value": round(v_all, 3),
         "unit": "Mcorrespondences/s",
-        "cores": threads,
+        "cores": naff,
         "kind": "port",
-        "sample": f"{n}-vs-{n} pts (same density, {side:.0f}x{side:.0f} m tile), {args.iters} ICP "
-                  f"iters of oracle/pcp_oracle.c ora_icp_timed: iterations {i_all:.2f} s (timed, = value), kd-tree "
-                  f"build {b_all:.2f} s (not in value)",
+        "sample": f"{n}-vs-{n} pts (same density, {side:.0f}x{side:.0f} m tile), {args.iters} ICP iters of "
+                  f"oracle/pcp_oracle.c ora_icp_timed on {naff} threads: iterations {i_all:.2f} s (timed, = value), "
+                  f"kd-tree build {b_all:.2f} s (not in value)",
+        "build": build,
+        "value_all": round(v_all, 3),
+        "cores_all": naff,
+        "value_share": round(v_sh, 3),
+        "cores_share": share,
+        "sample_share": f"the same sample on OMP_NUM_THREADS = {share} threads (the CPU share the harness allots one "
+                        f"GPU on this box): iterations {i_sh:.2f} s, build {b_sh:.2f} s",
         "value_1core": round(v_1, 3),
         "sample_1core": f"the same {n}-vs-{n} pts, first {args.cpu_iters1} ICP iters on 1 thread: iterations "
                         f"{i_1:.2f} s, build {b_1:.2f} s",
-        "cores_all": threads,
-        "value_all": round(v_all, 3),
         "nproc": ncpu,
         "affinity_cpus": naff,
+        "cgroup_cpu_quota": quota,
         "cpu_model": model,
-        "threads_note": "OMP_NUM_THREADS = the CPU share of one GPU on this box (the harness allots 16 threads "
-                        "per GPU); nproc shows the whole host",
     }
 
 

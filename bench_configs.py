@@ -48,14 +48,28 @@ class Timer:
         return self.ms / max(self.n, 1)
 
 
+_ORA = {}
+
+
 def _oracle():
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ctypes as ora  # test infrastructure: the cpu_baseline leg only
-    return ora
+    """The oracle built -O3 -march=native on this host (bench.native_oracle); cpu legs only."""
+    if not _ORA:
+        import bench
+        _ORA["ora"], _ORA["build"] = bench.native_oracle()
+    return _ORA["ora"]
 
 
 def _threads():
-    return int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    """Every CPU of the process's affinity set (the baselines' `cores`)."""
+    return len(os.sched_getaffinity(0))
+
+
+def _cpu_meta(rec):
+    import bench
+    model, ncpu, naff, quota = bench.cpu_info()
+    rec.update({"build": _ORA.get("build"), "cores_all": naff, "nproc": ncpu, "affinity_cpus": naff,
+                "cgroup_cpu_quota": quota, "cpu_model": model})
+    return rec
 
 
 def street_aos48(n, seed, device):
@@ -117,7 +131,7 @@ def cfg_c1(ctx, args, rank, timer):
         t0 = time.perf_counter()
         vox, _ = ora.voxel_filter(host, 0.1)
         vx = np.stack([vox["x"], vox["y"], vox["z"]], 1)
-        ora.KdTree(vx).knn(qh, 1)
+        ora.KdTree(vx).knn(qh, 1, nthreads=_threads())
         dt = time.perf_counter() - t0
         return {"value": round(n / dt / 1e6, 3), "unit": "Mpoints/s", "cores": _threads(), "kind": "port",
                 "sample": "the whole C1 workload: oracle voxel filter (1 thread) + kd-tree build + 1-NN (OpenMP)"}
@@ -151,7 +165,7 @@ def cfg_c2(ctx, args, rank, timer):
         tree = ora.KdTree(th)
         tb = time.perf_counter() - t0
         t0 = time.perf_counter()
-        tree.knn(qs, 8)
+        tree.knn(qs, 8, nthreads=_threads())
         dt = time.perf_counter() - t0
         return {"value": round(len(qs) / dt / 1e6, 3), "unit": "Mqueries/s", "cores": _threads(), "kind": "port",
                 "sample": f"oracle kd-tree (FLANN contract) over the same 1M targets: {len(qs)} queries k=8 in "
@@ -201,7 +215,7 @@ def cfg_c3(ctx, args, rank, timer):
         tv = time.perf_counter() - t0
         vx = np.stack([vox["x"], vox["y"], vox["z"]], 1)
         t0 = time.perf_counter()
-        ora.normals_knn(vx, 32)
+        ora.normals_knn(vx, 32, nthreads=_threads())
         tn = time.perf_counter() - t0
         return {"value": round(s / (tv + tn) / 1e6, 3), "unit": "Mpoints/s", "cores": _threads(), "kind": "port",
                 "sample": f"the first {s} points: oracle voxel filter {tv:.2f} s (1 thread) + kd-tree normals k=32 "
@@ -245,22 +259,21 @@ def cfg_c5(ctx, args, rank, timer):
 
     def cpu():
         ora = _oracle()
-        s = 20_000
-        xh = xyz.cpu().numpy().astype(np.float64)
+        ns, s = 2_000_000, 500_000
+        side_s = math.sqrt(ns / 1.5e6) * 40.0  # a tile of the same scene at the same density
+        xh = synth.street_scene(ns, 5001, extent=(side_s, side_s), device="cpu").numpy().astype(np.float64)
         t0 = time.perf_counter()
         tree = ora.KdTree(xh)
         tb = time.perf_counter() - t0
-        qs = np.random.default_rng(5).choice(n, s, replace=False)
+        qs = np.sort(np.random.default_rng(5).choice(ns, s, replace=False)).astype(np.int32)
         t0 = time.perf_counter()
-        for i in qs:
-            nb, _ = tree.radius(xh[i], 0.2)
-            P = xh[nb]
-            C = np.cov((P - P.mean(0)).T, bias=True)
-            np.linalg.eigh(C)
+        cnt, _ = tree.radius_normals(qs, 0.2, nthreads=_threads())
         dt = time.perf_counter() - t0
-        return {"value": round(s / dt / 1e6, 4), "unit": "Mpoints/s", "cores": 1, "kind": "port",
-                "sample": f"{s} random points of the same {n}-pt cloud: oracle kd-tree radiusSearch r=0.2 + fp64 PCA "
-                          f"per point (one thread, per-query calls) in {dt:.2f} s; kd-tree build {tb:.1f} s not in value"}
+        return {"value": round(s / dt / 1e6, 4), "unit": "Mpoints/s", "cores": _threads(), "kind": "port",
+                "sample": f"{s} random points of a {ns}-pt tile of the same scene at the same density "
+                          f"({side_s:.0f} x {side_s:.0f} m): oracle kd-tree radiusSearch r=0.2 (sorted rows) + fp64 F1 "
+                          f"per point, OpenMP over points (ora_radius_normals_batch), nbar {cnt.mean():.1f}, in "
+                          f"{dt:.2f} s; kd-tree build {tb:.1f} s not in value"}
     return step, info, cpu
 
 
@@ -312,7 +325,7 @@ def main(args):
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu()
+        line["cpu_baseline"] = _cpu_meta(cpu())
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -317,7 +317,15 @@ int pcp_icp_last_searched(const pcp_icp* icp, int64_t* n);
  * joint centroid (sequential fold over src ++ temp; non-finite points skipped unless both
  * clouds are dense, as cloud_all.is_dense = src.is_dense && temp.is_dense), float cast,
  * ICP(query = temp -> target = src), un-centring t' = t - R c + c.  mat_rot row-major.
- * Returns PCP_OK and *err (< 0 on failure). */
+ * Returns PCP_OK and *err (< 0 on failure).
+ * CONTRACT DIFFERENCE (trimesh2 is absent): the reference calls
+ * trimesh::ICP(..., maxdist = 0, ...) (point_cloud_helper.cpp:127), letting trimesh2 pick its
+ * distance threshold from the overlap, and returns trimesh2's error.  Here rmax is explicit and
+ * must be > 0 (rmax <= 0 -> PCP_ERR_UNSUPPORTED), the ICP is the build's deterministic
+ * point-to-point contract, and *err is the RMS distance (m) of the accepted pairs (d <= rmax)
+ * of the last iteration.  The reference's callers' thresholds on err (main.cpp:127-128:
+ * 0.13 / 0.22, used at main_blend.cpp:79-103) were tuned on trimesh2's value and are NOT
+ * calibrated for this one. */
 int pcp_get_rot_icp(pcp_ctx* ctx, const void* src_aos48_dev, int64_t ns, int src_is_dense,
                     const void* temp_aos48_dev, int64_t nt, int temp_is_dense,
                     double mat_rot_host[16], float rmax, int iters, int do_scale,
@@ -378,10 +386,17 @@ int pcp_grid_match(pcp_ctx* ctx, const pcp_grid* grid, const void* src_dev, int6
  * sizes.  width/height <= 0: n x 1.  PCP_ERR_EMPTY for n == 0 (the reference throws).
  * pcp_pcd_read: io::loadPCDFile (pcd_helper.h:1374-1378 -> PCDReader, pcd_helper.cpp:71-1395)
  * of DATA ascii / binary / binary_compressed; out_host NULL = size query (*n_out = POINTS).
+ * Header fields must be PCL datatypes (F 4/8, U/I 1/2/4) or PCP_ERR_ARG; a negative POINTS,
+ * WIDTH or HEIGHT, or a DATA section shorter than the header promises, is PCP_ERR_ARG.
+ * pcp_pcd_read_ex also reports the header's WIDTH/HEIGHT and is_dense as PCDReader sets it
+ * (pcd_helper.cpp:863, 1124-1179: 0 when a binary / binary_compressed field value is
+ * non-finite; ascii files stay dense); any of the three may be NULL.
  * pcp_lzf_compress / pcp_lzf_decompress: lzfCompress / lzfDecompress (lzf.cpp:86-415);
  * return the output size, 0 on failure. */
 int pcp_pcd_write(const char* path, const void* pts_host, int64_t n, int64_t width, int64_t height, int compressed);
 int pcp_pcd_read(const char* path, void* out_host, int64_t cap, int64_t* n_out);
+int pcp_pcd_read_ex(const char* path, void* out_host, int64_t cap, int64_t* n_out, int64_t* width_out,
+                    int64_t* height_out, int* dense_out);
 size_t pcp_lzf_compress(const void* in_host, size_t in_len, void* out_host, size_t out_len);
 size_t pcp_lzf_decompress(const void* in_host, size_t in_len, void* out_host, size_t out_len);
 

@@ -80,6 +80,14 @@ public:
     PointT& operator[](size_t i) { return points[i]; }
     const PointT& operator[](size_t i) const { return points[i]; }
     Ptr makeShared() const { return Ptr(new PointCloud<PointT>(*this)); }
+    // point_cloud.h:130-147: append, width = size, height = 1, dense only if both were
+    PointCloud& operator+=(const PointCloud& rhs) {
+        points.insert(points.end(), rhs.points.begin(), rhs.points.end());
+        width = (uint32_t)points.size();
+        height = 1;
+        is_dense = is_dense && rhs.is_dense;
+        return *this;
+    }
 };
 
 typedef PointXYZRGBA CloudItem;  // cmm_types.h:11-14
@@ -608,13 +616,25 @@ public:
         remove_duplicate(tmp, voxel_grid_size);
         if ((int)tmp->size() >= min_num) *cloud_src = *tmp;
     }
-    // get_rot_icp (:75-166): returns err (< 0 on failure); do_affine is outside this build
+    // get_rot_icp (:75-166): returns err (< 0 on failure); do_affine is outside this build.
+    // CONTRACT DIFFERENCE -- read before porting a caller.  The reference's get_rot_icp has no
+    // iteration count or distance parameters: it calls trimesh::ICP(..., maxdist = 0, ...)
+    // (:127), so trimesh2 (absent from the tree) chooses its own threshold from the overlap and
+    // its own stopping rule, and returns ITS error measure.  This build runs its deterministic
+    // point-to-point ICP for `iters` iterations with the explicit correspondence distance
+    // `maxdist` (defaults below are this build's choice: 20 iterations, 0.25 m), and err is the
+    // RMS distance (m) of the pairs accepted (d <= maxdist) in the last iteration.  The
+    // reference's thresholds on err (main.cpp:127-128: 0.13 / 0.22, used at main_blend.cpp:79-103)
+    // were tuned on trimesh2's value and are NOT calibrated for this one.  maxdist <= 0 (the
+    // reference's "automatic") is rejected: err = -1.
+    static constexpr int kIcpIters = 20;
+    static constexpr float kIcpMaxDist = 0.25f;
     template <class M>
     static float get_rot_icp(CloudPtr cloud_src, CloudPtr cloud_temp, M& mat_rot, bool do_scale = false,
-                             bool do_affine = false, int iters = 20, float maxdist = 0.25f) {
+                             bool do_affine = false, int iters = kIcpIters, float maxdist = kIcpMaxDist) {
         for (int r = 0; r < 4; r++)
             for (int col = 0; col < 4; col++) mat_rot(r, col) = (r == col) ? 1.0 : 0.0;
-        if (do_affine || !cloud_src || !cloud_temp) return -1.0f;
+        if (do_affine || !cloud_src || !cloud_temp || !(maxdist > 0.f)) return -1.0f;
         pcp_ctx* c = detail::Device::get().ctx();
         std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
         detail::DevBuf s, t;
@@ -942,12 +962,18 @@ private:
 
 // ------------------------------------------------------------------ PCD I/O (pcd_helper.h)
 namespace io {
-// io::loadPCDFile (pcd_helper.h:1374-1378): ascii / binary / binary_compressed; 0 or -1
+// io::loadPCDFile (pcd_helper.h:1374-1378): ascii / binary / binary_compressed; 0 or -1.
+// width / height come from the header and is_dense is set as PCDReader sets it
+// (pcd_helper.cpp:863, 1124-1179: false when a binary field value is non-finite).
 inline int loadPCDFile(const std::string& file_name, Cloud& cloud) {
-    int64_t n = 0;
-    if (pcp_pcd_read(file_name.c_str(), nullptr, 0, &n) != PCP_OK) return -1;
+    int64_t n = 0, w = 0, h = 0;
+    int dense = 1;
+    if (pcp_pcd_read_ex(file_name.c_str(), nullptr, 0, &n, nullptr, nullptr, nullptr) != PCP_OK) return -1;
     cloud.points.resize((size_t)n);
-    if (pcp_pcd_read(file_name.c_str(), cloud.points.data(), n, &n) != PCP_OK) return -1;
+    if (pcp_pcd_read_ex(file_name.c_str(), cloud.points.data(), n, &n, &w, &h, &dense) != PCP_OK) return -1;
+    cloud.width = (uint32_t)w;
+    cloud.height = (uint32_t)h;
+    cloud.is_dense = dense != 0;
     return 0;
 }
 // io::savePCDFile(binary_mode = true) / savePCDFileBinary -> writeBinary (:489-610); the

@@ -239,6 +239,48 @@ int ora_radius(const ora_kdtree* t, const double q[3], double radius, unsigned m
     return cnt;
 }
 
+/* C5 CPU baseline: per query point, radiusSearch(r) (kd_tree.h:863-903) + F1 over the
+ * neighbourhood in sorted order (calculate_feature.cpp:119-206) -- the reference's per-point
+ * loop shape (static.cpp / calculate_feature.cpp:222 OpenMP over points).  counts[i] = rows
+ * found; planes[i] = F1 of the row (curvature 1, zero normal for <= 3 neighbours). */
+void ora_radius_normals_batch(const ora_kdtree* t, const double* xyz, size_t stride, const int* qidx, int nq,
+                              double radius, int* counts, ora_plane* planes, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel
+    {
+        int cap = 256;
+        int* idx = (int*)malloc((size_t)cap * sizeof(int));
+        double* d2 = (double*)malloc((size_t)cap * sizeof(double));
+        double* nb = (double*)malloc((size_t)cap * 3 * sizeof(double));
+#pragma omp for schedule(dynamic, 64)
+        for (int i = 0; i < nq; i++) {
+            const double* q = xyz + (size_t)qidx[i] * stride;
+            int got = ora_radius(t, q, radius, 0, idx, d2, cap);
+            if (got > cap) {
+                cap = got;
+                idx = (int*)realloc(idx, (size_t)cap * sizeof(int));
+                d2 = (double*)realloc(d2, (size_t)cap * sizeof(double));
+                nb = (double*)realloc(nb, (size_t)cap * 3 * sizeof(double));
+                got = ora_radius(t, q, radius, 0, idx, d2, cap);
+            }
+            counts[i] = got;
+            if (got <= 3) {
+                planes[i].normal_x = planes[i].normal_y = planes[i].normal_z = 0.f;
+                planes[i].distance = 0.f; planes[i].min_value = 0.f; planes[i].curvature = 1.f;
+                continue;
+            }
+            for (int r = 0; r < got; r++) {
+                const double* p = xyz + (size_t)idx[r] * stride;
+                nb[3 * r] = p[0]; nb[3 * r + 1] = p[1]; nb[3 * r + 2] = p[2];
+            }
+            ora_plane_h_points(nb, got, &planes[i]);
+        }
+        free(idx); free(d2); free(nb);
+    }
+}
+
 /* =============================================================== V: minmax/centroid === */
 void ora_getminmax3d(const ora_point48* in, int n, int is_dense, double mn[4], double mx[4]) {
     for (int a = 0; a < 4; a++) { mn[a] = DBL_MAX; mx[a] = DBL_MIN; } /* point_cloud_helper.h:64-65 */
@@ -1178,8 +1220,10 @@ static int g_cmp(const void* a, const void* b) {
 }
 int ora_grid_points(const ora_grid* g, ora_point48* out) {
     ora_gcell* cs = (ora_gcell*)malloc(sizeof(ora_gcell) * (g->ncell ? g->ncell : 1));
-    memcpy(cs, g->cells, sizeof(ora_gcell) * g->ncell);
-    qsort(cs, g->ncell, sizeof(ora_gcell), g_cmp);
+    if (g->ncell > 0) {  /* memcpy/qsort of zero cells from a NULL table is UB (UBSan) */
+        memcpy(cs, g->cells, sizeof(ora_gcell) * g->ncell);
+        qsort(cs, g->ncell, sizeof(ora_gcell), g_cmp);
+    }
     int m = 0;
     for (int c = 0; c < g->ncell; c++)
         for (int q = 0; q < cs[c].n; q++) out[m++] = cs[c].p[q];

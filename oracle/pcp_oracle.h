@@ -116,6 +116,11 @@ void ora_plane_h_points(const double* xyz, int h, ora_plane* out);
 void ora_normals_knn(const ora_kdtree* t, const double* xyz, size_t stride_doubles, int n,
                      int k, ora_plane* out, int nthreads);
 
+/* C5 CPU baseline: radiusSearch(r) of the points qidx[0..nq) of the tree's cloud + F1 over
+ * each sorted row (kd_tree.h:863-903, calculate_feature.cpp:119-206), OpenMP over queries. */
+void ora_radius_normals_batch(const ora_kdtree* t, const double* xyz, size_t stride_doubles, const int* qidx,
+                              int nq, double radius, int* counts, ora_plane* planes, int nthreads);
+
 /* LAS_POINT_PROPERTY (data_struct.h:161-172), 48 bytes. */
 typedef struct ora_point_property {
     float normal_x, normal_y, normal_z;

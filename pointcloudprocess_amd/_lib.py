@@ -62,6 +62,7 @@ SIGNATURES = [
     ("pcp_pose_interpolate", _i32, [_vp, _i64, _i64, _i64]),
     ("pcp_pcd_write", _i32, [C.c_char_p, _vp, _i64, _i64, _i64, _i32]),
     ("pcp_pcd_read", _i32, [C.c_char_p, _vp, _i64, _P(_i64)]),
+    ("pcp_pcd_read_ex", _i32, [C.c_char_p, _vp, _i64, _P(_i64), _P(_i64), _P(_i64), _P(_i32)]),
     ("pcp_lzf_compress", _sz, [_vp, _sz, _vp, _sz]),
     ("pcp_lzf_decompress", _sz, [_vp, _sz, _vp, _sz]),
     ("pcp_grid_create", _i32, [_vp, _P(_vp)]),

@@ -158,13 +158,17 @@ def do_mul_frame_icp(ctx, line, stamp_file, start_index, end_index, grid, valid_
     of dicts {stamp, matrix (4x4), icperr} (g_status._clouds_stamp_rot_line; matrices are
     updated in place, at the first entry of each stamp as get_cloud_rot_with_stamp does);
     stamp_file: stamp -> PCD path; grid: the CloudGrid map cache.  load_cloud(path) -> (n, 48)
-    uint8 device records (default: pcd.load_pcd).  Returns (dis, rot) of the joint registration."""
+    uint8 device records, or (records, is_dense) (default: pcd.load_pcd_ex, which reports
+    is_dense as the reference's reader does).  The joint frame's is_dense is the AND of the
+    loaded clouds' (PointCloud::operator+=, point_cloud.h:130-147).  Returns (dis, rot) of
+    the joint registration."""
     import torch
     from . import pcd as _pcd
     from . import segments as _seg
     if load_cloud is None:
         def load_cloud(path):
-            return torch.from_numpy(_pcd.load_pcd(path).view(np.uint8).reshape(-1, 48).copy()).to(ctx.device)
+            arr, dense_f, _, _ = _pcd.load_pcd_ex(path)
+            return torch.from_numpy(arr.view(np.uint8).reshape(-1, 48).copy()).to(ctx.device), dense_f
     frames = []  # (stamp, path) in frame_files order
     for i in range(start_index + 1, end_index):  # the frames between the two ends (:662-679)
         st = line[i]["stamp"]
@@ -172,11 +176,12 @@ def do_mul_frame_icp(ctx, line, stamp_file, start_index, end_index, grid, valid_
             frames.append((st, stamp_file[st]))
     _frame_walk(line, start_index, -1, valid_count, min_icp_threshold, stamp_file, frames)
     _frame_walk(line, end_index, +1, valid_count, min_icp_threshold, stamp_file, frames)
-    clouds = [load_cloud(p) for _, p in frames]  # (:754-765)
+    loaded = [load_cloud(p) for _, p in frames]  # (:754-765)
+    clouds = [c[0] if isinstance(c, tuple) else c for c in loaded]
+    dense = all(c[1] if isinstance(c, tuple) else True for c in loaded)  # operator+= (point_cloud.h:143-146)
     frame = torch.cat(clouds) if clouds else torch.empty((0, 48), dtype=torch.uint8, device=ctx.device)
     frame = frame.clone()
     frame[:, 32:36] = torch.tensor([0, 0, 255, 0], dtype=torch.uint8, device=ctx.device)  # change_cloud_rgb 255,0,0
-    dense = bool(torch.isfinite(frame[:, :24].contiguous().view(torch.float64)).all()) if frame.shape[0] else True
     frame = ops.remove_duplicate(ctx, frame, 0.04, is_dense=dense)
     if is_shaft_filter:
         frame = _seg.shaft_filter(ctx, frame)

@@ -420,6 +420,12 @@ int pcp_get_rot_icp(pcp_ctx* ctx, const void* src, int64_t ns, int src_dense, co
         return set_error(ctx, PCP_ERR_ARG, "pcp_get_rot_icp: bad arguments");
     if (err) *err = -1.0f;
     for (int i = 0; i < 16; i++) M[i] = (i % 5 == 0) ? 1.0 : 0.0;
+    // the reference passes maxdist = 0 (point_cloud_helper.cpp:127), which makes trimesh2 derive
+    // its own threshold from the clouds' overlap (ICP.h:17-28; library absent, not restated):
+    // this build needs an explicit correspondence distance and says so instead of guessing one
+    if (!(rmax > 0.f))
+        return set_error(ctx, PCP_ERR_UNSUPPORTED,
+                         "pcp_get_rot_icp: rmax must be > 0 (trimesh2's automatic maxdist = 0 is not provided)");
     if (ns == 0 || nt == 0) return PCP_OK;  // ICP fails: err < 0 (ICP.h:26-28)
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     // joint centroid over cloud_all = src ++ temp (point_cloud_helper.cpp:78-83): one sequential

@@ -297,6 +297,11 @@ struct Tmp {  // per-call device temporaries, returned to the context's cache on
         v.push_back((void*)*p);
         return PCP_OK;
     }
+    // hand an allocation over to the caller (on success): the guard no longer frees it
+    void release(const void* p) {
+        for (void*& q : v)
+            if (q == p) q = nullptr;
+    }
 };
 
 }  // namespace
@@ -380,7 +385,7 @@ int pcp_grid_add_cloud(pcp_ctx* ctx, pcp_grid* g, const void* cloud_dev, int64_t
     int64_t* cst;
     uint64_t* ckey;
     PCP_TRY(tmp.get(&cst, (size_t)ncell + 1));
-    PCP_TRY(dmalloc(ctx, &ckey, ncell));
+    PCP_TRY(tmp.get(&ckey, ncell));  // every result is guarded until the swap below
     hipLaunchKernelGGL(k_grid_cells, dim3(grid_for(m, 256)), dim3(256), 0, st, k1, hs, head, m, cst, ckey);
     const int64_t mm = m;
     PCP_HIP(ctx, hipMemcpyAsync(cst + ncell, &mm, sizeof(int64_t), hipMemcpyHostToDevice, st));
@@ -396,13 +401,16 @@ int pcp_grid_add_cloud(pcp_ctx* ctx, pcp_grid* g, const void* cloud_dev, int64_t
     PCP_TRY(scan_u32_inplace(ctx, head, m, &nkeep));
     uint8_t* pts;
     int64_t* cstart;
-    PCP_TRY(dmalloc(ctx, &pts, 48 * (size_t)nkeep));
-    PCP_TRY(dmalloc(ctx, &cstart, (size_t)ncell + 1));
+    PCP_TRY(tmp.get(&pts, 48 * (size_t)nkeep));
+    PCP_TRY(tmp.get(&cstart, (size_t)ncell + 1));
     hipLaunchKernelGGL(k_grid_compact, dim3(grid_for(m, 256)), dim3(256), 0, st, rec, keep, head, m, pts);
     hipLaunchKernelGGL(k_grid_restart, dim3(grid_for(ncell + 1, 256)), dim3(256), 0, st, cst, head, (int64_t)ncell, m,
                        nkeep, cstart);
     PCP_LAUNCH_CHECK(ctx);
     PCP_HIP(ctx, hipStreamSynchronize(st));
+    tmp.release(pts);
+    tmp.release(ckey);
+    tmp.release(cstart);
     dfree(ctx, g->pts);
     dfree(ctx, g->keys);
     dfree(ctx, g->cstart);

@@ -262,9 +262,21 @@ int pcp_pcd_write(const char* path, const void* pts_host, int64_t n, int64_t wid
     return ok ? PCP_OK : PCP_ERR_ARG;
 }
 
-int pcp_pcd_read(const char* path, void* out_host, int64_t cap, int64_t* n_out) {
+// is_dense as the reference's reader sets it (pcd_helper.cpp:863, 1124-1179): true unless a
+// binary / binary_compressed field value of some point is non-finite (ascii stays dense)
+static bool field_finite(const uint8_t* p, const Field& f) {
+    if (f.type != 'F') return true;  // integers are always finite
+    if (f.size == 8) { double v; std::memcpy(&v, p, 8); return std::isfinite(v); }
+    float v; std::memcpy(&v, p, 4); return std::isfinite(v);
+}
+
+int pcp_pcd_read_ex(const char* path, void* out_host, int64_t cap, int64_t* n_out, int64_t* width_out,
+                    int64_t* height_out, int* dense_out) {
     if (!path || !n_out) return PCP_ERR_ARG;
     *n_out = 0;
+    if (width_out) *width_out = 0;
+    if (height_out) *height_out = 0;
+    if (dense_out) *dense_out = 1;
     FILE* fp = std::fopen(path, "rb");
     if (!fp) return PCP_ERR_ARG;
     std::fseek(fp, 0, SEEK_END);
@@ -277,13 +289,14 @@ int pcp_pcd_read(const char* path, void* out_host, int64_t cap, int64_t* n_out) 
     // header: lines up to and including DATA
     std::vector<Field> fields;
     int64_t npts = -1, width = 0, height = 1;
+    bool have_points = false;
     std::string data;
     size_t pos = 0;
     while (pos < file.size()) {
         size_t e = pos;
         while (e < file.size() && file[e] != '\n') e++;
         const std::string line((const char*)&file[pos], e - pos);
-        pos = e + 1;
+        pos = e < file.size() ? e + 1 : file.size();  // a last line without '\n' ends at the file's end
         const std::vector<std::string> t = split(line);
         if (t.empty() || t[0][0] == '#') continue;
         if (t[0] == "FIELDS" || t[0] == "COLUMNS") {
@@ -301,21 +314,40 @@ int pcp_pcd_read(const char* path, void* out_host, int64_t cap, int64_t* n_out) 
             height = std::atoll(t[1].c_str());
         } else if (t[0] == "POINTS" && t.size() > 1) {
             npts = std::atoll(t[1].c_str());
+            have_points = true;
         } else if (t[0] == "DATA" && t.size() > 1) {
             data = t[1];
             break;
         }
     }
     if (data.empty() || fields.empty()) return PCP_ERR_ARG;
-    if (npts < 0) npts = width * height;
-    *n_out = npts;
-    if (!out_host) return PCP_OK;  // size query
-    if (npts > cap) return PCP_ERR_CAPACITY;
-    std::vector<Layout> lay(fields.size());
+    if (width < 0 || height < 0 || (have_points && npts < 0)) return PCP_ERR_ARG;
+    if (!have_points) {
+        if (width > 0 && height > ((int64_t)1 << 62) / width) return PCP_ERR_ARG;
+        npts = width * height;
+    }
+    // the PCL datatypes the reference's reader accepts (sensor_msgs::PointField): F 4/8, U/I 1/2/4
     size_t psize = 0;
     for (size_t f = 0; f < fields.size(); f++) {
-        if (fields[f].size <= 0) return PCP_ERR_ARG;
+        const char ty = fields[f].type;
+        const int sz = fields[f].size;
+        const bool ok = (ty == 'F' && (sz == 4 || sz == 8)) || ((ty == 'U' || ty == 'I') && (sz == 1 || sz == 2 || sz == 4));
+        if (!ok) return PCP_ERR_ARG;
         if (fields[f].count < 1) fields[f].count = 1;
+        if (fields[f].count > (1 << 20)) return PCP_ERR_ARG;
+        psize += (size_t)sz * (size_t)fields[f].count;
+    }
+    *n_out = npts;
+    if (width_out) *width_out = width;
+    if (height_out) *height_out = height;
+    if (!out_host) return PCP_OK;  // size query
+    if (npts > cap) return PCP_ERR_CAPACITY;
+    // bytes of point data the header promises, overflow-checked
+    if (npts > 0 && psize > (SIZE_MAX / 2) / (size_t)npts) return PCP_ERR_ARG;
+    const size_t need = psize * (size_t)npts;
+    const size_t remain = file.size() - pos;  // pos <= file.size() by construction
+    std::vector<Layout> lay(fields.size());
+    for (size_t f = 0; f < fields.size(); f++) {
         const std::string& nm = fields[f].name;
         if (fields[f].count == 1) {
             if (nm == "x") lay[f].dst = 0;
@@ -324,32 +356,37 @@ int pcp_pcd_read(const char* path, void* out_host, int64_t cap, int64_t* n_out) 
             else if (nm == "rgba" || nm == "rgb") lay[f].dst = 3;
             else if (nm == "stamp_id") lay[f].dst = 4;
         }
-        psize += (size_t)fields[f].size * fields[f].count;
     }
     uint8_t* out = (uint8_t*)out_host;
     for (int64_t i = 0; i < npts; i++) default_record(out + 48 * i);
+    bool dense = true;
     if (data == "binary") {
-        if (file.size() - pos < psize * (size_t)npts) return PCP_ERR_ARG;
+        if (remain < need) return PCP_ERR_ARG;
         for (int64_t i = 0; i < npts; i++) {
             const uint8_t* row = &file[pos + psize * (size_t)i];
             size_t o = 0;
             for (size_t f = 0; f < fields.size(); f++) {
                 put(out + 48 * i, lay[f], row + o, fields[f]);
+                for (int c = 0; c < fields[f].count; c++) dense = dense && field_finite(row + o + (size_t)c * fields[f].size, fields[f]);
                 o += (size_t)fields[f].size * fields[f].count;
             }
         }
     } else if (data == "binary_compressed") {
-        if (file.size() - pos < 8) return PCP_ERR_ARG;
+        if (remain < 8) return PCP_ERR_ARG;
         uint32_t csz, usz;
         std::memcpy(&csz, &file[pos], 4);
         std::memcpy(&usz, &file[pos + 4], 4);
-        if (file.size() - pos - 8 < csz || usz < psize * (size_t)npts) return PCP_ERR_ARG;
+        if (remain - 8 < csz || usz < need) return PCP_ERR_ARG;
         std::vector<uint8_t> planes(usz);
         if (lzf_decompress(&file[pos + 8], csz, planes.data(), usz) != usz) return PCP_ERR_ARG;
         size_t p0 = 0;
         for (size_t f = 0; f < fields.size(); f++) {
             const size_t fs = (size_t)fields[f].size * fields[f].count;
-            for (int64_t i = 0; i < npts; i++) put(out + 48 * i, lay[f], &planes[p0 + fs * (size_t)i], fields[f]);
+            for (int64_t i = 0; i < npts; i++) {
+                const uint8_t* src = &planes[p0 + fs * (size_t)i];
+                put(out + 48 * i, lay[f], src, fields[f]);
+                for (int c = 0; c < fields[f].count; c++) dense = dense && field_finite(src + (size_t)c * fields[f].size, fields[f]);
+            }
             p0 += fs * (size_t)npts;
         }
     } else if (data == "ascii") {
@@ -385,7 +422,12 @@ int pcp_pcd_read(const char* path, void* out_host, int64_t cap, int64_t* n_out) 
     } else {
         return PCP_ERR_UNSUPPORTED;
     }
+    if (dense_out) *dense_out = dense ? 1 : 0;
     return PCP_OK;
+}
+
+int pcp_pcd_read(const char* path, void* out_host, int64_t cap, int64_t* n_out) {
+    return pcp_pcd_read_ex(path, out_host, cap, n_out, nullptr, nullptr, nullptr);
 }
 
 }  // extern "C"

@@ -3,6 +3,9 @@
   load_pcd(path, pinned=False)          io::loadPCDFile (pcd_helper.h:1374): ascii / binary /
                                         binary_compressed -> (n,) POINT48 numpy array (or a pinned
                                         (n, 48) uint8 tensor ready for one host-to-device copy)
+  load_pcd_ex(path, pinned=False)       the same + the cloud's is_dense, width, height as the
+                                        reference's PCDReader sets them (pcd_helper.cpp:863,
+                                        1124-1179)
   save_pcd(path, cloud, compressed=False)
                                         io::savePCDFile / savePCDFileBinary (writeBinary) or
                                         PCDWriter::writeBinaryCompressed (LZF)
@@ -21,18 +24,26 @@ def _path(p):
     return os.fsencode(os.fspath(p))
 
 
-def load_pcd(path, pinned=False):
+def load_pcd_ex(path, pinned=False):
+    """(cloud, is_dense, width, height): is_dense is False when a binary / binary_compressed
+    field value is non-finite (PCDReader, pcd_helper.cpp:1124-1179); ascii files stay dense."""
     lib = _lib.load()
-    n = C.c_int64()
-    _lib.check(lib.pcp_pcd_read(_path(path), None, 0, C.byref(n)))
+    n, w, h, dense = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int()
+    _lib.check(lib.pcp_pcd_read_ex(_path(path), None, 0, C.byref(n), None, None, None))
     if pinned:
         import torch
         buf = torch.empty((max(n.value, 1), 48), dtype=torch.uint8).pin_memory()
-        _lib.check(lib.pcp_pcd_read(_path(path), C.c_void_p(buf.data_ptr()), n.value, C.byref(n)))
-        return buf[:n.value]
+        _lib.check(lib.pcp_pcd_read_ex(_path(path), C.c_void_p(buf.data_ptr()), n.value, C.byref(n), C.byref(w),
+                                       C.byref(h), C.byref(dense)))
+        return buf[:n.value], bool(dense.value), w.value, h.value
     out = np.zeros(max(n.value, 1), dtype=POINT48)
-    _lib.check(lib.pcp_pcd_read(_path(path), out.ctypes.data, n.value, C.byref(n)))
-    return out[:n.value]
+    _lib.check(lib.pcp_pcd_read_ex(_path(path), out.ctypes.data, n.value, C.byref(n), C.byref(w), C.byref(h),
+                                   C.byref(dense)))
+    return out[:n.value], bool(dense.value), w.value, h.value
+
+
+def load_pcd(path, pinned=False):
+    return load_pcd_ex(path, pinned)[0]
 
 
 def save_pcd(path, cloud, compressed=False, width=0, height=0):

@@ -28,13 +28,28 @@ def _ptr(a, ctype):
     return a.ctypes.data_as(C.POINTER(ctype))
 
 
-def load():
+def use_native():
+    """bench.py cpu_baseline only: build the oracle on THIS host with -O3 -march=native
+    (`make -C oracle native`, oracle/_build/native-<march>/) and make every later oracle call
+    in this process use it.  Returns (path, march).  The parity build (-O2, portable) stays
+    what tests/ and smoke() load."""
     global _lib
-    if _lib is not None:
+    out = subprocess.check_output(["make", "-s", "-C", ORACLE_DIR, "native"], text=True).strip().splitlines()
+    path = os.path.join(ORACLE_DIR, out[-1])
+    _lib = None
+    load(path)
+    return path, os.path.basename(os.path.dirname(path)).replace("native-", "")
+
+
+def load(path=None):
+    global _lib
+    if _lib is not None and path is None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
-    lib = C.CDLL(LIB_PATH)
+    if path is None:
+        path = LIB_PATH
+        if not os.path.exists(LIB_PATH):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+    lib = C.CDLL(path)
     vp = C.c_void_p
     lib.ora_kdtree_build.restype = vp
     lib.ora_kdtree_build.argtypes = [vp, C.c_size_t, C.c_int, vp, C.c_int]
@@ -60,6 +75,7 @@ def load():
     lib.ora_remove_duplicate_c.argtypes = [vp, C.c_int, C.c_int, C.c_float, vp, vp]
     lib.ora_plane_h_points.argtypes = [vp, C.c_int, vp]
     lib.ora_normals_knn.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_int, vp, C.c_int]
+    lib.ora_radius_normals_batch.argtypes = [vp, vp, C.c_size_t, vp, C.c_int, C.c_double, vp, vp, C.c_int]
     lib.ora_eigen_sym3.argtypes = [vp, vp, vp]
     lib.ora_f32index_build.restype = vp
     lib.ora_f32index_build.argtypes = [vp, C.c_int]
@@ -121,13 +137,23 @@ class KdTree:
     def size(self):
         return self.lib.ora_kdtree_size(self.h)
 
-    def knn(self, q, k):
+    def knn(self, q, k, nthreads=0):
         q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, 3)
         idx = np.empty((len(q), k), np.int32)
         d2 = np.empty((len(q), k), np.float64)
         self.lib.ora_knn_batch(self.h, q.ctypes.data, 3, len(q), k, idx.ctypes.data,
-                               d2.ctypes.data, 0)
+                               d2.ctypes.data, int(nthreads))
         return idx, d2
+
+    def radius_normals(self, qidx, r, nthreads=0):
+        """C5 CPU leg: radiusSearch(r) of the tree's own points qidx + F1 per row (OpenMP).
+        The tree must be built over its (n, 3) xyz with stride 3."""
+        qidx = np.ascontiguousarray(qidx, dtype=np.int32)
+        cnt = np.empty(max(len(qidx), 1), np.int32)
+        planes = np.empty(max(len(qidx), 1), PLANE)
+        self.lib.ora_radius_normals_batch(self.h, self.xyz.ctypes.data, 3, qidx.ctypes.data, len(qidx), float(r),
+                                          cnt.ctypes.data, planes.ctypes.data, int(nthreads))
+        return cnt[:len(qidx)], planes[:len(qidx)]
 
     def radius(self, q, r, max_nn=0, cap=None):
         q = np.ascontiguousarray(q, dtype=np.float64).reshape(3)

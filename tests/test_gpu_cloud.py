@@ -264,3 +264,15 @@ def test_get_rot_icp_non_dense(ctx):
     assert np.isfinite(M).all() and err > 0 and eerr > 0
     assert abs(err - eerr) <= 1e-5
     assert np.abs(M - eM).max() <= 1e-5 * max(1.0, np.abs(off).max())
+
+
+@pytest.mark.parametrize("rmax", [0.0, -1.0])
+def test_get_rot_icp_rejects_automatic_maxdist(ctx, rmax):
+    """The reference's maxdist = 0 lets trimesh2 choose its threshold (point_cloud_helper.cpp:127,
+    ICP.h:17-28; library absent): this build rejects it loudly instead of substituting one."""
+    from pointcloudprocess_amd import _lib, ops
+    src = ora.make_cloud(np.random.default_rng(5).uniform(0, 5, (2000, 3)))
+    d = ops.cloud_to_device(src, ctx.device)
+    with pytest.raises(_lib.PcpError) as ei:
+        ops.get_rot_icp(ctx, d, d, rmax, iters=5)
+    assert ei.value.code == -5  # PCP_ERR_UNSUPPORTED

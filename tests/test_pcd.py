@@ -88,3 +88,57 @@ def test_pcd_read_other_layouts(tmp_path):
     p2.write_text(head.format(n=n, d="ascii") + "\n".join(lines) + "\n")
     a = pcd.load_pcd(p2)
     assert np.allclose(a["x"], xyz[:, 0], rtol=0, atol=1e-6) and np.array_equal(a["rgba"], rgb)
+
+
+HEAD = ("# .PCD v0.7\nVERSION 0.7\nFIELDS x y z\nSIZE {s}\nTYPE {t}\nCOUNT 1 1 1\nWIDTH {w}\nHEIGHT 1\n"
+        "VIEWPOINT 0 0 0 1 0 0 0\nPOINTS {n}\nDATA {d}")
+
+
+def _xyz_file(tmp_path, name, n, data, s="4 4 4", t="F F F", w=None, body=b"", newline=True):
+    p = tmp_path / name
+    h = HEAD.format(s=s, t=t, w=n if w is None else w, n=n, d=data) + ("\n" if newline else "")
+    p.write_bytes(h.encode() + body)
+    return p
+
+
+@pytest.mark.parametrize("data", ["binary", "binary_compressed"])
+def test_pcd_read_rejects_truncated_data(tmp_path, data):
+    """a DATA line with no data after it (with or without its newline) or a body
+    shorter than POINTS promises is rejected, never read past the file's end."""
+    for nl in (True, False):
+        with pytest.raises(Exception):
+            pcd.load_pcd(_xyz_file(tmp_path, f"t{nl}.pcd", 10, data, newline=nl))
+    short = np.zeros(9 * 3, dtype=np.float32).tobytes()
+    with pytest.raises(Exception):
+        pcd.load_pcd(_xyz_file(tmp_path, "s.pcd", 10, "binary", body=short))
+
+
+def test_pcd_read_rejects_bad_header(tmp_path):
+    body = np.zeros(30, dtype=np.float32).tobytes()
+    with pytest.raises(Exception):  # negative POINTS
+        pcd.load_pcd(_xyz_file(tmp_path, "neg.pcd", -5, "binary", body=body))
+    for s, t in (("2 2 2", "F F F"), ("8 8 8", "U U U"), ("3 3 3", "I I I"), ("4 4 4", "X X X")):
+        with pytest.raises(Exception):  # sizes / types PCL's PointField does not have
+            pcd.load_pcd(_xyz_file(tmp_path, "bad.pcd", 10, "binary", s=s, t=t, body=body * 2))
+    with pytest.raises(Exception):  # POINTS so large that psize * POINTS overflows
+        pcd.load_pcd(_xyz_file(tmp_path, "big.pcd", 2**62, "binary", body=body))
+
+
+def test_pcd_read_dense_flag_and_size(tmp_path):
+    """is_dense as PCDReader sets it (pcd_helper.cpp:863, 1124-1179): False once a binary field
+    value is non-finite; ascii stays dense; WIDTH / HEIGHT come from the header."""
+    xyz = np.arange(30, dtype=np.float32).reshape(10, 3)
+    _, dense, w, h = pcd.load_pcd_ex(_xyz_file(tmp_path, "d.pcd", 10, "binary", body=xyz.tobytes()))
+    assert dense and (w, h) == (10, 1)
+    bad = xyz.copy()
+    bad[4, 1] = np.nan
+    arr, dense, _, _ = pcd.load_pcd_ex(_xyz_file(tmp_path, "n.pcd", 10, "binary", body=bad.tobytes()))
+    assert not dense and np.isnan(arr["y"][4])
+    c = cloud(300, 5)
+    c["z"][7] = np.inf
+    p = tmp_path / "c.pcd"
+    pcd.save_pcd(p, c, compressed=True)
+    assert not pcd.load_pcd_ex(p)[1]
+    txt = "\n".join("1 2 nan" if i == 2 else "1 2 3" for i in range(4)) + "\n"
+    pa = _xyz_file(tmp_path, "a.pcd", 4, "ascii", body=txt.encode())
+    assert pcd.load_pcd_ex(pa)[1]  # the reference checks binary data only
