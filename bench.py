@@ -16,9 +16,11 @@ torch.distributed.run from a parent that never touches the GPU):
                   slab widened by a halo; a device guard certifies each iteration that the pose
                   keeps the owned queries inside the halo.  Collective per iteration:
                   all_reduce(SUM) of the 24 accumulators (RCCL over xGMI).
-  --mode sharded  the north_star layout: the target sharded by x-slab, queries replicated;
-                  per iteration ReduceScatter(MIN) of 8-byte (d2, index) keys per query, then
-                  all_reduce(SUM) of the 24 accumulators of each rank's query slice.
+  --mode sharded  the north_star layout: the target sharded by x-slab (a rank holds only its
+                  shard), queries replicated; per iteration ReduceScatter(MIN) of 8-byte (d2,
+                  index) keys per query, AllGather of the 1-byte owning shard of each winner,
+                  each rank accumulates the winners it owns from its own shard, then
+                  all_reduce(SUM) of the 24 accumulators.
   --mode weak     WEAK scaling: each rank registers its own 50M-vs-50M tile.
 At N > 1 the line also carries the two other modes under "alt_modes" (--no-alt skips them).
 
@@ -288,12 +290,13 @@ def main():
                          hi + args.halo - args.rmax)
                 info["halo_m"] = args.halo
                 del tgt, q
-            else:  # sharded: x-sorted target, equal-count contiguous shards; queries replicated
-                tgt = tgt[torch.argsort(tgt[:, 0])].contiguous()
-                lo_i, hi_i = D.shard_range(n, world, rank)
-                tile_t, tile_q = tgt[lo_i:hi_i].contiguous(), q.contiguous()
-                tgt_all = tgt
-                del q
+            else:  # sharded: x-sorted target, equal-count contiguous shards; queries replicated.
+                # The rank keeps ONLY its shard (the full cloud is synthetic set-up, freed here).
+                tgt = tgt[torch.argsort(tgt[:, 0])]
+                bounds = [D.shard_range(n, world, r)[0] for r in range(world)] + [n]
+                tile_t, tile_q = tgt[bounds[rank]:bounds[rank + 1]].contiguous(), q.contiguous()
+                info["target_points_per_rank"] = int(tile_t.shape[0])
+                del tgt, q
         torch.cuda.synchronize()
         result = {}
 
@@ -301,7 +304,7 @@ def main():
             st = {}
             eng = D.GpuEngine(ctx, tile_t, tile_q, cell_size=args.cell)
             if mode == "sharded":
-                err, T = D.run_target_sharded_dev(eng, np.eye(4), args.rmax, args.iters, lo_i, tile_q, tgt_all,
+                err, T = D.run_target_sharded_dev(eng, np.eye(4), args.rmax, args.iters, bounds,
                                                   exchange=exch if timed else None)
                 ok = True
             else:
@@ -361,8 +364,9 @@ def main():
         achieved = BYTES_PER_CORR * r["units_per_launch"] / (k_avg_ms * 1e-3) / 1e9  # algorithmic GB/s per launch
         par = {"slab": f"x-slabs x{world}: owned queries + targets of the slab +- {args.halo} m halo per rank; "
                        "RCCL all_reduce(SUM) of 24 fp64 accumulators per iteration",
-               "sharded": f"target sharded x{world} (x-slabs), queries replicated; RCCL ReduceScatter(MIN) of 8-B "
-                          "(d2, index) keys per query + all_reduce(SUM) of 24 fp64 per iteration",
+               "sharded": f"target sharded x{world} (x-slabs; a rank holds only its shard), queries replicated; RCCL "
+                          "ReduceScatter(MIN) of 8-B (d2, index) keys + AllGather of the 1-B owning shard per query + "
+                          "all_reduce(SUM) of 24 fp64 per iteration",
                "weak": f"co-partitioned tiles x{world} (each rank its own 50M-vs-50M); all_reduce(SUM) of 24 fp64"}
         line = {
             "metric": METRIC,

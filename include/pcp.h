@@ -264,18 +264,28 @@ int pcp_icp_accumulate_keys(pcp_ctx* ctx, pcp_icp* icp, const double T_host[16],
                             const uint64_t* keys_dev, int64_t lo, int64_t hi,
                             const float* shard_xyz_dev, size_t shard_stride_bytes,
                             double* acc_dev);
-/* Device-resident form of the target-sharded loop (pose T_dev: row-major 4x4 doubles in HBM):
- * pcp_icp_keys_dev = pcp_icp_keys at the device pose.  After a ReduceScatter(MIN) of the keys
- * (each rank keeps the keys of its slice of queries, original order), pcp_icp_accumulate_slice
- * writes the 24 accumulators of that slice: q_dev = the slice's queries, keys_dev = its
- * reduced keys, tgt_dev = the full target array indexed by the keys' global indices.  A SUM
- * over ranks then gives the accumulators of every query (point_cloud_helper.cpp:75-166 ICP
- * correspondence/transform step). */
+/* Device-resident form of the target-sharded loop (pose T_dev: row-major 4x4 doubles in HBM),
+ * in which no rank holds more of the target than its own shard:
+ *   1. pcp_icp_keys_dev = pcp_icp_keys at the device pose (this rank's local winners);
+ *   2. ReduceScatter(MIN) of the keys: each rank gets the global winners of its slice of the
+ *      queries (original order);
+ *   3. pcp_keys_owner: per key of the slice, the shard s owning its global target index
+ *      (bounds_dev[s] <= index < bounds_dev[s + 1], nshards + 1 int64 entries), 255 for none;
+ *      AllGather of these bytes gives every rank the owner of every query's winner;
+ *   4. pcp_icp_accumulate_owned: the 24 accumulators of the queries (q_dev: ALL the queries in
+ *      the original order) whose winner this rank owns (owner == rank), read from its own
+ *      shard (shard_xyz_dev, global indices [lo, hi)) through its local keys (keys_dev: the
+ *      rank's step-1 keys -- for an owned query they equal the global MIN);
+ *   5. all_reduce(SUM) of the 24 accumulators, pcp_icp_solve_dev.
+ * (point_cloud_helper.cpp:75-166 ICP correspondence/transform step). */
 int pcp_icp_keys_dev(pcp_ctx* ctx, pcp_icp* icp, const double* T_dev, float rmax,
                      int64_t target_offset, uint64_t* keys_dev);
-int pcp_icp_accumulate_slice(pcp_ctx* ctx, const double* T_dev, const float* q_dev,
-                             size_t q_stride_bytes, int64_t nq, const uint64_t* keys_dev,
-                             const float* tgt_dev, size_t tgt_stride_bytes, double* acc_dev);
+int pcp_keys_owner(pcp_ctx* ctx, const uint64_t* keys_dev, int64_t n, const int64_t* bounds_dev, int nshards,
+                   uint8_t* owner_dev);
+int pcp_icp_accumulate_owned(pcp_ctx* ctx, const double* T_dev, const float* q_dev, size_t q_stride_bytes,
+                             int64_t nq, const uint64_t* keys_dev, const uint8_t* owner_dev, int rank,
+                             int64_t lo, int64_t hi, const float* shard_xyz_dev, size_t shard_stride_bytes,
+                             double* acc_dev);
 /* Co-partitioned (slab) multi-GPU mode: latch *flag_dev = 1 when the owned queries' box
  * (host, {x0,x1,y0,y1,z0,z1}) under the device pose reaches outside x in [lo, hi], i.e.
  * the rank's target halo no longer certifies its correspondences (one thread, on the

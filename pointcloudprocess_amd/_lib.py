@@ -85,7 +85,8 @@ SIGNATURES = [
     ("pcp_icp_keys", _i32, [_vp, _vp, _P(_f64), _f32, _i64, _vp]),
     ("pcp_icp_accumulate_keys", _i32, [_vp, _vp, _P(_f64), _vp, _i64, _i64, _vp, _sz, _vp]),
     ("pcp_icp_keys_dev", _i32, [_vp, _vp, _vp, _f32, _i64, _vp]),
-    ("pcp_icp_accumulate_slice", _i32, [_vp, _vp, _vp, _sz, _i64, _vp, _vp, _sz, _vp]),
+    ("pcp_keys_owner", _i32, [_vp, _vp, _i64, _vp, _i32, _vp]),
+    ("pcp_icp_accumulate_owned", _i32, [_vp, _vp, _vp, _sz, _i64, _vp, _vp, _i32, _i64, _i64, _vp, _sz, _vp]),
     ("pcp_slab_guard", _i32, [_vp, _vp, _P(_f64), _f64, _f64, _vp]),
     ("pcp_icp_solve", _i32, [_P(_f64), _i32, _P(_f64)]),
     ("pcp_icp_run", _i32, [_vp, _vp, _P(_f64), _f32, _i32, _i32, _f64, _P(_f32)]),

@@ -315,6 +315,7 @@ int pcp_grid_create(pcp_ctx* ctx, pcp_grid** out) {
     if (!ctx || !out) return PCP_ERR_ARG;
     pcp_grid* g = new pcp_grid();
     g->ctx = ctx;
+    ctx_retain(ctx);
     *out = g;
     return PCP_OK;
 }
@@ -334,7 +335,9 @@ int pcp_grid_clear(pcp_ctx* ctx, pcp_grid* g) {
 int pcp_grid_destroy(pcp_grid* g) {
     if (!g) return PCP_ERR_ARG;
     pcp_grid_clear(g->ctx, g);
+    pcp_ctx* owner = g->ctx;
     delete g;
+    ctx_release(owner);
     return PCP_OK;
 }
 

@@ -37,6 +37,12 @@ struct pcp_ctx {
     std::unordered_map<void*, size_t> block_size;
     size_t cached_bytes = 0;
     size_t cache_cap = (size_t)16 << 30;
+    // lifetime: every index / ICP handle / CloudGrid made on the context holds a reference, so
+    // the objects may be destroyed before OR after pcp_ctx_destroy (a garbage-collected host
+    // language finalises them in any order): destroy marks the context closing, frees what no
+    // object uses, and the last object's destroy finishes the job
+    int live = 0;
+    bool closing = false;
 };
 
 namespace pcp {
@@ -64,6 +70,9 @@ int scratch(pcp_ctx* ctx, size_t bytes, void** out);
 int cache_alloc(pcp_ctx* ctx, size_t bytes, void** p);
 void dfree(pcp_ctx* ctx, void* p);
 void cache_release(pcp_ctx* ctx);
+// object lifetime references on a context (see pcp_ctx::live)
+void ctx_retain(pcp_ctx* ctx);
+void ctx_release(pcp_ctx* ctx);
 // a timing event from ctx's pool (or a new one); event_put returns it to the pool
 hipError_t event_get(pcp_ctx* ctx, hipEvent_t* ev);
 void event_put(pcp_ctx* ctx, hipEvent_t ev);

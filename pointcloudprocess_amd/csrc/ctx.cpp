@@ -83,6 +83,11 @@ void dfree(pcp_ctx* ctx, void* p) {
         (void)hipFree(p);
         return;
     }
+    if (ctx->closing) {  // nothing is cached on a closing context
+        ctx->block_size.erase(it);
+        (void)hipFree(p);
+        return;
+    }
     ctx->free_blocks.emplace(it->second, p);
     ctx->cached_bytes += it->second;
     // over the cap: drop the largest cached blocks (stream work using them is complete
@@ -119,6 +124,27 @@ void cache_release(pcp_ctx* ctx) {
     ctx->cached_bytes = 0;
 }
 
+// the rest of pcp_ctx_destroy, once no object uses the context any more
+static void ctx_finish(pcp_ctx* ctx) {
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->block_size) (void)hipFree(kv.first);  // (blocks an object leaked)
+    ctx->block_size.clear();
+    for (hipEvent_t ev : ctx->event_pool) (void)hipEventDestroy(ev);
+    ctx->event_pool.clear();
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void ctx_retain(pcp_ctx* ctx) {
+    if (ctx) ctx->live++;
+}
+
+void ctx_release(pcp_ctx* ctx) {
+    if (!ctx) return;
+    if (--ctx->live == 0 && ctx->closing) ctx_finish(ctx);
+}
+
 }  // namespace pcp
 
 extern "C" {
@@ -145,15 +171,16 @@ int pcp_ctx_create(int device, void* stream, pcp_ctx** out) {
 }
 
 int pcp_ctx_destroy(pcp_ctx* ctx) {
-    if (!ctx) return PCP_ERR_ARG;
+    if (!ctx || ctx->closing) return PCP_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->scan_status) (void)hipFree(ctx->scan_status);
+    ctx->scratch = nullptr;
+    ctx->scan_status = nullptr;
     pcp::cache_release(ctx);
-    for (hipEvent_t ev : ctx->event_pool) (void)hipEventDestroy(ev);
-    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
-    delete ctx;
+    ctx->closing = true;
+    if (ctx->live == 0) pcp::ctx_finish(ctx);  // else the last object's destroy finishes it
     return PCP_OK;
 }
 

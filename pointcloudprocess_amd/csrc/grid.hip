@@ -341,6 +341,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     pcp_index* ix = new pcp_index();
     ix->is_f64 = is_f64;
     ix->owner = ctx;
+    ctx_retain(ctx);
     ix->n_in = n_in;
     auto fail = [&](int rc) { pcp_index_destroy(ix); return rc; };
 
@@ -623,7 +624,9 @@ int pcp_index_destroy(pcp_index* ix) {
     pcp::dfree(ix->owner, ix->pos_of_j);
     pcp::dfree(ix->owner, ix->h16);
     pcp::dfree(ix->owner, ix->cell);
+    pcp_ctx* owner = ix->owner;
     delete ix;
+    pcp::ctx_release(owner);
     return PCP_OK;
 }
 

@@ -24,7 +24,8 @@
 #endif
 
 struct pcp_icp {
-    pcp_ctx* ctx = nullptr;
+    pcp_ctx* ctx = nullptr;       // the context of the last call (launches go to its stream)
+    pcp_ctx* owner = nullptr;     // the creating context: owns the buffers (a lifetime reference)
     const pcp_index* target = nullptr;
     int64_t nq = 0;               // finite queries
     int64_t nq_in = 0;            // queries passed to pcp_icp_create
@@ -1599,12 +1600,38 @@ __global__ void __launch_bounds__(256) k_sum_partials(const double* part, int nb
     }
 }
 
-// reduce-scatter form of the target-sharded mode: the accumulators of this rank's slice of the
-// queries (original order), whose global winners come from the MIN-reduced keys; the winner's
-// coordinates are read from the full (replicated) target array by global index.  The pose is
-// the device 4x4 (cast to fp32 exactly as k_pose_set does).
-__global__ void __launch_bounds__(256) k_acc_slice(const double* T, const float* q, size_t qs, int64_t n,
-                                                   const uint64_t* keys, const float* tgt, size_t ts, double* partials) {
+// Target-sharded mode, device-resident form: after a ReduceScatter(MIN) of
+// the per-query keys, each rank knows the global winners of its slice of the queries; the shard
+// that owns each winner (by its global target index) is all-gathered as one byte per query, and
+// every rank accumulates exactly the queries whose winner lies in its own shard, reading the
+// winner from its LOCAL shard -- no rank ever holds the full target.  A SUM over ranks gives the
+// accumulators of every query.
+// owner[i] = s with bounds[s] <= global index < bounds[s + 1], or 255 (no correspondence)
+__global__ void k_keys_owner(const uint64_t* keys, int64_t n, const int64_t* bounds, int nshards, uint8_t* owner) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        uint8_t o = 255;
+        if (k != kNoKey) {
+            const int64_t g = (int64_t)(k & 0xffffffffull);
+            int lo = 0, hi = nshards;  // the last s with bounds[s] <= g
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (bounds[mid] <= g) lo = mid;
+                else hi = mid;
+            }
+            o = (uint8_t)lo;
+        }
+        owner[i] = o;
+    }
+}
+
+// accumulators of the queries (original order, q) whose winner this rank owns: the winner is
+// the rank's local key's target (its global index less lo) -- for an owned query the local key
+// IS the global MIN.  The pose is the device 4x4 cast to fp32 as k_pose_set does; products of
+// fp32 values are exact in fp64, so only the summation order differs from the oracle.
+__global__ void __launch_bounds__(256) k_acc_owned(const double* T, const float* q, size_t qs, int64_t n,
+                                                   const uint64_t* keys, const uint8_t* owner, int rank, int64_t lo,
+                                                   int64_t hi, const float* shard, size_t ss, double* partials) {
     float R[9], t[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
@@ -1616,10 +1643,12 @@ __global__ void __launch_bounds__(256) k_acc_slice(const double* T, const float*
 #pragma unroll
     for (int k = 0; k < kAcc - 1; k++) acc[k] = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (owner[i] != (uint8_t)rank) continue;
         const uint64_t key = keys[i];
-        if (key == kNoKey) continue;
+        const int64_t g = (int64_t)(key & 0xffffffffull);
+        if (key == kNoKey || g < lo || g >= hi) continue;
         const float* qp = q + (size_t)i * qs;
-        const float* p = tgt + (size_t)(key & 0xffffffffull) * ts;
+        const float* p = shard + (size_t)(g - lo) * ss;
         const float x = __fmaf_rn(R[2], qp[2], __fmaf_rn(R[1], qp[1], __fmaf_rn(R[0], qp[0], t[0])));
         const float y = __fmaf_rn(R[5], qp[2], __fmaf_rn(R[4], qp[1], __fmaf_rn(R[3], qp[0], t[1])));
         const float z = __fmaf_rn(R[8], qp[2], __fmaf_rn(R[7], qp[1], __fmaf_rn(R[6], qp[0], t[2])));
@@ -2085,6 +2114,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     }
     pcp_icp* icp = new pcp_icp();
     icp->ctx = ctx;
+    icp->owner = ctx;
+    pcp::ctx_retain(ctx);
     icp->target = target;
     icp->nq = nfin;
     icp->nq_in = nq;
@@ -2165,35 +2196,37 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
 
 int pcp_icp_destroy(pcp_icp* icp) {
     if (!icp) return PCP_ERR_ARG;
-    (void)hipSetDevice(icp->ctx->device);
-    pcp::dfree(icp->ctx, icp->q);
-    pcp::dfree(icp->ctx, icp->partials);
-    pcp::dfree(icp->ctx, icp->acc);
-    pcp::dfree(icp->ctx, icp->cand);
-    pcp::dfree(icp->ctx, icp->hot);
-    pcp::dfree(icp->ctx, icp->dlb);
-    pcp::dfree(icp->ctx, icp->pose_hist);
-    pcp::dfree(icp->ctx, icp->sv);
-    pcp::dfree(icp->ctx, icp->sv_count);
-    pcp::dfree(icp->ctx, icp->sv_off);
-    pcp::dfree(icp->ctx, icp->svc);
+    (void)hipSetDevice(icp->owner->device);
+    pcp::dfree(icp->owner, icp->q);
+    pcp::dfree(icp->owner, icp->partials);
+    pcp::dfree(icp->owner, icp->acc);
+    pcp::dfree(icp->owner, icp->cand);
+    pcp::dfree(icp->owner, icp->hot);
+    pcp::dfree(icp->owner, icp->dlb);
+    pcp::dfree(icp->owner, icp->pose_hist);
+    pcp::dfree(icp->owner, icp->sv);
+    pcp::dfree(icp->owner, icp->sv_count);
+    pcp::dfree(icp->owner, icp->sv_off);
+    pcp::dfree(icp->owner, icp->svc);
 
-    pcp::dfree(icp->ctx, icp->dbgcnt);
-    pcp::dfree(icp->ctx, icp->dbgfz);
-    pcp::dfree(icp->ctx, icp->fb);
-    pcp::dfree(icp->ctx, icp->fb_count);
-    pcp::dfree(icp->ctx, icp->fb_off);
-    pcp::dfree(icp->ctx, icp->fbc);
-    pcp::dfree(icp->ctx, icp->pose_dev);
-    pcp::event_put(icp->ctx, icp->ev0);
-    pcp::event_put(icp->ctx, icp->ev1);
-    pcp::event_put(icp->ctx, icp->ev_mid);
-    pcp::event_put(icp->ctx, icp->ev_ver);
+    pcp::dfree(icp->owner, icp->dbgcnt);
+    pcp::dfree(icp->owner, icp->dbgfz);
+    pcp::dfree(icp->owner, icp->fb);
+    pcp::dfree(icp->owner, icp->fb_count);
+    pcp::dfree(icp->owner, icp->fb_off);
+    pcp::dfree(icp->owner, icp->fbc);
+    pcp::dfree(icp->owner, icp->pose_dev);
+    pcp::event_put(icp->owner, icp->ev0);
+    pcp::event_put(icp->owner, icp->ev1);
+    pcp::event_put(icp->owner, icp->ev_mid);
+    pcp::event_put(icp->owner, icp->ev_ver);
     for (auto& pr : icp->tev) {
-        pcp::event_put(icp->ctx, pr.first);
-        pcp::event_put(icp->ctx, pr.second);
+        pcp::event_put(icp->owner, pr.first);
+        pcp::event_put(icp->owner, pr.second);
     }
+    pcp_ctx* owner = icp->owner;
     delete icp;
+    pcp::ctx_release(owner);
     return PCP_OK;
 }
 
@@ -2287,19 +2320,34 @@ int pcp_icp_keys_dev(pcp_ctx* ctx, pcp_icp* icp, const double* T_dev, float rmax
     return PCP_OK;
 }
 
-int pcp_icp_accumulate_slice(pcp_ctx* ctx, const double* T_dev, const float* q_dev, size_t q_stride, int64_t nq,
-                             const uint64_t* keys_dev, const float* tgt_dev, size_t tgt_stride, double* acc_dev) {
-    if (!ctx || !T_dev || nq < 0 || (nq > 0 && (!q_dev || !keys_dev || !tgt_dev)) || !acc_dev) return PCP_ERR_ARG;
+int pcp_keys_owner(pcp_ctx* ctx, const uint64_t* keys_dev, int64_t n, const int64_t* bounds_dev, int nshards,
+                   uint8_t* owner_dev) {
+    if (!ctx || n < 0 || (n > 0 && (!keys_dev || !owner_dev)) || !bounds_dev || nshards < 1 || nshards > 255)
+        return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (n == 0) return PCP_OK;
+    hipLaunchKernelGGL(pcp::k_keys_owner, dim3(pcp::grid_for(n, 256, 8192)), dim3(256), 0, ctx->stream, keys_dev, n,
+                       bounds_dev, nshards, owner_dev);
+    PCP_LAUNCH_CHECK(ctx);
+    return PCP_OK;
+}
+
+int pcp_icp_accumulate_owned(pcp_ctx* ctx, const double* T_dev, const float* q_dev, size_t q_stride, int64_t nq,
+                             const uint64_t* keys_dev, const uint8_t* owner_dev, int rank, int64_t lo, int64_t hi,
+                             const float* shard_xyz_dev, size_t shard_stride, double* acc_dev) {
+    if (!ctx || !T_dev || nq < 0 || (nq > 0 && (!q_dev || !keys_dev || !owner_dev)) || !acc_dev || rank < 0 ||
+        rank > 254 || lo < 0 || hi < lo || (hi > lo && !shard_xyz_dev))
+        return PCP_ERR_ARG;
     if (q_stride == 0) q_stride = 3 * sizeof(float);
-    if (tgt_stride == 0) tgt_stride = 3 * sizeof(float);
-    if (q_stride % sizeof(float) || tgt_stride % sizeof(float))
+    if (shard_stride == 0) shard_stride = 3 * sizeof(float);
+    if (q_stride % sizeof(float) || shard_stride % sizeof(float))
         return pcp::set_error(ctx, PCP_ERR_ARG, "strides must be whole floats");
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     const int nb = (int)std::min<int64_t>(std::max<int64_t>(1, (nq + 255) / 256), 2048);
     double* part = nullptr;
     PCP_TRY(pcp::dmalloc(ctx, &part, (size_t)nb * pcp::kAcc));
-    hipLaunchKernelGGL(pcp::k_acc_slice, dim3(nb), dim3(256), 0, ctx->stream, T_dev, q_dev, q_stride / sizeof(float),
-                       nq, keys_dev, tgt_dev, tgt_stride / sizeof(float), part);
+    hipLaunchKernelGGL(pcp::k_acc_owned, dim3(nb), dim3(256), 0, ctx->stream, T_dev, q_dev, q_stride / sizeof(float),
+                       nq, keys_dev, owner_dev, rank, lo, hi, shard_xyz_dev, shard_stride / sizeof(float), part);
     hipLaunchKernelGGL(pcp::k_sum_partials, dim3(1), dim3(256), 0, ctx->stream, (const double*)part, nb, acc_dev);
     pcp::dfree(ctx, part);
     PCP_LAUNCH_CHECK(ctx);

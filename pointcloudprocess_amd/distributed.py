@@ -15,15 +15,18 @@ differs between the two partitionings:
 * target-sharded (the north_star layout): each rank indexes one shard of the target, the
   query set is replicated.  Per iteration: per-query int64 keys (fp32 d2 bits << 32 |
   global target index) -> MIN over ranks gives the global lexicographic (d2, index)
-  winner (all_reduce + per-shard accumulation, or -- device-resident -- ReduceScatter(MIN)
-  + accumulation of each rank's query slice) -> all_reduce(SUM) of the 24 accumulators.
-  8 bytes per query per iteration cross xGMI, so it scales worse than co-partitioning; it
-  needs no spatial partition of the queries.
+  winner (all_reduce + per-shard accumulation, or -- device-resident -- ReduceScatter(MIN),
+  an AllGather of the winners' owning shard (1 byte per query) and accumulation of the owned
+  winners from the rank's own shard) -> all_reduce(SUM) of the 24 accumulators.  No rank holds
+  more than its shard of the target; 8 + 1 bytes per query per iteration cross xGMI, so it
+  scales worse than co-partitioning; it needs no spatial partition of the queries.
 
 An *engine* supplies the local compute:
     step(T, rmax) -> acc            (24 float64, torch tensor on the engine's device)
     keys(T, rmax, offset) -> keys   (int64 torch tensor, one per query)
     accumulate_keys(T, keys, lo, hi) -> acc
+    keys_dev(T_dev, rmax, offset, out), key_owner(keys, bounds, out),
+    accumulate_owned(T_dev, keys, owner, rank, lo, hi) -> acc   (device-resident sharded loop)
 and, for the device-resident loop (run_copartitioned_dev: the pose and the solve stay on
 the device, the all-reduce is enqueued on the same stream, no host round trip per
 iteration):
@@ -47,7 +50,12 @@ def _world():
 
 def _allreduce(t, op):
     if _world() > 1:
-        dist.all_reduce(t, op=op)
+        if t.is_cuda and dist.get_backend() == "gloo":  # (one-GPU rehearsals: through host memory)
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op)
     return t
 
 
@@ -108,41 +116,65 @@ def _reduce_scatter_min(out, inp):
     world = _world()
     if world == 1:
         out.copy_(inp)
-    elif dist.get_backend() == "gloo":
-        dist.all_reduce(inp, op=dist.ReduceOp.MIN)
-        out.copy_(inp.view(world, -1)[dist.get_rank()])
+    elif dist.get_backend() == "gloo":  # (rehearsals on one GPU / CPU tests: through host memory)
+        h = inp.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MIN)
+        out.copy_(h.view(world, -1)[dist.get_rank()])
     else:
         dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.MIN)
     return out
 
 
-def run_target_sharded_dev(engine, T0, rmax, iters, lo, q_all, tgt_all, do_scale=False, exchange=None):
-    """The north_star layout with the pose on the device: every rank indexes its target shard
-    (global indices from lo) and holds the replicated queries.  Per iteration: keys at the
-    device pose -> ReduceScatter(MIN) (each rank keeps the reduced keys of its 1/G slice of
-    the queries, original order) -> accumulators of that slice (winners read from the full
-    target by global index) -> all_reduce(SUM) of 24 doubles -> device solve.  No host round
-    trip.  `exchange`: optional list that receives (start, end) CUDA event pairs around the
-    ReduceScatter of each iteration.  Returns (err, T), identical on every rank."""
+def _all_gather_bytes(out, inp):
+    """out <- the concatenation over ranks of inp (equal-size slices)."""
+    world = _world()
+    if world == 1:
+        out.copy_(inp)
+    elif dist.get_backend() == "gloo":  # (rehearsals on one GPU / CPU tests: through host memory)
+        parts = [torch.empty_like(inp, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, inp.cpu())
+        out.copy_(torch.cat(parts))
+    else:
+        dist.all_gather_into_tensor(out, inp)
+    return out
+
+
+def run_target_sharded_dev(engine, T0, rmax, iters, bounds, do_scale=False, exchange=None):
+    """The north_star layout with the pose on the device and no rank holding more of the target
+    than its own shard.  Every rank indexes its shard (global target indices [bounds[r],
+    bounds[r + 1])) and holds the replicated queries.  Per iteration (no host round trip):
+      keys at the device pose (this rank's local winners, 8 B per query)
+      -> ReduceScatter(MIN): the global winners of this rank's 1/G slice of the queries
+      -> the owning shard of each of those winners (1 B per query) -> AllGather
+      -> accumulators of the queries whose winner this rank owns, read from its own shard
+      -> all_reduce(SUM) of 24 doubles -> device solve.
+    `exchange`: optional list that receives (start, end) CUDA event pairs around the two
+    per-query collectives of each iteration.  Returns (err, T), identical on every rank."""
     world = _world()
     rank = dist.get_rank() if world > 1 else 0
-    nq = q_all.shape[0]
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    nq = engine.nq
+    dev = engine.device
     chunk = -(-nq // world)
-    keys = torch.full((chunk * world,), NO_KEY, dtype=torch.int64, device=q_all.device)
-    mine = torch.empty(chunk, dtype=torch.int64, device=q_all.device)
-    q0, q1 = min(nq, rank * chunk), min(nq, (rank + 1) * chunk)
+    keys = torch.full((chunk * world,), NO_KEY, dtype=torch.int64, device=dev)
+    mine = torch.empty(chunk, dtype=torch.int64, device=dev)
+    own_mine = torch.empty(chunk, dtype=torch.uint8, device=dev)
+    owner = torch.empty(chunk * world, dtype=torch.uint8, device=dev)
+    bnd = torch.tensor([int(b) for b in bounds], dtype=torch.int64, device=dev)
     T_dev, stats = engine.new_pose(T0)
     for _ in range(iters):
         engine.keys_dev(T_dev, rmax, lo, keys)
         ev = None
-        if exchange is not None and q_all.is_cuda:
+        if exchange is not None and keys.is_cuda:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        _reduce_scatter_min(mine, keys)
+        _reduce_scatter_min(mine, keys.clone() if keys.device.type == "cpu" else keys)  # (gloo reduces in place)
+        engine.key_owner(mine, bnd, own_mine)
+        _all_gather_bytes(owner, own_mine)
         if ev is not None:
             ev[1].record()
             exchange.append(ev)
-        acc = engine.accumulate_slice(T_dev, q_all[q0:q1], mine, tgt_all)
+        acc = engine.accumulate_owned(T_dev, keys, owner, rank, lo, hi)
         _allreduce(acc, dist.ReduceOp.SUM)
         engine.solve_dev(acc, T_dev, stats, do_scale)
     st = stats.cpu().numpy()
@@ -212,6 +244,8 @@ class GpuEngine:
         self.target = target_xyz.contiguous()
         self.index = ops.GridIndex(ctx, self.target, cell_size=cell_size)
         self.icp = ops.ICP(self.index, query_xyz.contiguous())
+        self.device = ctx.device
+        self.nq = query_xyz.shape[0]
 
     def step(self, T, rmax):
         return self.icp.step(T, rmax)
@@ -234,8 +268,12 @@ class GpuEngine:
     def keys_dev(self, T_dev, rmax, offset, out=None):
         return self.icp.keys_dev(T_dev, rmax, offset, out)
 
-    def accumulate_slice(self, T_dev, q, keys, tgt):
-        return ops.accumulate_slice(self.index.ctx, T_dev, q, keys, tgt, self.icp.acc)
+    def key_owner(self, keys, bounds, out):
+        return ops.keys_owner(self.index.ctx, keys, bounds, out)
+
+    def accumulate_owned(self, T_dev, keys, owner, rank, lo, hi):
+        return ops.accumulate_owned(self.index.ctx, T_dev, self.icp.q, keys, owner, rank, lo, hi, self.target,
+                                    self.icp.acc)
 
     def slab_guard(self, T_dev, box, lo, hi, flag):
         ops.slab_guard(self.index.ctx, T_dev, box, lo, hi, flag)

@@ -420,15 +420,28 @@ class ICP:
         self.close()
 
 
-def accumulate_slice(ctx, T_dev, q, keys, tgt, acc=None):
-    """Accumulators of the queries q (n x 3 fp32, original order) with their MIN-reduced keys
-    (global indices into tgt, the full target): the reduce-scatter form of the sharded loop."""
+def keys_owner(ctx, keys, bounds, out=None):
+    """Per key (int64, global target index in the low 32 bits), the shard owning its winner:
+    s with bounds[s] <= index < bounds[s + 1] (bounds: int64 device tensor, nshards + 1), 255
+    for no correspondence.  uint8 device tensor."""
+    n = keys.numel()
+    out = torch.empty(n, dtype=torch.uint8, device=ctx.device) if out is None else out
+    assert keys.dtype == torch.int64 and bounds.dtype == torch.int64 and out.numel() >= n
+    ctx.check(ctx.lib.pcp_keys_owner(ctx.h, _ptr(keys), n, _ptr(bounds), bounds.numel() - 1, _ptr(out)))
+    return out
+
+
+def accumulate_owned(ctx, T_dev, q, keys, owner, rank, lo, hi, shard_xyz, acc=None):
+    """Accumulators of the queries q (n x 3 fp32, ALL queries, original order) whose winner
+    this rank owns (owner == rank), read from its own shard (global indices [lo, hi)) through
+    its local keys: the device-resident target-sharded loop's accumulation."""
     acc = torch.zeros(24, dtype=torch.float64, device=ctx.device) if acc is None else acc
     n = q.shape[0]
-    assert keys.numel() >= n and keys.dtype == torch.int64
-    ctx.check(ctx.lib.pcp_icp_accumulate_slice(ctx.h, _ptr(T_dev), _ptr(q) if n else None,
-                                               q.stride(0) * q.element_size(), n, _ptr(keys), _ptr(tgt),
-                                               tgt.stride(0) * tgt.element_size(), _ptr(acc)))
+    assert keys.numel() >= n and keys.dtype == torch.int64 and owner.numel() >= n and owner.dtype == torch.uint8
+    ctx.check(ctx.lib.pcp_icp_accumulate_owned(ctx.h, _ptr(T_dev), _ptr(q) if n else None,
+                                               q.stride(0) * q.element_size(), n, _ptr(keys), _ptr(owner), int(rank),
+                                               int(lo), int(hi), _ptr(shard_xyz),
+                                               shard_xyz.stride(0) * shard_xyz.element_size(), _ptr(acc)))
     return acc
 
 

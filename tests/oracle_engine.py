@@ -19,6 +19,8 @@ class OracleEngine:
         self.t = np.ascontiguousarray(target_xyz, dtype=np.float32)
         self.q = np.ascontiguousarray(query_xyz, dtype=np.float32)
         self.ix = ora.F32Index(self.t)
+        self.device = torch.device("cpu")
+        self.nq = len(self.q)
 
     def step(self, T, rmax):
         R, t = _rt(T)
@@ -71,16 +73,22 @@ class OracleEngine:
         out[:len(k)] = k
         return out
 
-    def accumulate_slice(self, T_dev, q, keys, tgt):
+    def key_owner(self, keys, bounds, out):
+        k = keys.numpy()
+        b = bounds.numpy()
+        o = np.where(k == NO_KEY, 255, np.searchsorted(b, k & 0xFFFFFFFF, side="right") - 1).astype(np.uint8)
+        out[:len(o)] = torch.from_numpy(o)
+        return out
+
+    def accumulate_owned(self, T_dev, keys, owner, rank, lo, hi):
         R, t = _rt(T_dev.numpy().reshape(4, 4))
-        q = np.ascontiguousarray(np.asarray(q), dtype=np.float32)
-        k = keys.numpy()[:len(q)]
-        ok = k != NO_KEY
-        # the winners as a dense target table in slice order (accumulate reads tgt[idx[i]])
-        idx = np.where(ok, np.arange(len(q)), -1).astype(np.int32)
-        win = np.ascontiguousarray(np.asarray(tgt, dtype=np.float32)[np.where(ok, k & 0xFFFFFFFF, 0)])
-        d2 = np.where(ok, (k >> 32).astype(np.uint32).view(np.float32), np.inf).astype(np.float32)
-        return torch.from_numpy(ora.icp_accumulate(win, q, R, t, idx, d2))
+        k = keys.numpy()[:len(self.q)]
+        o = owner.numpy()[:len(self.q)]
+        g = k & 0xFFFFFFFF
+        mine = (o == rank) & (k != NO_KEY) & (g >= lo) & (g < hi)
+        idx = np.where(mine, g - lo, -1).astype(np.int32)
+        d2 = np.where(mine, (k >> 32).astype(np.uint32).view(np.float32), np.inf).astype(np.float32)
+        return torch.from_numpy(ora.icp_accumulate(self.t, self.q, R, t, idx, d2))
 
     def slab_guard(self, T_dev, box, lo, hi, flag):
         T = T_dev.numpy().reshape(4, 4)

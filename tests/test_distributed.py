@@ -60,9 +60,13 @@ def _worker(rank, world, port, mode, out):
                                                                     b[rank + 1] + halo - 0.25))
         assert ok
     elif mode == "target_sharded_dev":
-        lo, hi = D.shard_range(len(tgt), world, rank)
-        eng = OracleEngine(tgt[lo:hi], q)
-        err, T = D.run_target_sharded_dev(eng, np.eye(4), 0.25, 8, lo, torch.from_numpy(q), torch.from_numpy(tgt))
+        # x-sorted target, equal-count shards: each rank holds ONLY its shard
+        tgt = tgt[np.argsort(tgt[:, 0], kind="stable")]
+        bounds = [D.shard_range(len(tgt), world, r)[0] for r in range(world)] + [len(tgt)]
+        lo, hi = bounds[rank], bounds[rank + 1]
+        eng = OracleEngine(tgt[lo:hi].copy(), q)
+        del tgt
+        err, T = D.run_target_sharded_dev(eng, np.eye(4), 0.25, 8, bounds)
     else:
         lo, hi = D.shard_range(len(tgt), world, rank)
         eng = OracleEngine(tgt[lo:hi], q)

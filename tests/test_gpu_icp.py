@@ -78,6 +78,14 @@ def test_verify_pass_exact_over_registration(ctx):
         gi = ci.cpu().numpy()
         assert np.array_equal(gi, ei), f"iter {it}: {(gi != ei).sum()} mismatching correspondences"
         assert np.array_equal(cd.cpu().numpy()[ei >= 0], ed[ei >= 0])
+        # the incremental raw-frame accounting: every accounted pair is this pose's exact winner
+        # (the pair count is exact) and the accumulators match the oracle's direct sums
+        gacc = acc.cpu().numpy().copy()
+        eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
+        assert gacc[0] == eacc[0], f"iter {it}: {gacc[0]} accounted pairs, oracle {eacc[0]}"
+        scale = np.abs(eacc[:23]).max()
+        assert np.allclose(gacc[:22], eacc[:22], rtol=1e-7, atol=1e-8 * scale), f"iter {it}"
+        assert abs(gacc[22] - eacc[22]) <= 1e-6 * eacc[22], f"iter {it}: sum d2 {gacc[22]} vs {eacc[22]}"
         searched.append(icp.last_searched())
         poses.append(T)
         rc, dT = ops.icp_solve(acc.cpu().numpy())
@@ -243,26 +251,30 @@ def test_target_sharded_keys_match_oracle(ctx):
         e.close()
 
 
-def test_target_sharded_dev_reduce_scatter_form(ctx):
-    """Device-resident target-sharded loop pieces (keys_dev + accumulate_slice): x-slab shards
-    (so most queries lie outside a shard's grid and take the octant pass's out-of-grid exit,
-    then the verify pass), MIN of the keys = the oracle's global correspondences bit-exact at
-    every pose of a sequence; the two query slices' accumulators sum to the oracle's."""
+def test_target_sharded_dev_owned_form(ctx):
+    """Device-resident target-sharded loop pieces (keys_dev + keys_owner + accumulate_owned), two
+    shard engines on one GPU, each holding ONLY its x-slab of the target: most queries lie
+    outside a shard's grid (the octant pass's out-of-grid exit, then the verify passes).  The
+    MIN of the keys = the oracle's global correspondences bit-exact at every pose of a
+    sequence; the owners of the winners split the queries, and the two ranks' accumulators --
+    each over the queries whose winner it owns, read from its own shard -- sum to the
+    oracle's."""
     import torch
     from pointcloudprocess_amd import distributed as D, ops, synth
     tgt, q = _pair(150_000, 33, synth.rigid())
     tgt = tgt[torch.argsort(tgt[:, 0])].contiguous()  # global index = x order: slabs
     n, nq = tgt.shape[0], q.shape[0]
-    dq, dt = q.to(ctx.device), tgt.to(ctx.device)
-    shards = [D.shard_range(n, 2, r) for r in range(2)]
-    engines = [D.GpuEngine(ctx, dt[lo:hi], dq, cell_size=0.1) for lo, hi in shards]
+    dq = q.to(ctx.device)
+    bounds = [D.shard_range(n, 2, r)[0] for r in range(2)] + [n]
+    engines = [D.GpuEngine(ctx, tgt[bounds[r]:bounds[r + 1]].to(ctx.device), dq, cell_size=0.1) for r in range(2)]
+    bnd = torch.tensor(bounds, dtype=torch.int64, device=ctx.device)
     T_dev, _ = engines[0].new_pose(np.eye(4))
     ix = ora.F32Index(tgt.numpy())
     for T in (np.eye(4), synth.rigid(0.1, 0.05, 0.0, (0.02, 0.01, 0.0)), synth.rigid(0.3, 0.1, -0.05, (0.1, 0.0, 0.02)),
               synth.rigid(0.1, 0.05, 0.0, (0.02, 0.01, 0.0))):
         T_dev.copy_(torch.from_numpy(np.ascontiguousarray(T.reshape(16))).to(ctx.device))
-        keys = torch.minimum(engines[0].keys_dev(T_dev, 0.25, shards[0][0]),
-                             engines[1].keys_dev(T_dev, 0.25, shards[1][0]))
+        local = [engines[r].keys_dev(T_dev, 0.25, bounds[r]).clone() for r in range(2)]
+        keys = torch.minimum(local[0], local[1])
         k = keys.cpu().numpy()
         R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
         ei, ed = ix.correspond(q.numpy(), R, t, 0.25)
@@ -270,9 +282,12 @@ def test_target_sharded_dev_reduce_scatter_form(ctx):
         assert np.array_equal(none, ei < 0)
         assert np.array_equal((k[~none] & 0xFFFFFFFF).astype(np.int32), ei[~none])
         assert np.array_equal((k[~none] >> 32).astype(np.uint32).view(np.float32), ed[~none])
-        h = nq // 2
-        acc = (ops.accumulate_slice(ctx, T_dev, dq[:h], keys[:h], dt).cpu().numpy().copy() +
-               ops.accumulate_slice(ctx, T_dev, dq[h:], keys[h:], dt).cpu().numpy().copy())
+        owner = ops.keys_owner(ctx, keys, bnd)
+        o = owner.cpu().numpy()
+        assert np.array_equal(o == 255, none)
+        assert np.array_equal(o[~none], (ei[~none] >= bounds[1]).astype(np.uint8))
+        acc = sum(engines[r].accumulate_owned(T_dev, local[r], owner, r, bounds[r], bounds[r + 1]).cpu().numpy().copy()
+                  for r in range(2))
         eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
         assert np.allclose(acc[:23], eacc[:23], rtol=1e-12, atol=1e-12 * np.abs(eacc[:23]).max())
     for e in engines:
