@@ -14,6 +14,8 @@
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include "sortcfg.hpp"
 
 #include "grid.hpp"
@@ -57,6 +59,12 @@ struct pcp_icp {
     double* acc = nullptr;        // 24 (scratch for pcp_icp_run)
     int nb_fast = 0, nb_ring = 0;
     int nb_fast_l = 0;            // octant grid of the list launches (<= nb_fast)
+    int engine_tile = 1;          // dense grids: the LDS-tiled streaming search (0: the cached
+                                  // verify / octant / ring passes; env PCP_ICP_ENGINE=cache)
+    int nb_tile = 0;
+    int32_t* bstart = nullptr;    // tile engine: first sorted query of each query brick (+ nq), nbk + 1
+    int64_t nbk = 0;              // query bricks
+    uint32_t* fb_base = nullptr;  // tile engine: per workgroup, its fallback segment's start              // tile engine: workgroups (grid-stride over the tiles)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr, ev_ver = nullptr;
     float* pose_dev = nullptr;    // 24 floats: this launch's pose (R row-major, t), then the previous one
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-launch timing events (device loop)
@@ -154,7 +162,8 @@ __device__ __forceinline__ void load_prev_pose(IcpArgs& a) {
 }
 
 // Ablation switches for profiling (env PCP_ICP_ABLATE); results are wrong when any is set.
-constexpr int kDbgNoScan = 1, kDbgNoAccum = 4, kDbgNoFallback = 8, kDbgCount = 16, kDbgNoVerify = 64;
+constexpr int kDbgNoScan = 1, kDbgNoAccum = 4, kDbgNoFallback = 8, kDbgCount = 16, kDbgNoVerify = 64,
+              kDbgTileOctOnly = 128, kDbgTileNone = 256;
 
 __device__ __forceinline__ void xform(const IcpArgs& a, const float4 q, float& x, float& y, float& z) {
     // q' = R q + t: x' = fmaf(R02,z,fmaf(R01,y,fmaf(R00,x,t0)))
@@ -1271,6 +1280,489 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
     }
 }
 
+// ---- LDS-tiled streaming search (dense grid, the default engine)
+// One pass over the sorted queries per launch, no per-query state.  The queries are sorted
+// once by 8x8x8-cell brick of the target grid (pcp_icp_create); a workgroup takes whole query
+// bricks, transforms their queries, and stages in LDS every target of the box of cells
+// [min c - 1, max c + 1] around the brick's query cells c: per (y, z) row of the box one
+// contiguous range of the dense table, plus a table of the rows' cell starts.  Each query then
+// runs, entirely in LDS:
+//   1. the 2x2x2 octant block (the four x-rows [floor(f - 1/2), +1]) keeping its 3 nearest on
+//      packed keys (Top3 as the octant pass), settled when the exact winner among them is
+//      within the block's certified radius (>= 1/2 cell) and beats the 4th key;
+//   2. otherwise the 3x3x3 cells around it (1-NN by (d2, index), certified within >= 1 cell);
+//   3. otherwise the global fallback list (k_icp_ring's exact box search).
+// Both stages read the same float4 records as a global search, so d2 and the winner are
+// bit-identical to the contract.  A brick whose box exceeds the LDS capacity is staged per
+// 256-query round; a round still too large sends its queries to the fallback list.
+// Accumulation as the octant pass (fp32 per 64-query chunk, centred, un-centred in fp64).
+constexpr int kTilePts = 3584;    // LDS points (56 KB; the last slot holds the far sentinel)
+constexpr int kTileTab = 3072;    // LDS cell-start table entries
+constexpr int kTileRows = 384;    // box rows (y, z)
+constexpr int kTileW = kIcpBlock / 64;
+constexpr int kStageU = 4;        // staging: global loads in flight per thread
+
+struct TileShared {
+    float4 pts[kTilePts];
+    uint32_t tab[kTileTab];        // local start of cell x0 + j of row r: tab[r * (nx + 1) + j]
+    uint32_t rgs[kTileRows];       // per row: global sorted position of its first staged point
+    uint32_t rls[kTileRows + 1];   // per row: local start (exclusive prefix of the row lengths)
+    int box[8];                    // x0, x1, y0, y1, z0, z1, ok, npts
+    int red[kTileW][6];
+    uint32_t fbw[2][kTileW];       // per round (parity): each wave's fallback count
+    double acc[kTileW][kAcc];
+};
+
+// position in LDS of candidate v of four concatenated LDS row ranges (rows past the list: the
+// far sentinel `sent`)
+__device__ __forceinline__ uint32_t tile_addr(uint32_t v, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t L,
+                                              uint32_t o0, uint32_t o1, uint32_t o2, uint32_t o3, uint32_t sent) {
+    return cat_addr_l(v, c1, c2, c3, L, o0, o1, o2, o3, sent);
+}
+
+// Stage the box of cells around the queries of one (sub)tile.  Every thread passes the cell
+// coordinates of its queries (in-grid ones; others pass inq = false).  Returns false (uniform)
+// when the box exceeds the LDS capacity.
+__device__ __forceinline__ bool tile_stage(const IcpArgs& a, TileShared& S, const int (&cmin)[3], const int (&cmax)[3]) {
+    const GridDesc& g = a.g;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // block-wide min / max of the query cells
+    int v[6] = {cmin[0], cmin[1], cmin[2], -cmax[0], -cmax[1], -cmax[2]};
+#pragma unroll
+    for (int k = 0; k < 6; k++) v[k] = wave_min_i(v[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 6; k++) S.red[wid][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int m[6];
+        for (int k = 0; k < 6; k++) {
+            m[k] = S.red[0][k];
+            for (int w = 1; w < kTileW; w++) m[k] = min(m[k], S.red[w][k]);
+        }
+        const int x0 = max(m[0] - 1, 0), y0 = max(m[1] - 1, 0), z0 = max(m[2] - 1, 0);
+        const int x1 = min(-m[3] + 1, g.n[0] - 1), y1 = min(-m[4] + 1, g.n[1] - 1), z1 = min(-m[5] + 1, g.n[2] - 1);
+        const bool any = m[0] <= -m[3];
+        const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
+        const bool fits = any && (int64_t)ny * nz <= kTileRows && (int64_t)ny * nz * (nx + 1) <= kTileTab;
+        S.box[0] = x0; S.box[1] = x1; S.box[2] = y0; S.box[3] = y1; S.box[4] = z0; S.box[5] = z1;
+        S.box[6] = fits ? 1 : 0;
+    }
+    __syncthreads();
+    if (!S.box[6]) return false;
+    const int x0 = S.box[0], x1 = S.box[1], y0 = S.box[2], y1 = S.box[3], z0 = S.box[4], z1 = S.box[5];
+    const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nrows = ny * (z1 - z0 + 1);
+    // row ranges: [cstart(x0), cstart(x1 + 1)) (x1 + 1 == n0 reads the next row's start = this row's end)
+    for (int r = threadIdx.x; r < nrows; r += blockDim.x) {
+        const int y = y0 + r % ny, z = z0 + r / ny;
+        const uint32_t s = g.cstart[dense_id(g, x0, y, z)], e = g.cstart[dense_id(g, x1, y, z) + 1];
+        S.rgs[r] = s;
+        S.rls[r + 1] = e - s;  // lengths, scanned below
+    }
+    __syncthreads();
+    if (wid == 0) {  // exclusive scan of the row lengths (one wave, 64 rows per step)
+        uint32_t carry = 0;
+        for (int r0 = 0; r0 < nrows; r0 += 64) {
+            const int r = r0 + lane;
+            uint32_t x = r < nrows ? S.rls[r + 1] : 0u;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (r < nrows) S.rls[r + 1] = carry + x;
+            carry += (uint32_t)__shfl((int)x, 63, 64);
+        }
+        if (lane == 0) {
+            S.rls[0] = 0;
+            S.box[7] = (int)carry;
+            S.box[6] = carry + 1 <= (uint32_t)kTilePts ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    if (!S.box[6]) return false;
+    const int npts = S.box[7];
+    // the cell-start table (local positions) and the points: flat over the entries, kStageU
+    // independent global loads in flight per thread
+    constexpr int U = kStageU;
+    const int ne = nrows * (nx + 1);
+    for (int e0 = threadIdx.x; e0 < ne; e0 += U * kIcpBlock) {
+        uint32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = e0 + u * kIcpBlock;
+            if (e < ne) {
+                const int r = e / (nx + 1), j = e - r * (nx + 1);
+                v[u] = g.cstart[dense_id(g, x0, y0 + r % ny, z0 + r / ny) + j];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = e0 + u * kIcpBlock;
+            if (e < ne) {
+                const int r = e / (nx + 1);
+                S.tab[e] = S.rls[r] + (v[u] - S.rgs[r]);
+            }
+        }
+    }
+    for (int e0 = threadIdx.x; e0 < npts; e0 += U * kIcpBlock) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = e0 + u * kIcpBlock;
+            if (e < npts) {
+                // the row holding local position e: the last r with rls[r] <= e
+                int lo = 0, hi = nrows - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (S.rls[mid] <= (uint32_t)e) lo = mid; else hi = mid - 1;
+                }
+                v[u] = ld16(a.tp, S.rgs[lo] + ((uint32_t)e - S.rls[lo]));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = e0 + u * kIcpBlock;
+            if (e < npts) S.pts[e] = v[u];
+        }
+    }
+    if (threadIdx.x == 0) {
+        S.pts[npts] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(0x7fffffff));
+        if (a.dbg & kDbgCount) {
+            atomicAdd(a.dbgcnt + 10, (unsigned long long)npts);
+            atomicAdd(a.dbgcnt + 11, 1ull);
+            atomicAdd(a.dbgcnt + 14, (unsigned long long)nrows);
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
+// one query against the staged box: octant, then the 3x3x3 cells; returns settled (else it goes
+// to the fallback list) and the winner (found: d2, coordinates, global sorted position)
+struct TileRes {
+    bool settled = false, found = false;
+    float d2 = INFINITY, px = 0.f, py = 0.f, pz = 0.f;
+    uint32_t gpos = ~0u;
+    int stage = 0;  // settled by: 1 the octant, 2 the 3x3x3 cells
+};
+// Every lane of the wave must call it (the octant's trip count is a wave reduction); a lane
+// with no query (active = false) scans nothing and returns unsettled.
+__device__ __forceinline__ TileRes tile_query(const IcpArgs& a, const TileShared& S, bool active, float qx, float qy,
+                                              float qz, float fx, float fy, float fz) {
+    const GridDesc& g = a.g;
+    const int x0 = S.box[0], y0 = S.box[2], z0 = S.box[4];
+    const int nx = S.box[1] - x0 + 1, ny = S.box[3] - y0 + 1;
+    const int nxe = nx + 1;
+    const uint32_t sent = (uint32_t)S.box[7];
+    auto row_of = [&](int y, int z) { return (z - z0) * ny + (y - y0); };
+    TileRes res;
+    // ---- 1. octant (2x2x2 block at floor(f - 1/2))
+    const int bx = (int)floorf(fx - a.rho), by = (int)floorf(fy - a.rho), bz = (int)floorf(fz - a.rho);
+    const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
+    uint32_t rs[4], rn[4], rd[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int y = by + (r & 1), z = bz + (r >> 1);
+        const bool in = active && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
+        const int R = in ? row_of(y, z) : 0;
+        const uint32_t s = in ? S.tab[R * nxe + (xa - x0)] : 0u, e = in ? S.tab[R * nxe + (xb + 1 - x0)] : 0u;
+        rs[r] = s;
+        rn[r] = e - s;
+        rd[r] = in ? S.rgs[R] - S.rls[R] : 0u;  // local -> global sorted position
+    }
+    const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
+    const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
+    const uint32_t Lw = (uint32_t)__builtin_amdgcn_readfirstlane(wave_max_u((int)L));
+    if ((a.dbg & kDbgCount) && (threadIdx.x & 63) == 0) {
+        atomicAdd(a.dbgcnt + 12, (unsigned long long)Lw);
+        atomicAdd(a.dbgcnt + 13, 1ull);
+    }
+    float d0 = INFINITY, dnext = INFINITY, wx = 0.f, wy = 0.f, wz = 0.f;
+    int wj = 0x7fffffff;
+    uint32_t wv = ~0u;
+    if (Lw <= kMaxOctList) {
+        Top3P k;
+        uint32_t v = 0;
+        constexpr int U = 4;
+        for (; v < Lw; v += U) {
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) p[u] = S.pts[tile_addr(v + u, c1, c2, c3, L, o0, o1, o2, o3, sent)];
+#pragma unroll
+            for (int u = 0; u < U; u++) k.consider(qx, qy, qz, p[u], v + u);
+        }
+        const uint32_t kt[3] = {k.t0, k.t1, k.t2};
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            if (kt[s] == kKeyMax) continue;
+            const uint32_t vv = kt[s] & 0xffu;
+            const float4 p = S.pts[tile_addr(vv, c1, c2, c3, L, o0, o1, o2, o3, sent)];
+            const float e = icp_d2(qx, qy, qz, p);
+            const int id = __float_as_int(p.w);
+            const bool t = e < d0 || (e == d0 && id < wj);
+            d0 = t ? e : d0;
+            wj = t ? id : wj;
+            wv = t ? vv : wv;
+            wx = t ? p.x : wx;
+            wy = t ? p.y : wy;
+            wz = t ? p.z : wz;
+        }
+        dnext = k.t3 == kKeyMax ? INFINITY : __uint_as_float(k.t3 & ~0xffu);
+    } else {  // a list of 256 or more: compare-swap top 3 on exact d2
+        Top3 b;
+        for (uint32_t v = 0; v < L; v++) b.consider(qx, qy, qz, S.pts[tile_addr(v, c1, c2, c3, L, o0, o1, o2, o3, sent)], v);
+        const uint32_t kp[3] = {b.p0, b.p1, b.p2};
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            if (kp[s] == ~0u) continue;
+            const float4 p = S.pts[tile_addr(kp[s], c1, c2, c3, L, o0, o1, o2, o3, sent)];
+            const float e = icp_d2(qx, qy, qz, p);
+            const int id = __float_as_int(p.w);
+            const bool t = e < d0 || (e == d0 && id < wj);
+            d0 = t ? e : d0;
+            wj = t ? id : wj;
+            wv = t ? kp[s] : wv;
+            wx = t ? p.x : wx;
+            wy = t ? p.y : wy;
+            wz = t ? p.z : wz;
+        }
+        dnext = b.d3;
+    }
+    if (!active) return res;
+    {
+        const float m = fminf(fminf(fminf(fx - (float)bx, (float)(bx + 2) - fx), fminf(fy - (float)by, (float)(by + 2) - fy)),
+                              fminf(fz - (float)bz, (float)(bz + 2) - fz)) - a.mc;
+        const float rr = m * g.hf;
+        const float cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
+        const bool found = d0 <= a.r2;
+        if (found ? (d0 < dnext && d0 <= cert2) : a.r2 <= cert2) {
+            res.settled = true;
+            res.stage = 1;
+            res.found = found;
+            res.d2 = d0;
+            res.px = wx;
+            res.py = wy;
+            res.pz = wz;
+            if (found) {
+                const uint32_t rw = wv < c1 ? 0u : wv < c2 ? 1u : wv < c3 ? 2u : 3u;
+                const uint32_t loc = tile_addr(wv, c1, c2, c3, L, o0, o1, o2, o3, sent);
+                res.gpos = loc + (rw == 0 ? rd[0] : rw == 1 ? rd[1] : rw == 2 ? rd[2] : rd[3]);
+            }
+            return res;
+        }
+    }
+    if (a.dbg & kDbgTileOctOnly) return res;
+    // ---- 2. the 3x3x3 cells around the query's cell, from the octant's winner as the bound
+    const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
+    const float lx = fx - (float)cx, ly = fy - (float)cy, lz = fz - (float)cz;
+    const float inv_h2 = g.inv_hf * g.inv_hf;
+    const float gxl = sq_gap(lx, a.mc), gxr = sq_gap(1.f - lx, a.mc);
+    float bd = a.r2;
+    int bj = 0x7fffffff;
+    uint32_t bl = ~0u, bg = ~0u;
+    if (d0 <= a.r2) {
+        bd = d0;
+        bj = wj;
+    }
+    for (int dz = -1; dz <= 1; dz++) {
+        const int z = cz + dz;
+        if (z < 0 || z >= g.n[2]) continue;
+        const float gz2 = sq_gap(axis_gap<float>(z, cz, lz), a.mc);
+        for (int dy = -1; dy <= 1; dy++) {
+            const int y = cy + dy;
+            if (y < 0 || y >= g.n[1]) continue;
+            const float lim = bd * 1.00002f * inv_h2;
+            const float gyz = gz2 + sq_gap(axis_gap<float>(y, cy, ly), a.mc);
+            if (gyz > lim) continue;
+            int xlo = max(cx - 1, 0), xhi = min(cx + 1, g.n[0] - 1);
+            if (xlo == cx - 1 && gyz + gxl > lim) xlo = cx;
+            if (xhi == cx + 1 && gyz + gxr > lim) xhi = cx;
+            if (xlo > xhi) continue;
+            const int R = row_of(y, z);
+            const uint32_t s = S.tab[R * nxe + (xlo - x0)], e = S.tab[R * nxe + (xhi + 1 - x0)];
+            const uint32_t del = S.rgs[R] - S.rls[R];
+            for (uint32_t k = s; k < e; k++) {
+                const float4 p = S.pts[k];
+                const float d2 = icp_d2(qx, qy, qz, p);
+                const int id = __float_as_int(p.w);
+                const bool t = d2 < bd || (d2 == bd && id <= bj);
+                bd = t ? d2 : bd;
+                bj = t ? id : bj;
+                bl = t ? k : bl;
+                bg = t ? k + del : bg;
+            }
+        }
+    }
+    const float m3 = fminf(fminf(fminf(fx - (float)(cx - 1), (float)(cx + 2) - fx), fminf(fy - (float)(cy - 1), (float)(cy + 2) - fy)),
+                           fminf(fz - (float)(cz - 1), (float)(cz + 2) - fz)) - a.mc;
+    const float r3 = m3 * g.hf;
+    const float c3e = r3 * r3 * (1.f - 2e-5f);
+    const bool found3 = bj != 0x7fffffff;
+    if (found3 ? bd <= c3e : a.r2 <= c3e) {
+        res.settled = true;
+        res.stage = 2;
+        res.found = found3;
+        if (found3) {
+            const float4 p = S.pts[bl];
+            res.d2 = bd;
+            res.px = p.x;
+            res.py = p.y;
+            res.pz = p.z;
+            res.gpos = bg;
+        }
+    }
+    return res;
+}
+
+// query i of the sorted set under the iteration's pose: coordinates, cell coordinates, in-grid
+// (staged search) or, outside, whether it is farther than rmax from the grid (no correspondence)
+struct TileQ {
+    float x, y, z, fx, fy, fz;
+    bool inq, out;
+};
+__device__ __forceinline__ TileQ tile_load_query(const IcpArgs& a, int64_t i) {
+    const GridDesc& g = a.g;
+    TileQ t;
+    xform(a, a.q[i], t.x, t.y, t.z);
+    t.fx = cell_f<float>(g, t.x, 0);
+    t.fy = cell_f<float>(g, t.y, 1);
+    t.fz = cell_f<float>(g, t.z, 2);
+    t.inq = t.fx >= 0.f && t.fx < (float)g.n[0] && t.fy >= 0.f && t.fy < (float)g.n[1] && t.fz >= 0.f &&
+            t.fz < (float)g.n[2];
+    t.out = false;
+    if (!t.inq) {
+        const float ox = fmaxf(fmaxf(-t.fx, t.fx - (float)g.n[0]), 0.f);
+        const float oy = fmaxf(fmaxf(-t.fy, t.fy - (float)g.n[1]), 0.f);
+        const float oz = fmaxf(fmaxf(-t.fz, t.fz - (float)g.n[2]), 0.f);
+        const float dout = fmaxf(sqrtf(__fmaf_rn(oz, oz, __fmaf_rn(oy, oy, ox * ox))) - a.mc, 0.f) * g.hf;
+        t.out = dout * dout > a.r2 * 1.0001f;
+    }
+    return t;
+}
+
+// first position p in [0, n] with v[p] >= key (v ascending)
+__device__ __forceinline__ int64_t lower_bound_i32(const int32_t* v, int64_t n, int64_t key) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)v[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// Workgroup w takes the query bricks (runs of sorted queries of one 8x8x8-cell brick,
+// bstart[0..nbk], bstart[nbk] = nq) starting in [w Q, (w + 1) Q), Q = ceil(nq / grid): a
+// contiguous query range [qlo, qhi) about Q long.  Per brick: one pass over its queries for
+// the box of their cells under the pose, the box staged once, then its queries in rounds of
+// 256.  Fallback queries are written in query order at fb[qlo ..] (workgroup segment).
+__global__ void __launch_bounds__(kIcpBlock, 2) k_icp_tile(IcpArgs a, const int32_t* __restrict__ bstart, int64_t nbk,
+                                                           uint32_t* __restrict__ fb_base, int write_cand) {
+    __shared__ TileShared S;
+    load_pose(a);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane < kAcc) S.acc[wid][lane] = 0.0;
+    const int64_t Q = (a.nq + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = lower_bound_i32(bstart, nbk, (int64_t)blockIdx.x * Q);
+    const int64_t b1 = lower_bound_i32(bstart, nbk, (int64_t)(blockIdx.x + 1) * Q);
+    const int64_t qlo = bstart[b0];
+    uint32_t fbn = 0;  // the workgroup's fallback count so far (same in every thread)
+    int par = 0;
+    for (int64_t b = b0; b < b1; b++) {
+        const int64_t s = bstart[b], e = bstart[b + 1];
+        // 1. the box of the brick's query cells under the pose
+        int cmin[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, cmax[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
+        for (int64_t i = s + threadIdx.x; i < e; i += kIcpBlock) {
+            const TileQ t = tile_load_query(a, i);
+            if (t.inq) {
+                const int c[3] = {(int)floorf(t.fx), (int)floorf(t.fy), (int)floorf(t.fz)};
+#pragma unroll
+                for (int d = 0; d < 3; d++) {
+                    cmin[d] = min(cmin[d], c[d]);
+                    cmax[d] = max(cmax[d], c[d]);
+                }
+            }
+        }
+        const bool whole = tile_stage(a, S, cmin, cmax);
+        if ((a.dbg & kDbgCount) && threadIdx.x == 0) {
+            atomicAdd(a.dbgcnt + 0, 1ull);
+            if (whole) atomicAdd(a.dbgcnt + 1, 1ull);
+        }
+        // 2. its queries, 256 per round
+#pragma unroll 1
+        for (int64_t r0 = s; r0 < e; r0 += kIcpBlock) {
+            const int64_t i = r0 + threadIdx.x;
+            const bool val = i < e;
+            TileQ t{};
+            if (val) t = tile_load_query(a, i);
+            bool staged = whole;
+            if (!whole) {  // the round on its own
+                int rmin[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, rmax[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
+                if (val && t.inq) {
+                    rmin[0] = rmax[0] = (int)floorf(t.fx);
+                    rmin[1] = rmax[1] = (int)floorf(t.fy);
+                    rmin[2] = rmax[2] = (int)floorf(t.fz);
+                }
+                __syncthreads();  // the previous round's readers are done with the LDS
+                staged = tile_stage(a, S, rmin, rmax);
+                if ((a.dbg & kDbgCount) && threadIdx.x == 0) atomicAdd(a.dbgcnt + (staged ? 2 : 3), 1ull);
+            }
+            // full wave: the octant's trip count is reduced over the wave
+            TileRes r = tile_query(a, S, val && !t.out && t.inq && staged && !(a.dbg & kDbgTileNone), t.x, t.y, t.z,
+                                   t.fx, t.fy, t.fz);
+            bool fb = false;
+            if (val) {
+                if (t.out) r.settled = true;  // farther than rmax from the grid: no correspondence
+                fb = !r.settled;
+                if (write_cand && r.settled)
+                    a.cand[i] = make_uint4(r.found ? r.gpos : ~0u, ~0u, ~0u, pack_dlb(0.f, a.launch));
+            }
+            // fallback list in query order: this wave's place among the workgroup's four
+            const uint64_t fbm = __ballot(fb);
+            if (lane == 0) S.fbw[par][wid] = (uint32_t)__popcll(fbm);
+            __syncthreads();
+            uint32_t before = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < kTileW; w++) {
+                const uint32_t c = S.fbw[par][w];
+                before += w < wid ? c : 0u;
+                tot += c;
+            }
+            par ^= 1;
+            if (fb) {
+                const uint32_t pos = fbn + before + __builtin_amdgcn_mbcnt_hi((uint32_t)(fbm >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)fbm, 0u));
+                a.fb[qlo + pos] = (int32_t)i;
+            }
+            fbn += tot;
+            if (a.dbg & kDbgCount) {
+                const uint64_t m4 = __ballot(val && r.stage == 1), m5 = __ballot(val && r.stage == 2);
+                const uint64_t m6 = __ballot(fb && t.inq && staged), m7 = __ballot(fb && t.inq && !staged);
+                const uint64_t m8 = __ballot(fb && !t.inq), m9 = __ballot(val && t.out);
+                if (lane == 0) {
+                    atomicAdd(a.dbgcnt + 24, (unsigned long long)__popcll(m4));
+                    atomicAdd(a.dbgcnt + 25, (unsigned long long)__popcll(m5));
+                    atomicAdd(a.dbgcnt + 26, (unsigned long long)__popcll(m6));
+                    atomicAdd(a.dbgcnt + 27, (unsigned long long)__popcll(m7));
+                    atomicAdd(a.dbgcnt + 28, (unsigned long long)__popcll(m8));
+                    atomicAdd(a.dbgcnt + 29, (unsigned long long)__popcll(m9));
+                }
+            }
+            const bool acc_ok = val && r.settled && r.found && !(a.dbg & kDbgNoAccum);
+            const Best w{r.d2, 0, 0u, r.px, r.py, r.pz};
+            chunk_accumulate(acc_ok, t.x, t.y, t.z, w, S.acc[wid], lane);
+        }
+        __syncthreads();  // the LDS box is reused by the next brick
+    }
+    if (threadIdx.x == 0) {
+        a.fb_count[blockIdx.x] = fbn;
+        a.fb_off[blockIdx.x] = fbn;
+        fb_base[blockIdx.x] = (uint32_t)qlo;
+        if (blockIdx.x == 0) a.fb_off[gridDim.x] = 0u;
+    }
+    write_wave_partials(S.acc, a.partials + (int64_t)blockIdx.x * kAcc);
+}
+
 // Lanes per query by the list's density (measured per launch on the C4 bench registration,
 // tools/gpu_octg_ab.sh): dense lists share candidate lines between neighbouring queries and
 // want one lane each; sparse ones want the group form.
@@ -1453,13 +1945,15 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
     write_wave_partials(s_acc, partials + (int64_t)blockIdx.x * kAcc);
 }
 
-// concatenate the per-wave fallback segments (one wave per segment)
+// concatenate the fallback segments (one wave per segment; segment s starts at base[s], or at
+// s * seg_cap without a base table)
 __global__ void k_fb_compact(const int32_t* fb, const uint32_t* cnt, const uint32_t* off, int64_t nseg,
-                             int64_t seg_cap, int32_t* out) {
+                             int64_t seg_cap, int32_t* out, const uint32_t* base = nullptr) {
     const int64_t seg = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (seg >= nseg) return;
     const uint32_t n = cnt[seg], o = off[seg];
-    for (uint32_t k = threadIdx.x & 63; k < n; k += 64) out[o + k] = fb[seg * seg_cap + k];
+    const int64_t b = base ? (int64_t)base[seg] : seg * seg_cap;
+    for (uint32_t k = threadIdx.x & 63; k < n; k += 64) out[o + k] = fb[b + k];
 }
 
 // fixed-order reduction of nb partial rows of 24 doubles -> out[24]: thread t sums column
@@ -1739,6 +2233,20 @@ __global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_
     }
 }
 
+// the first query of each query brick (PCP_QBRICK^3 cells) in the sorted keys (finite keys only)
+#ifndef PCP_ICP_TILE_DEFAULT  // dense grids: 1 = the LDS-tiled engine by default, 0 = the cached engine
+#define PCP_ICP_TILE_DEFAULT 0
+#endif
+struct BrickHead {
+    const uint32_t* k;
+    uint32_t end;
+    __device__ bool operator()(int i) const {
+        constexpr uint32_t B3 = PCP_QBRICK * PCP_QBRICK * PCP_QBRICK;
+        const uint32_t v = k[i];
+        return v < end && (i == 0 || v / B3 != k[i - 1] / B3);
+    }
+};
+
 // number of finite queries = first position of the sentinel key in the sorted keys
 // (a single-address atomic per wave costs ~9 ms at 50M queries; this costs nothing)
 __global__ void k_first_at_least(const uint32_t* sorted, int64_t n, uint32_t key, unsigned long long* out) {
@@ -1939,6 +2447,43 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     }
     if (icp->dbgcnt) PCP_HIP(ctx, hipMemsetAsync(icp->dbgcnt, 0, 32 * sizeof(unsigned long long), ctx->stream));
     PCP_HIP(ctx, hipEventRecord(e0, ctx->stream));
+    if (a.g.dense && icp->engine_tile && icp->bstart) {
+        // the LDS-tiled streaming search of every query, then the exact fallback of the rest
+        icp->last_verified = false;
+        PCP_HIP(ctx, hipMemsetAsync(part_v, 0, (size_t)(icp->nb_ver + icp->nb_fast) * kAcc * sizeof(double),
+                                    ctx->stream));
+        a.partials = part_o;
+        a.nseg = icp->nb_tile;  // one fallback segment per workgroup
+        a.fb_seg = 0;
+        const int want_cand = (corr_idx != nullptr || args_out != nullptr) ? 1 : 0;
+        if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_ver, ctx->stream));
+        hipLaunchKernelGGL(k_icp_tile, dim3(icp->nb_tile), dim3(kIcpBlock), 0, ctx->stream, a,
+                           (const int32_t*)icp->bstart, icp->nbk, icp->fb_base, want_cand);
+        if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_mid, ctx->stream));
+        PCP_TRY(scan_u32_inplace(ctx, icp->fb_off, a.nseg + 1, nullptr));
+        hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)((a.nseg + 3) / 4)), dim3(256), 0, ctx->stream, icp->fb,
+                           (const uint32_t*)icp->fb_count, (const uint32_t*)icp->fb_off, a.nseg, (int64_t)0, icp->fbc,
+                           (const uint32_t*)icp->fb_base);
+        a.partials = part_r;
+        a.ring_g = icp->ring_g;
+        hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, ctx->stream, a, part_r,
+                           (const int32_t*)icp->fbc, (const uint32_t*)(icp->fb_off + a.nseg));
+        PCP_HIP(ctx, hipEventRecord(e1, ctx->stream));
+        hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kAcc * kRedGroups), 0, ctx->stream, icp->partials,
+                           icp->nb_ver + icp->nb_fast + icp->nb_ring, acc_dev, (const uint32_t*)(icp->fb_off + a.nseg));
+        if (corr_idx) {
+            if (icp->nq_in > icp->nq)
+                hipLaunchKernelGGL(k_fill_corr, dim3(grid_for(icp->nq_in, 256)), dim3(256), 0, ctx->stream, corr_idx,
+                                   corr_d2, icp->nq_in);
+            if (icp->nq > 0)
+                hipLaunchKernelGGL(k_scatter_corr, dim3(grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, a,
+                                   corr_idx, corr_d2);
+        }
+        if (args_out) *args_out = a;
+        icp->launches++;
+        PCP_LAUNCH_CHECK(ctx);
+        return PCP_OK;
+    }
     const bool verify = a.g.dense && icp->launches > 0;  // the first launch has nothing cached
     icp->last_verified = verify;
     if (a.g.dense) {
@@ -2072,6 +2617,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     hipStream_t st = ctx->stream;
     float4* qs = nullptr;
     int64_t nfin = 0;
+    int32_t* bst = nullptr;  // query bricks (dense target grids)
+    int64_t nbk = 0;
     {
         uint32_t *k0 = nullptr, *k1 = nullptr;
         float4* r0 = nullptr;
@@ -2081,8 +2628,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
         if (!rc) rc = pcp::dmalloc(ctx, &k1, nq);
         if (!rc) rc = pcp::dmalloc(ctx, &r0, nq);
         if (!rc) rc = pcp::dmalloc(ctx, &qs, nq + 1);
-        if (!rc) rc = pcp::dmalloc(ctx, &d_cnt, 1);
-        if (!rc && hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long), st) != hipSuccess)
+        if (!rc) rc = pcp::dmalloc(ctx, &d_cnt, 2);
+        if (!rc && hipMemsetAsync(d_cnt, 0, 2 * sizeof(unsigned long long), st) != hipSuccess)
             rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
         if (!rc && nq > 0) {
             hipLaunchKernelGGL(pcp::k_query_keys, dim3(pcp::grid_for(nq, 256)), dim3(256), 0, st, target->g, q,
@@ -2096,11 +2643,37 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
             if (!rc && e == hipSuccess)
                 hipLaunchKernelGGL(pcp::k_first_at_least, dim3(1), dim3(1), 0, st, k1, nq,
                                    pcp::query_key_end(target->g), d_cnt);
-            unsigned long long hc = 0;
-            if (!rc && e == hipSuccess) e = hipMemcpyAsync(&hc, d_cnt, sizeof(hc), hipMemcpyDeviceToHost, st);
+            // the tile engine's query bricks: heads of the brick runs -> k0 (as int32)
+            const bool bricks = target->g.dense;
+            if (!rc && e == hipSuccess && bricks) {
+                const pcp::BrickHead head{k1, pcp::query_key_end(target->g)};
+                size_t tb2 = 0;
+                e = rocprim::select(nullptr, tb2, rocprim::counting_iterator<int>(0), (int*)k0, d_cnt + 1, (size_t)nq,
+                                    head, st);
+                if (e == hipSuccess && tb2 > tb) {
+                    pcp::dfree(ctx, tmp);
+                    tmp = nullptr;
+                    rc = pcp::dmalloc(ctx, (char**)&tmp, tb2);
+                    tb = tb2;
+                }
+                if (!rc && e == hipSuccess)
+                    e = rocprim::select(tmp, tb2, rocprim::counting_iterator<int>(0), (int*)k0, d_cnt + 1, (size_t)nq,
+                                        head, st);
+            }
+            unsigned long long hc[2] = {0, 0};
+            if (!rc && e == hipSuccess) e = hipMemcpyAsync(hc, d_cnt, sizeof(hc), hipMemcpyDeviceToHost, st);
             if (!rc && e == hipSuccess) e = hipStreamSynchronize(st);
             if (!rc && e != hipSuccess) rc = pcp::hip_fail(ctx, e, "query sort", __FILE__, __LINE__);
-            nfin = (int64_t)hc;
+            nfin = (int64_t)hc[0];
+            if (!rc && bricks && hc[1] > 0) {
+                nbk = (int64_t)hc[1];
+                const int32_t last = (int32_t)nfin;
+                rc = pcp::dmalloc(ctx, &bst, (size_t)nbk + 1);
+                if (!rc && (hipMemcpyAsync(bst, k0, (size_t)nbk * sizeof(int32_t), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                            hipMemcpyAsync(bst + nbk, &last, sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+                            hipStreamSynchronize(st) != hipSuccess))
+                    rc = pcp::set_error(ctx, PCP_ERR_HIP, "query bricks");
+            }
         }
         pcp::dfree(ctx, k0);
         pcp::dfree(ctx, k1);
@@ -2109,6 +2682,7 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
         pcp::dfree(ctx, tmp);
         if (rc) {
             pcp::dfree(ctx, qs);
+            pcp::dfree(ctx, bst);
             return rc;
         }
     }
@@ -2120,6 +2694,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     icp->nq = nfin;
     icp->nq_in = nq;
     icp->q = qs;
+    icp->bstart = bst;
+    icp->nbk = nbk;
     int dev_cus = 256;  // one attribute query (the whole hipDeviceProp_t costs ~0.1 ms per create)
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess && cus > 0)
@@ -2132,6 +2708,10 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     const int64_t nwaves_l = (int64_t)icp->nb_fast_l * (pcp::kIcpBlock / 64);  // the smaller grid: larger segments
     const int64_t nchunks64 = (icp->nq + 63) / 64;
     icp->fb_seg = ((nchunks64 + nwaves_l - 1) / nwaves_l) * 64;
+    // tile engine: two workgroups per CU (LDS-bound), each a contiguous range of query bricks
+    icp->nb_tile = (int)std::max<int64_t>(1, std::min<int64_t>(icp->nbk, (int64_t)dev_cus * 2));
+    icp->engine_tile = PCP_ICP_TILE_DEFAULT;
+    if (const char* eg = std::getenv("PCP_ICP_ENGINE")) icp->engine_tile = std::strcmp(eg, "tile") == 0 ? 1 : std::strcmp(eg, "cache") == 0 ? 0 : icp->engine_tile;
     icp->nb_ver = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_VER_WAVES));
     const int64_t nwaves_v = (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64);
 #if PCP_VER_XCD
@@ -2162,10 +2742,14 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_off, (size_t)icp->nseg_v + 1);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->svc, icp->nq + 1);
 
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb, (size_t)nwaves * icp->fb_seg + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_count, (size_t)nwaves);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_off, (size_t)nwaves + 1);
+    // fallback segments: the octant pass's or the tile engine's, whichever needs more
+    const int64_t nseg_t = icp->nb_tile;  // the tile engine's segments sit at their query range
+    const int64_t fb_cap = std::max<int64_t>(nwaves * icp->fb_seg, icp->nq);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb, (size_t)fb_cap + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_count, (size_t)std::max<int64_t>(nwaves, nseg_t));
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_off, (size_t)std::max<int64_t>(nwaves, nseg_t) + 1);
     if (!rc) rc = pcp::dmalloc(ctx, &icp->fbc, icp->nq + 1);
+    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_base, (size_t)icp->nb_tile);
     if (!rc && (pcp::event_get(ctx, &icp->ev0) != hipSuccess || pcp::event_get(ctx, &icp->ev1) != hipSuccess ||
                 pcp::event_get(ctx, &icp->ev_mid) != hipSuccess || pcp::event_get(ctx, &icp->ev_ver) != hipSuccess))
         rc = pcp::set_error(ctx, PCP_ERR_HIP, "hipEventCreate failed");
@@ -2215,6 +2799,8 @@ int pcp_icp_destroy(pcp_icp* icp) {
     pcp::dfree(icp->owner, icp->fb_count);
     pcp::dfree(icp->owner, icp->fb_off);
     pcp::dfree(icp->owner, icp->fbc);
+    pcp::dfree(icp->owner, icp->bstart);
+    pcp::dfree(icp->owner, icp->fb_base);
     pcp::dfree(icp->owner, icp->pose_dev);
     pcp::event_put(icp->owner, icp->ev0);
     pcp::event_put(icp->owner, icp->ev1);
@@ -2255,7 +2841,15 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
         (void)hipEventElapsedTime(&mv, icp->ev0, icp->ev_ver);
         std::fprintf(stderr, "[pcp icp dbg=%d] verify %.4f ms  octant %.4f ms  fallback %.4f ms  searched %u  "
                      "n_fallback %u\n", icp->dbg, mv, m1 - mv, ms - m1, nsv, icp->last_fallback);
-        if (icp->dbgcnt) {
+        if (icp->dbgcnt && icp->engine_tile && icp->bstart) {
+            unsigned long long c[32];
+            PCP_HIP(ctx, hipMemcpy(c, icp->dbgcnt, sizeof(c), hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "[pcp icp tile] bricks %llu whole %llu | rounds staged alone %llu failed %llu | settled octant %llu "
+                         "3x3x3 %llu | fallback staged %llu unstaged %llu outside %llu | no-corr outside %llu | "
+                         "points/staging %.1f rows/staging %.1f stagings %llu | octant trip/wave %.1f waves %llu\n",
+                         c[0], c[1], c[2], c[3], c[24], c[25], c[26], c[27], c[28], c[29], (double)c[10] / (double)(c[11] ? c[11] : 1),
+                         (double)c[14] / (double)(c[11] ? c[11] : 1), c[11], (double)c[12] / (double)(c[13] ? c[13] : 1), c[13]);
+        } else if (icp->dbgcnt) {
             unsigned long long c[32];
             PCP_HIP(ctx, hipMemcpy(c, icp->dbgcnt, sizeof(c), hipMemcpyDeviceToHost));
             std::fprintf(stderr, "[pcp icp dbg] octant candidates/query %.2f  wave max list/chunk %.2f  chunks %llu (compare-swap %llu)  "

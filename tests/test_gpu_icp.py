@@ -58,10 +58,76 @@ def test_correspondence_bit_exact(ctx, cell):
         assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * scale)
 
 
-def test_verify_pass_exact_over_registration(ctx):
+@pytest.mark.parametrize("engine", ["tile", "cache"])
+def test_registration_exact_every_iteration(ctx, engine, monkeypatch):
+    """Both engines over a registration: correspondences bit-exact and accumulators equal to the
+    oracle's direct sums at every iteration (the LDS-tiled streaming search, the default, and
+    the cached verify / octant / ring passes, PCP_ICP_ENGINE=cache)."""
+    monkeypatch.setenv("PCP_ICP_ENGINE", engine)
+    from pointcloudprocess_amd import ops, synth
+    T_true = synth.rigid()
+    tgt, q = _pair(250_000, 41, T_true)
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+    icp = ops.ICP(index, q.to(ctx.device))
+    oi = ora.F32Index(tgt.numpy())
+    T = np.eye(4)
+    for it in range(10):
+        acc, ci, cd = icp.step(T, 0.25, corr=True)
+        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+        ei, ed = oi.correspond(q.numpy(), R, t, 0.25)
+        gi = ci.cpu().numpy()
+        assert np.array_equal(gi, ei), f"iter {it}: {(gi != ei).sum()} mismatching correspondences"
+        assert np.array_equal(cd.cpu().numpy()[ei >= 0], ed[ei >= 0])
+        gacc = acc.cpu().numpy().copy()
+        eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
+        assert gacc[0] == eacc[0]
+        scale = np.abs(eacc[:23]).max()
+        assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * scale), f"iter {it}"
+        rc, dT = ops.icp_solve(gacc)
+        assert rc == 0
+        T = dT @ T
+    icp.close()
+    index.close()
+
+
+@pytest.mark.parametrize("cell,per_cell", [(0.5, 40.0), (0.5, 1500.0)])
+def test_tile_engine_dense_cells(ctx, cell, per_cell, monkeypatch):
+    """Crowded cells: octant lists over 256 (the compare-swap top 3), bricks staged per 256-query
+    round, and (1500 per cell) boxes no round can hold, whose queries all take the exact fallback."""
+    from pointcloudprocess_amd import ops
+    monkeypatch.setenv("PCP_ICP_ENGINE", "tile")
+    rng = np.random.default_rng(7)
+    side = 4.0 if per_cell > 100 else 10.0
+    n = int(per_cell * (side / cell) ** 3)
+    tgt = rng.uniform(0, side, (n, 3)).astype(np.float32)
+    q = rng.uniform(-0.2, side + 0.2, (min(n, 150_000), 3)).astype(np.float32)
+    index = ops.GridIndex(ctx, torch.from_numpy(tgt).to(ctx.device), cell_size=cell)
+    icp = ops.ICP(index, torch.from_numpy(q).to(ctx.device))
+    oi = ora.F32Index(tgt)
+    for T in (np.eye(4), _small_motion()):
+        acc, ci, cd = icp.step(T, 0.25, corr=True)
+        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+        ei, ed = oi.correspond(q, R, t, 0.25)
+        assert np.array_equal(ci.cpu().numpy(), ei)
+        assert np.array_equal(cd.cpu().numpy()[ei >= 0], ed[ei >= 0])
+        eacc = ora.icp_accumulate(tgt, q, R, t, ei, ed)
+        gacc = acc.cpu().numpy()
+        assert gacc[0] == eacc[0]
+        assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * np.abs(eacc[:23]).max())
+    icp.close()
+    index.close()
+
+
+def _small_motion():
+    from pointcloudprocess_amd import synth
+    return synth.rigid(0.2, -0.1, 0.1, (0.03, -0.02, 0.01))
+
+
+def test_verify_pass_exact_over_registration(ctx, monkeypatch):
     # The verify pass settles a query from its previous winner and lower bound (triangle
     # inequality); it must return exactly what an exhaustive search returns, at every
     # iteration of a registration, on a repeated pose, and after a jump back to the start.
+    monkeypatch.setenv("PCP_ICP_ENGINE", "cache")
     from pointcloudprocess_amd import ops, synth
     T_true = synth.rigid()
     tgt, q = _pair(200_000, 31, T_true)
@@ -313,6 +379,7 @@ def test_octant_lane_groups_exact(ctx, gs, monkeypatch):
     the oracle's correspondences over a registration, on lattice ties and a dense cluster."""
     from pointcloudprocess_amd import ops, synth
     monkeypatch.setenv("PCP_OCT_G", gs)
+    monkeypatch.setenv("PCP_ICP_ENGINE", "cache")
     T_true = synth.rigid()
     tgt, q = _pair(120_000, 51, T_true)
     rng = np.random.default_rng(52)
