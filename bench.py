@@ -24,7 +24,7 @@ torch.distributed.run from a parent that never touches the GPU):
   --mode weak     WEAK scaling: each rank registers its own 50M-vs-50M tile.
 At N > 1 the line also carries the two other modes under "alt_modes" (--no-alt skips them).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode slab|sharded|weak] [--n 50000000]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode slab|sharded|weak] [--n|--points 50000000]
 
 The other BASELINE.json configs print the same JSON contract with --config (one step = one
 pass of that config's hot path over one batch; every rank runs its own batch, so N > 1 is weak
@@ -62,7 +62,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--mode", choices=("slab", "sharded", "weak"), default="slab")
-    ap.add_argument("--n", type=int, default=50_000_000, help="points per cloud (per GPU in weak mode)")
+    ap.add_argument("--n", "--points", dest="n", type=int, default=50_000_000,
+                    help="points per cloud (per GPU in weak mode); spell it --points under "
+                         "torch.distributed.run, whose parser rejects the ambiguous prefix --n")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rmax", type=float, default=0.25)
     ap.add_argument("--cell", type=float, default=0.12, help="ICP target grid cell (m); swept 0.1-0.16, 0.12 best")
@@ -83,7 +85,9 @@ def launch(args):
     port = s.getsockname()[1]
     s.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    # torch.distributed.run's parser rejects "--n" (ambiguous prefix of its own options)
+    cmd += ["--points" if a == "--n" else "--points=" + a[4:] if a.startswith("--n=") else a for a in sys.argv[1:]]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.call(cmd, env=env)
 
@@ -211,12 +215,20 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch(args)
 
+    import faulthandler
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
+    from pointcloudprocess_amd import _lib
     from pointcloudprocess_amd import distributed as D
     from pointcloudprocess_amd import ops, synth
+
+    # a fatal signal prints the Python stack (faulthandler) and, first, the faulting native
+    # library and frames (libpcp's dladdr report, which then chains to faulthandler)
+    faulthandler.enable()
+    _lib.load().pcp_fault_report_install()
 
     if args.config != "C4":
         import bench_configs  # the other BASELINE.json configs (same JSON contract)

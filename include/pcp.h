@@ -73,6 +73,10 @@ int         pcp_ctx_set_stream(pcp_ctx* ctx, void* stream);
 void*       pcp_ctx_stream(pcp_ctx* ctx);
 const char* pcp_last_error(const pcp_ctx* ctx);
 int         pcp_sync(pcp_ctx* ctx);
+/* Diagnostics: on SIGSEGV/SIGBUS/SIGILL/SIGFPE/SIGABRT print the faulting library (dladdr) and
+ * native frames to stderr, then chain to the previously installed handler (no reference
+ * counterpart; the reference process has no fault reporting). */
+int         pcp_fault_report_install(void);
 
 int pcp_malloc(pcp_ctx* ctx, void** dev_ptr, size_t bytes);
 int pcp_free(pcp_ctx* ctx, void* dev_ptr);

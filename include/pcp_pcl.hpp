@@ -19,20 +19,28 @@
 //
 // Device: all calls run on one process-wide pcp context (device PCP_DEVICE env or 0, the
 // device's default stream).  const searches may be called concurrently from OpenMP threads
-// (calculate_feature.cpp:216-233): the shim serialises them on the context mutex.  The batch
-// methods (nearestKSearchBatch / radiusSearchBatch / normals) are the fast path; the
-// per-point overloads keep the reference's call sites compiling and correct.
+// (calculate_feature.cpp:216-233): per-point nearestKSearch / radiusSearch calls on one tree
+// are coalesced (detail::Combiner): whichever caller finds no batch running takes every
+// pending request and runs them as one launch per distinct k (or radius), so T threads cost
+// about one launch per T queries.  The batch methods (nearestKSearchBatch /
+// radiusSearchBatch / normals) remain the fast path.
 // Non-zero pcp status -> the reference's visible behaviour: empty results for searches,
 // PCLException for VoxelGrid, err = -1 for ICP (SURVEY.md §8(b) "Errors").
 #ifndef PCP_PCL_HPP
 #define PCP_PCL_HPP
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <exception>
+#include <map>
 #include <memory>
 #include <mutex>
+#include <utility>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -236,6 +244,60 @@ inline std::vector<double> pack_xyz(const std::vector<PointT>& q) {
     return v;
 }
 
+// Flat combining of concurrent single requests: submit() enqueues r; a caller that finds no
+// batch running becomes the combiner, takes every pending request (its own included) and runs
+// them with run(batch); others wait and take over if theirs is still pending when that batch
+// ends.  The combiner first waits up to kWindowUs for as many requests as the recent batches
+// held (the callers released by the last batch are usually about to come back), so T busy
+// threads settle into batches of about T; the hint decays by one per batch when they stop.
+// Each request's results are written by the combiner before `done` is set under the lock; a
+// failure is re-thrown in every thread whose request was in the failed batch.
+template <class Req>
+class Combiner {
+public:
+    template <class Run>
+    void submit(Req* r, Run&& run) {
+        std::unique_lock<std::mutex> lk(m_);
+        q_.push_back(r);
+        arrive_.notify_one();
+        while (!r->done) {
+            if (busy_) {
+                cv_.wait(lk);
+                continue;
+            }
+            busy_ = true;
+            if (q_.size() < hint_)
+                arrive_.wait_for(lk, std::chrono::microseconds(kWindowUs), [&] { return q_.size() >= hint_; });
+            std::vector<Req*> batch;
+            batch.swap(q_);
+            hint_ = std::max(batch.size(), hint_ > 1 ? hint_ - 1 : (size_t)1);
+            lk.unlock();
+            std::exception_ptr err;
+            try {
+                run(batch);
+            } catch (...) {
+                err = std::current_exception();
+            }
+            lk.lock();
+            for (Req* b : batch) {
+                b->err = err;
+                b->done = true;
+            }
+            busy_ = false;
+            cv_.notify_all();
+        }
+        if (r->err) std::rethrow_exception(r->err);
+    }
+
+private:
+    static constexpr int kWindowUs = 100;
+    std::mutex m_;
+    std::condition_variable cv_, arrive_;
+    std::vector<Req*> q_;
+    bool busy_ = false;
+    size_t hint_ = 1;
+};
+
 }  // namespace detail
 
 // ------------------------------------------------------------------ K: KdTreeFLANN
@@ -285,11 +347,8 @@ public:
         const int64_t n = pcp_index_size(st_->index);
         if (k > n) k = (int)n;
         if (k == 0) return 0;
-        std::vector<int> idx;
-        std::vector<double> d2;
-        run_knn(std::vector<PointT>(1, point), k, idx, d2);
-        k_indices.assign(idx.begin(), idx.end());
-        k_sqr_distances.assign(d2.begin(), d2.end());
+        KnnReq r{{point.x, point.y, point.z}, k, &k_indices, &k_sqr_distances};
+        st_->knn_q.submit(&r, [this](std::vector<KnnReq*>& b) { run_knn_batch(b); });
         return k;
     }
     int nearestKSearch(const PointCloud<PointT>& cloud, int index, int k, std::vector<int>& k_indices,
@@ -305,8 +364,11 @@ public:
     // kd_tree.h:863-903
     int radiusSearch(const PointT& point, double radius, std::vector<int>& k_indices,
                      std::vector<double>& k_sqr_distances, unsigned int max_nn = 0) const {
-        std::vector<int64_t> off;
-        radiusSearchBatch(std::vector<PointT>(1, point), radius, off, k_indices, k_sqr_distances, max_nn);
+        k_indices.clear();
+        k_sqr_distances.clear();
+        if (!st_) return 0;
+        RadReq r{{point.x, point.y, point.z}, radius, max_nn, &k_indices, &k_sqr_distances};
+        st_->rad_q.submit(&r, [this](std::vector<RadReq*>& b) { run_radius_batch(b); });
         return (int)k_indices.size();
     }
     int radiusSearch(const PointCloud<PointT>& cloud, int index, double radius, std::vector<int>& k_indices,
@@ -351,11 +413,85 @@ public:
         k_indices.clear();
         k_sqr_distances.clear();
         if (!st_ || queries.empty()) return;
+        run_radius(detail::pack_xyz(queries), radius, max_nn, offsets, k_indices, k_sqr_distances);
+    }
+
+    // device-side handles for callers that keep their data in HBM (pcp.h)
+    const pcp_index* index() const { return st_ ? st_->index : nullptr; }
+    const double* device_cloud() const { return st_ ? (const double*)st_->cloud.ptr() : nullptr; }
+
+private:
+    // one coalesced per-point request (nearestKSearch / radiusSearch)
+    struct KnnReq {
+        double xyz[3];
+        int k;
+        std::vector<int>* idx;
+        std::vector<double>* d2;
+        bool done = false;
+        std::exception_ptr err;
+    };
+    struct RadReq {
+        double xyz[3];
+        double radius;
+        unsigned int max_nn;
+        std::vector<int>* idx;
+        std::vector<double>* d2;
+        bool done = false;
+        std::exception_ptr err;
+    };
+    struct State {
+        pcp_index* index = nullptr;
+        detail::DevBuf cloud, indices;
+        detail::Combiner<KnnReq> knn_q;
+        detail::Combiner<RadReq> rad_q;
+        detail::DevBuf sq, scnt, soff, soi, sod;  // search scratch (grow-only, device mutex held)
+        ~State() {
+            if (index) pcp_index_destroy(index);
+        }
+    };
+    // one launch per distinct k; row r of request i -> its vectors
+    void run_knn_batch(std::vector<KnnReq*>& b) const {
+        std::map<int, std::vector<KnnReq*>> by_k;
+        for (KnnReq* r : b) by_k[r->k].push_back(r);
+        for (auto& g : by_k) {
+            const int k = g.first;
+            std::vector<double> qh(3 * g.second.size());
+            for (size_t i = 0; i < g.second.size(); i++)
+                for (int d = 0; d < 3; d++) qh[3 * i + d] = g.second[i]->xyz[d];
+            std::vector<int> idx;
+            std::vector<double> d2;
+            run_knn_xyz(qh, k, idx, d2);
+            for (size_t i = 0; i < g.second.size(); i++) {
+                g.second[i]->idx->assign(idx.begin() + i * k, idx.begin() + (i + 1) * k);
+                g.second[i]->d2->assign(d2.begin() + i * k, d2.begin() + (i + 1) * k);
+            }
+        }
+    }
+    // one launch per distinct (radius, max_nn)
+    void run_radius_batch(std::vector<RadReq*>& b) const {
+        std::map<std::pair<double, unsigned int>, std::vector<RadReq*>> by_r;
+        for (RadReq* r : b) by_r[{r->radius, r->max_nn}].push_back(r);
+        for (auto& g : by_r) {
+            std::vector<double> qh(3 * g.second.size());
+            for (size_t i = 0; i < g.second.size(); i++)
+                for (int d = 0; d < 3; d++) qh[3 * i + d] = g.second[i]->xyz[d];
+            std::vector<int64_t> off;
+            std::vector<int> idx;
+            std::vector<double> d2;
+            run_radius(qh, g.first.first, g.first.second, off, idx, d2);
+            for (size_t i = 0; i < g.second.size(); i++) {
+                g.second[i]->idx->assign(idx.begin() + off[i], idx.begin() + off[i + 1]);
+                g.second[i]->d2->assign(d2.begin() + off[i], d2.begin() + off[i + 1]);
+            }
+        }
+    }
+    void run_radius(const std::vector<double>& qh, double radius, unsigned int max_nn, std::vector<int64_t>& offsets,
+                    std::vector<int>& k_indices, std::vector<double>& k_sqr_distances) const {
         pcp_ctx* c = detail::Device::get().ctx();
         std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
-        const int64_t nq = (int64_t)queries.size();
-        std::vector<double> qh = detail::pack_xyz(queries);
-        detail::DevBuf q, cnt, off, oi, od;
+        const int64_t nq = (int64_t)(qh.size() / 3);
+        offsets.assign(nq + 1, 0);
+        detail::DevBuf &q = st_->sq, &cnt = st_->scnt, &off = st_->soff, &oi = st_->soi, &od = st_->sod;  // under the device mutex
         q.upload(qh.data(), qh.size() * sizeof(double));
         cnt.reserve(nq * sizeof(int32_t));
         off.reserve((nq + 1) * sizeof(int64_t));
@@ -375,25 +511,14 @@ public:
         oi.download(k_indices.data(), total * sizeof(int32_t));
         od.download(k_sqr_distances.data(), total * sizeof(double));
     }
-
-    // device-side handles for callers that keep their data in HBM (pcp.h)
-    const pcp_index* index() const { return st_ ? st_->index : nullptr; }
-    const double* device_cloud() const { return st_ ? (const double*)st_->cloud.ptr() : nullptr; }
-
-private:
-    struct State {
-        pcp_index* index = nullptr;
-        detail::DevBuf cloud, indices;
-        ~State() {
-            if (index) pcp_index_destroy(index);
-        }
-    };
     void run_knn(const std::vector<PointT>& queries, int k, std::vector<int>& idx, std::vector<double>& d2) const {
+        run_knn_xyz(detail::pack_xyz(queries), k, idx, d2);
+    }
+    void run_knn_xyz(const std::vector<double>& qh, int k, std::vector<int>& idx, std::vector<double>& d2) const {
         pcp_ctx* c = detail::Device::get().ctx();
         std::lock_guard<std::mutex> lk(detail::Device::get().mutex());
-        const int64_t nq = (int64_t)queries.size();
-        std::vector<double> qh = detail::pack_xyz(queries);
-        detail::DevBuf q, oi, od;
+        const int64_t nq = (int64_t)(qh.size() / 3);
+        detail::DevBuf &q = st_->sq, &oi = st_->soi, &od = st_->sod;  // under the device mutex
         q.upload(qh.data(), qh.size() * sizeof(double));
         oi.reserve(nq * k * sizeof(int32_t));
         od.reserve(nq * k * sizeof(double));

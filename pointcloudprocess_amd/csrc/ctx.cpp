@@ -1,5 +1,11 @@
 // Context, error and memory helpers of the C-ABI (host code, built by hipcc).
 #include <cstdarg>
+#include <csignal>
+#include <cstdio>
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <ucontext.h>
+#include <unistd.h>
 #include <algorithm>
 #include <cstring>
 #include <iterator>
@@ -243,3 +249,61 @@ int pcp_memset(pcp_ctx* ctx, void* dst, int value, size_t bytes) {
 }
 
 }  // extern "C"
+
+// ---- fault report: name the library (dladdr) and the native frames of a fatal signal, then
+// hand the signal to whatever handler was installed before (Python's faulthandler prints the
+// Python stack) or to the default action.  Diagnostics only; nothing here runs on a good path.
+namespace {
+constexpr int kFaultSigs[] = {SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT};
+struct sigaction g_prev[sizeof(kFaultSigs) / sizeof(kFaultSigs[0])];
+bool g_fault_installed = false;
+
+void fault_write(const char* s) { (void)!write(2, s, std::strlen(s)); }
+
+void fault_handler(int sig, siginfo_t* si, void* ucv) {
+    char buf[512];
+    void* pc = nullptr;
+#if defined(__x86_64__)
+    pc = (void*)((ucontext_t*)ucv)->uc_mcontext.gregs[REG_RIP];
+#endif
+    Dl_info di{};
+    const bool named = pc && dladdr(pc, &di) && di.dli_fname;
+    std::snprintf(buf, sizeof(buf), "[pcp fault] signal %d at address %p, pc %p in %s (%s+0x%lx)\n", sig,
+                  si ? si->si_addr : nullptr, pc, named ? di.dli_fname : "?",
+                  named && di.dli_sname ? di.dli_sname : "?",
+                  named ? (unsigned long)((char*)pc - (char*)(di.dli_sname ? di.dli_saddr : di.dli_fbase)) : 0ul);
+    fault_write(buf);
+    void* frames[48];
+    const int n = backtrace(frames, 48);
+    backtrace_symbols_fd(frames, n, 2);
+    // chain: the previous handler, else the default action
+    for (size_t k = 0; k < sizeof(kFaultSigs) / sizeof(kFaultSigs[0]); k++) {
+        if (kFaultSigs[k] != sig) continue;
+        sigaction(sig, &g_prev[k], nullptr);
+        const struct sigaction& pv = g_prev[k];
+        if ((pv.sa_flags & SA_SIGINFO) && pv.sa_sigaction) {
+            pv.sa_sigaction(sig, si, ucv);
+            return;
+        }
+        if (pv.sa_handler != SIG_DFL && pv.sa_handler != SIG_IGN && pv.sa_handler) {
+            pv.sa_handler(sig);
+            return;
+        }
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+}  // namespace
+
+extern "C" int pcp_fault_report_install(void) {
+    if (g_fault_installed) return PCP_OK;
+    for (size_t k = 0; k < sizeof(kFaultSigs) / sizeof(kFaultSigs[0]); k++) {
+        struct sigaction sa{};
+        sa.sa_sigaction = fault_handler;
+        sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+        sigemptyset(&sa.sa_mask);
+        if (sigaction(kFaultSigs[k], &sa, &g_prev[k]) != 0) return PCP_ERR_ARG;
+    }
+    g_fault_installed = true;
+    return PCP_OK;
+}

@@ -12,6 +12,9 @@
 #include <unordered_map>
 #include <vector>
 
+#include <chrono>
+#include <omp.h>
+
 #include "pcp_pcl.hpp"
 extern "C" {
 #include "../../oracle/pcp_oracle.h"
@@ -449,7 +452,66 @@ static void test_mul_frame_icp() {
     CloudGrid::instance().clear();
 }
 
+
+// Concurrent per-point searches (the reference's OpenMP loops, calculate_feature.cpp:216-233):
+// 16 threads call nearestKSearch(k = 20) / radiusSearch per point; the shim coalesces them into
+// batched launches.  Every row must equal the batch call's; throughput is printed beside a
+// single-thread per-point loop (batches of one).
+static void test_concurrent_per_point() {
+    const int n = 1000000, k = 20;
+    CloudPtr cloud = random_cloud(n, 21, 50.0);
+    KdTreeFLANN<CloudItem> tree;
+    tree.setInputCloud(cloud);
+    std::vector<int> bi;
+    std::vector<double> bd;
+    tree.nearestKSearchBatch(cloud->points, k, bi, bd);
+    long bad = 0;
+    auto t0 = std::chrono::steady_clock::now();
+#pragma omp parallel for num_threads(16) schedule(dynamic, 512) reduction(+ : bad)
+    for (int i = 0; i < n; i++) {
+        std::vector<int> ki;
+        std::vector<double> kd;
+        const int got = tree.nearestKSearch(cloud->points[i], k, ki, kd);
+        bad += got != k;
+        for (int r = 0; r < k && r < (int)ki.size(); r++) bad += ki[r] != bi[(size_t)i * k + r] || kd[r] != bd[(size_t)i * k + r];
+    }
+    const double t16 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    CHECK(bad == 0, "%ld concurrent per-point kNN mismatches", bad);
+    const int n1 = 20000;
+    t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n1; i++) {
+        std::vector<int> ki;
+        std::vector<double> kd;
+        tree.nearestKSearch(cloud->points[i], k, ki, kd);
+    }
+    const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("per-point kNN k=%d over %d pts: 16 threads coalesced %.0f queries/s (%.2f s); "
+                "1 thread %.0f queries/s\n", k, n, n / t16, t16, n1 / t1);
+    // radius, 16 threads, against the batch call
+    const int nr = 200000;
+    const double rad = 0.6;
+    std::vector<CloudItem> qs(cloud->points.begin(), cloud->points.begin() + nr);
+    std::vector<int64_t> off;
+    std::vector<int> ri;
+    std::vector<double> rd;
+    tree.radiusSearchBatch(qs, rad, off, ri, rd);
+    long rbad = 0;
+    t0 = std::chrono::steady_clock::now();
+#pragma omp parallel for num_threads(16) schedule(dynamic, 512) reduction(+ : rbad)
+    for (int i = 0; i < nr; i++) {
+        std::vector<int> ki;
+        std::vector<double> kd;
+        const int got = tree.radiusSearch(qs[i], rad, ki, kd);
+        rbad += got != (int)(off[i + 1] - off[i]);
+        for (int r = 0; r < got && off[i] + r < off[i + 1]; r++) rbad += ki[r] != ri[off[i] + r] || kd[r] != rd[off[i] + r];
+    }
+    const double tr = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    CHECK(rbad == 0, "%ld concurrent per-point radius mismatches", rbad);
+    std::printf("per-point radius r=%.1f over %d queries: 16 threads coalesced %.0f queries/s\n", rad, nr, nr / tr);
+}
+
 int main() {
+    test_concurrent_per_point();
     test_mul_frame_icp();
     test_region_growing();
     test_batched_callers();
