@@ -33,8 +33,8 @@ scaling with no collective):
   --config C2   1M-vs-1M brute-force kNN k=8 (fp32 MFMA ranking, certified fp64 re-rank)
   --config C3   10M-pt street scene: VoxelGrid leaf 0.05, then the fp64 index of the centroids
                 and calculate_feature normals k=32
-  --config C5   radius r=0.2 + normals over the fp16 cell-relative index: 25M pts per GPU (one
-                eighth of the 200M-pt scene at its density)
+  --config C5   radius r=0.2 + normals over the fp16 cell-relative index: the 200M-pt scene per
+                GPU (--c5-points)
 """
 import argparse
 import glob
@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--cpu-iters1", type=int, default=3, help="CPU baseline iterations on 1 thread")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-alt", action="store_true", help="N > 1: skip the alt_modes runs")
+    ap.add_argument("--c5-points", type=int, default=200_000_000,
+                    help="--config C5: points per GPU (the 200M-pt scene fits one GPU)")
     ap.add_argument("--config", choices=("C1", "C2", "C3", "C4", "C5"), default="C4")
     return ap.parse_args()
 

@@ -225,7 +225,7 @@ def cfg_c3(ctx, args, rank, timer):
 
 def cfg_c5(ctx, args, rank, timer):
     from pointcloudprocess_amd import ops, synth
-    n = 25_000_000
+    n = int(args.c5_points)
     side = math.sqrt(n / 1.5e6) * 40.0  # the C5 test density (1.5M pts on 40 x 40 m)
     xyz = synth.street_scene(n, 5001 + 1000 * rank, extent=(side, side), device=ctx.device)
     ktimer = Timer()
