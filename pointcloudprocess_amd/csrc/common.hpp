@@ -36,7 +36,7 @@ struct pcp_ctx {
     std::multimap<size_t, void*> free_blocks;
     std::unordered_map<void*, size_t> block_size;
     size_t cached_bytes = 0;
-    size_t cache_cap = (size_t)16 << 30;
+    size_t cache_cap = (size_t)16 << 30;  // set from the device size at create (a third of HBM)
     // lifetime: every index / ICP handle / CloudGrid made on the context holds a reference, so
     // the objects may be destroyed before OR after pcp_ctx_destroy (a garbage-collected host
     // language finalises them in any order): destroy marks the context closing, frees what no

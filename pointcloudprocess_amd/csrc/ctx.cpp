@@ -171,7 +171,10 @@ int pcp_ctx_create(int device, void* stream, pcp_ctx** out) {
     c->device = device;
     c->stream = (hipStream_t)stream;  // NULL = the device's default (null) stream
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) c->cache_cap = std::min(c->cache_cap, tot / 8);
+    // scratch cache: up to a third of HBM, so a pipeline's largest temporaries (C5's sorted-order
+    // rows at 200M points are ~52 GB) are reused across calls instead of freed and re-mapped;
+    // cache_alloc gives the cache back and retries when an allocation fails
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) c->cache_cap = tot / 3;
     *out = c;
     return PCP_OK;
 }

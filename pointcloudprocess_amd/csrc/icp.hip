@@ -834,6 +834,15 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
                 const float Dv = __uint_as_float(Dw & ~0xffu);
                 if (ok) {
                     atomicAdd(a.dbgcnt + 20, 1ull);
+#if !PCP_VER_HOT
+                    // would a one-gather first tier have settled it: the first cached point
+                    // beats the others' distances at the search pose less the motion
+                    const float qsx = qx - ex, qsy = qy - ey, qsz = qz - ez;
+                    const float s1 = sqrtf(icp_d2(qsx, qsy, qsz, p1)), s2 = sqrtf(icp_d2(qsx, qsy, qsz, p2));
+                    const float lb1 = fminf(fminf(s1, s2), __uint_as_float(Dw & ~0xffu)) * 0.99998f - delta;
+                    const float e0 = icp_d2(qx, qy, qz, p0);
+                    if (lb1 > 0.f && fminf(e0 * 1.0003f, r2m) + 1e-12f < lb1 * lb1) atomicAdd(a.dbgcnt + 31, 1ull);
+#endif
                 } else if (((a.launch - Dw) & 0xffu) >= kMaxAge) {
                     atomicAdd(a.dbgcnt + 21, 1ull);
                 } else if (Dv == 0.f) {
@@ -2617,8 +2626,11 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     hipStream_t st = ctx->stream;
     float4* qs = nullptr;
     int64_t nfin = 0;
-    int32_t* bst = nullptr;  // query bricks (dense target grids)
+    int32_t* bst = nullptr;  // query bricks (dense target grids, tile engine)
     int64_t nbk = 0;
+    int engine_tile = PCP_ICP_TILE_DEFAULT;
+    if (const char* eg = std::getenv("PCP_ICP_ENGINE"))
+        engine_tile = std::strcmp(eg, "tile") == 0 ? 1 : std::strcmp(eg, "cache") == 0 ? 0 : engine_tile;
     {
         uint32_t *k0 = nullptr, *k1 = nullptr;
         float4* r0 = nullptr;
@@ -2644,7 +2656,7 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
                 hipLaunchKernelGGL(pcp::k_first_at_least, dim3(1), dim3(1), 0, st, k1, nq,
                                    pcp::query_key_end(target->g), d_cnt);
             // the tile engine's query bricks: heads of the brick runs -> k0 (as int32)
-            const bool bricks = target->g.dense;
+            const bool bricks = target->g.dense && engine_tile;  // only the tile engine reads them
             if (!rc && e == hipSuccess && bricks) {
                 const pcp::BrickHead head{k1, pcp::query_key_end(target->g)};
                 size_t tb2 = 0;
@@ -2710,8 +2722,7 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     icp->fb_seg = ((nchunks64 + nwaves_l - 1) / nwaves_l) * 64;
     // tile engine: two workgroups per CU (LDS-bound), each a contiguous range of query bricks
     icp->nb_tile = (int)std::max<int64_t>(1, std::min<int64_t>(icp->nbk, (int64_t)dev_cus * 2));
-    icp->engine_tile = PCP_ICP_TILE_DEFAULT;
-    if (const char* eg = std::getenv("PCP_ICP_ENGINE")) icp->engine_tile = std::strcmp(eg, "tile") == 0 ? 1 : std::strcmp(eg, "cache") == 0 ? 0 : icp->engine_tile;
+    icp->engine_tile = engine_tile;
     icp->nb_ver = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_VER_WAVES));
     const int64_t nwaves_v = (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64);
 #if PCP_VER_XCD
@@ -2860,6 +2871,7 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
                          c[5], c[6]);
             std::fprintf(stderr, "[pcp icp dbg] freeze model: chunks %llu skippable %llu (searched lanes in them %llu) "
                          "refrozen with slack>0 %llu\n", c[18], c[16], c[17], c[19]);
+            std::fprintf(stderr, "[pcp icp dbg] verify: one-gather tier would settle %llu of the settled\n", c[31]);
             std::fprintf(stderr, "[pcp icp dbg] verify: settled %llu  searched: aged %llu  fallback-reset(D=0) %llu  "
                          "d_win/D <.5 %llu <.75 %llu <1 %llu >=1 %llu | delta/D <.1 %llu <.25 %llu <.5 %llu >=.5 %llu\n",
                          c[20], c[21], c[22], c[23], c[24], c[25], c[26], c[27], c[28], c[29], c[30]);
