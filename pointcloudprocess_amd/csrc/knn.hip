@@ -822,27 +822,51 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
         const int64_t s = order[valid ? c * 64 + lane : c * 64];  // a sorted position
         const double4 q = pts[s];
         const int cx = cell_i<double>(g, q.x, 0), cy = cell_i<double>(g, q.y, 1), cz = cell_i<double>(g, q.z, 2);
-        // split the wave into G groups (1, 2 or 4) so that every group's box fits the LDS list
-        int G = 1;
-        bool fits = false;
-        for (; G <= 4; G *= 2) {
-            fits = true;
-            for (int gi = 0; gi < G && fits; gi++) {
-                const TileBox b = tile_box(g, cx, cy, cz, lane / (64 / G) == gi, R, lane, s_rs, s_rb, false);
-                fits = b.total <= (uint32_t)kTileCap;
+        // Groups of lanes, each staged and scanned on its own: the whole wave when its box fits
+        // the LDS list; else the runs of lanes in one query brick (the wave's queries are in
+        // brick order, so a wave that crosses into a distant brick -- the next row of bricks --
+        // splits there), cut to at most 16 lanes if a run still does not fit.  A group whose box
+        // does not fit even then takes the exact search.
+        int grp = 0, G = 1;
+        bool over = false;  // this lane's group does not fit: deferred
+        if (tile_box(g, cx, cy, cz, valid, R, lane, s_rs, s_rb, false).total > (uint32_t)kTileCap) {
+            const int nbx = (g.n[0] + 7) >> kTileBrick, nby = (g.n[1] + 7) >> kTileBrick;
+            const int bxq = clampi(cx, 0, g.n[0] - 1) >> kTileBrick, byq = clampi(cy, 0, g.n[1] - 1) >> kTileBrick,
+                      bzq = clampi(cz, 0, g.n[2] - 1) >> kTileBrick;
+            const uint32_t bid = (uint32_t)(((int64_t)bzq * nby + byq) * nbx + bxq);
+            const uint32_t prev = (uint32_t)__shfl_up((int)bid, 1, 64);
+            const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
+            const uint64_t heads = __ballot(lane == 0 || bid != prev);
+            const int run = __popcll(heads & below) - 1;
+            const int rstart = 63 - __clzll(heads & below);
+            const int nruns = __popcll(heads);
+            for (int pass = 0; pass < 2; pass++) {
+                G = pass == 0 ? nruns : nruns * 4;
+                grp = pass == 0 ? run : run * 4 + (lane - rstart) / 16;
+                bool bad = false;
+                for (int gi = 0; gi < G; gi++) {
+                    const bool in = valid && grp == gi;
+                    if (!__ballot(in)) continue;
+                    const TileBox b = tile_box(g, cx, cy, cz, in, R, lane, s_rs, s_rb, false);
+                    if (b.total > (uint32_t)kTileCap) {
+                        bad = true;
+                        over = over || grp == gi;
+                    }
+                }
+                if (!bad) break;
+                if (pass == 0) over = false;
             }
-            if (fits) break;
         }
-        if (!fits) {  // the whole wave takes the exact search
+        if (over) {  // this lane's group takes the exact search
             if (valid) defer(far, s);
-            if (stats && lane == 0) atomicAdd(stats + 1, 64ull);
-            continue;
+            if (stats) atomicAdd(stats + 1, 1ull);
         }
         if (stats && lane == 0 && G > 1) atomicAdd(stats + 3, (unsigned long long)G);
         for (int gi = 0; gi < G; gi++) {
-            const bool mine = lane / (64 / G) == gi;
+            const bool mine = grp == gi && !over;
+            if (!__ballot(mine && valid)) continue;  // an empty or deferred group
             wave_lds_fence();  // the previous group's readers are done with the lists
-            const TileBox b = tile_box(g, cx, cy, cz, mine, R, lane, s_rs, s_rb, true);
+            const TileBox b = tile_box(g, cx, cy, cz, mine && valid, R, lane, s_rs, s_rb, true);
             const uint32_t total = b.total;
             wave_lds_fence();
             // 14-bit fixed point relative to the box corner, one step for all three axes
