@@ -73,6 +73,7 @@ struct pcp_icp {
     int oct_g_first = 1;          // lanes per query of the octant pass: first launch (all queries)
     int oct_g_list = PCP_OCT_GLIST;  // ... and the verify pass's search lists (PCP_OCT_G=first,list)
     int ring_g = 0;               // lanes per query of the fallback pass (env PCP_RING_LANES), 0 = by length
+    int ver_dense = 0;            // verify: whole-chunk search threshold (PCP_VER_DENSE, env PCP_VER_DENSE)
     unsigned long long* dbgcnt = nullptr;  // kDbgCount: [candidates, rows, queries]
     uint2* dbgfz = nullptr;       // kDbgCount: per 64-query chunk {slack bits, launch} (freeze model)
     double last_ms = 0.0;
@@ -140,6 +141,7 @@ struct IcpArgs {
     int dbg;            // ablation flags (PCP_ICP_ABLATE, profiling builds of the bench only)
     int oct_g;          // octant pass lanes per query: 1, 2, 4, 8, or 0 = by the list's density
     int ring_g;         // fallback pass lanes per query: 1, 2, 4, 8, or 0 = PCP_RING_G / by length
+    int ver_dense;      // verify: a 64-query chunk with at least this many failures is searched whole (0: off)
     const float* pose;  // device poses (current, previous: 24 floats) overriding R/t, Rp/tq, or null
     unsigned long long* dbgcnt;  // kDbgCount counters, or null
     uint2* dbgfz;       // kDbgCount: chunk freeze model state
@@ -805,6 +807,10 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             const float thr = fminf(m * 1.0003f, r2m);
             bool ok = valid && !tie && ((a.launch - Dw) & 0xffu) < kMaxAge && lb > 0.f && thr + 1e-12f < lb * lb;
             ok = ok && !(a.dbg & kDbgNoVerify);
+            // a chunk where many queries fail is searched whole: the search list then holds runs
+            // of 64 neighbouring queries, which the search pass scans at its dense cost (the
+            // lanes share candidate lines), and the chunk's caches are all refreshed
+            if (a.ver_dense && (int)__popcll(__ballot(valid && !ok)) >= a.ver_dense) ok = false;
             const bool srch = valid && !ok;
             const uint64_t msk = __ballot(srch);
             if (srch) {
@@ -2243,6 +2249,9 @@ __global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_
 }
 
 // the first query of each query brick (PCP_QBRICK^3 cells) in the sorted keys (finite keys only)
+#ifndef PCP_VER_DENSE  // verify: failures per 64-query chunk from which the whole chunk is searched (0: off)
+#define PCP_VER_DENSE 0
+#endif
 #ifndef PCP_ICP_TILE_DEFAULT  // dense grids: 1 = the LDS-tiled engine by default, 0 = the cached engine
 #define PCP_ICP_TILE_DEFAULT 0
 #endif
@@ -2434,6 +2443,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.nseg = (int64_t)icp->nb_fast * (kIcpBlock / 64);
     a.ring_all = a.g.dense ? 0 : 1;
     a.dbg = icp->dbg;
+    a.ver_dense = icp->ver_dense;
     a.dbgcnt = icp->dbgcnt;
     a.dbgfz = icp->dbgfz;
     double* part_v = icp->partials;
@@ -2723,6 +2733,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     // tile engine: two workgroups per CU (LDS-bound), each a contiguous range of query bricks
     icp->nb_tile = (int)std::max<int64_t>(1, std::min<int64_t>(icp->nbk, (int64_t)dev_cus * 2));
     icp->engine_tile = engine_tile;
+    icp->ver_dense = PCP_VER_DENSE;
+    if (const char* vd = std::getenv("PCP_VER_DENSE")) icp->ver_dense = std::max(0, std::min(64, std::atoi(vd)));
     icp->nb_ver = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_VER_WAVES));
     const int64_t nwaves_v = (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64);
 #if PCP_VER_XCD
