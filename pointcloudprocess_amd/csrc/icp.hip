@@ -59,8 +59,8 @@ struct pcp_icp {
     double* acc = nullptr;        // 24 (scratch for pcp_icp_run)
     int nb_fast = 0, nb_ring = 0;
     int nb_fast_l = 0;            // octant grid of the list launches (<= nb_fast)
-    int engine_tile = 1;          // dense grids: the LDS-tiled streaming search (0: the cached
-                                  // verify / octant / ring passes; env PCP_ICP_ENGINE=cache)
+    int engine_tile = 0;          // dense grids: 1 = the LDS-tiled streaming search (env
+                                  // PCP_ICP_ENGINE=tile), 0 = the cached verify / octant / ring passes
     int nb_tile = 0;
     int32_t* bstart = nullptr;    // tile engine: first sorted query of each query brick (+ nq), nbk + 1
     int64_t nbk = 0;              // query bricks
@@ -1295,7 +1295,8 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
     }
 }
 
-// ---- LDS-tiled streaming search (dense grid, the default engine)
+// ---- LDS-tiled streaming search (dense grid; opt-in PCP_ICP_ENGINE=tile, measured slower than
+// the cached engine: DESIGN.md §5.1)
 // One pass over the sorted queries per launch, no per-query state.  The queries are sorted
 // once by 8x8x8-cell brick of the target grid (pcp_icp_create); a workgroup takes whole query
 // bricks, transforms their queries, and stages in LDS every target of the box of cells
