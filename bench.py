@@ -167,9 +167,11 @@ def native_oracle():
 def cpu_baseline(args, T_true, synth):
     """The oracle's ICP (C restatement: kd-tree + OpenMP correspondences, per-thread
     accumulators), built -O3 -march=native on this host, on a bounded sample of the same
-    workload.  The kd-tree build and the iterations are timed separately; `value` is the
-    iteration rate with ALL the process's CPUs (affinity count); the 16-thread share one GPU
-    gets on this box and one core are reported beside it."""
+    workload.  The kd-tree build and the iterations are timed separately.  It runs with ALL the
+    process's CPUs (affinity count, value_all) and with the thread count the harness allots one
+    GPU (OMP_NUM_THREADS, value_share), and on one core; `value` is the faster of the first two
+    (under a cgroup CPU quota smaller than the affinity set, the all-thread run oversubscribes
+    the quota and is the slower one)."""
     import numpy as np
     ora, build = native_oracle()
     model, ncpu, naff, quota = cpu_info()
@@ -187,14 +189,16 @@ def cpu_baseline(args, T_true, synth):
     v_all, b_all, i_all = run(naff, args.iters)
     v_sh, b_sh, i_sh = run(share, args.iters) if share != naff else (v_all, b_all, i_all)
     v_1, b_1, i_1 = run(1, args.cpu_iters1)
+    best_all = v_all >= v_sh
+    v_best, c_best, i_best, b_best = (v_all, naff, i_all, b_all) if best_all else (v_sh, share, i_sh, b_sh)
     return {
-        "value": round(v_all, 3),
+        "value": round(v_best, 3),
         "unit": "Mcorrespondences/s",
-        "cores": naff,
+        "cores": c_best,
         "kind": "port",
         "sample": f"{n}-vs-{n} pts (same density, {side:.0f}x{side:.0f} m tile), {args.iters} ICP iters of "
-                  f"oracle/pcp_oracle.c ora_icp_timed on {naff} threads: iterations {i_all:.2f} s (timed, = value), "
-                  f"kd-tree build {b_all:.2f} s (not in value)",
+                  f"oracle/pcp_oracle.c ora_icp_timed on {c_best} threads (the faster of {naff} and {share}): "
+                  f"iterations {i_best:.2f} s (timed, = value), kd-tree build {b_best:.2f} s (not in value)",
         "build": build,
         "value_all": round(v_all, 3),
         "cores_all": naff,

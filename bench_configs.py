@@ -60,8 +60,13 @@ def _oracle():
 
 
 def _threads():
-    """Every CPU of the process's affinity set (the baselines' `cores`)."""
-    return len(os.sched_getaffinity(0))
+    """The baselines' `cores`: every CPU of the process's affinity set, capped at the cgroup CPU
+    quota when there is one (more threads than the quota only time-slice: on the GPU box 256
+    affinity CPUs share a 16-CPU quota, and the C4 leg measured 3x slower at 256 threads)."""
+    import bench
+    naff = len(os.sched_getaffinity(0))
+    quota = bench.cpu_info()[3]
+    return max(1, min(naff, int(quota))) if quota else naff
 
 
 def _cpu_meta(rec):
