@@ -25,13 +25,21 @@
 #define PCP_OCT_GLIST 0  // 0: by the list's density (octant_lanes)
 #endif
 
+namespace pcp {
+// a sorted query's coordinates: 12 bytes (one global_load_dwordx3 per lane)
+struct QXyz {
+    float x, y, z;
+};
+}  // namespace pcp
+
 struct pcp_icp {
     pcp_ctx* ctx = nullptr;       // the context of the last call (launches go to its stream)
     pcp_ctx* owner = nullptr;     // the creating context: owns the buffers (a lifetime reference)
     const pcp_index* target = nullptr;
     int64_t nq = 0;               // finite queries
     int64_t nq_in = 0;            // queries passed to pcp_icp_create
-    float4* q = nullptr;          // sorted queries {x,y,z,bits(original index)}
+    pcp::QXyz* q = nullptr;       // sorted queries, 12-byte xyz (the verify stream reads 12 B, not 16)
+    int32_t* qidx = nullptr;      // their original indices (read only for caller-order outputs)
     uint4* cand = nullptr;        // per sorted query: sorted-target positions of its kCache nearest targets
                                   // at its last search (~0u = empty slot); the winner is always among them
     float4* hot = nullptr;        // per sorted query (PCP_VER_HOT): 2 records {x,y,z,dlb word}, {x,y,z,0}:
@@ -110,7 +118,8 @@ constexpr int kAcc = 24;
 struct IcpArgs {
     GridDesc g;
     const float4* tp;   // sorted target points
-    const float4* q;    // sorted queries
+    const QXyz* q;      // sorted queries (xyz)
+    const int32_t* qidx;  // their original indices
     int64_t nq;
     int64_t nchunks;
     float R[9], t[3];
@@ -146,6 +155,12 @@ struct IcpArgs {
     unsigned long long* dbgcnt;  // kDbgCount counters, or null
     uint2* dbgfz;       // kDbgCount: chunk freeze model state
 };
+
+// sorted query i as {x, y, z, 0}
+__device__ __forceinline__ float4 ldq(const IcpArgs& a, int64_t i) {
+    const QXyz v = a.q[i];
+    return make_float4(v.x, v.y, v.z, 0.f);
+}
 
 // the pose as the kernels use it: from the device copy when the loop is device-resident
 __device__ __forceinline__ void load_pose(IcpArgs& a) {
@@ -687,7 +702,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     auto raw = [&](int64_t k, float4& q, float4& h0, float4& h1) {
         const int64_t i = (cstart_ + k * cstep) * 64 + lane;
         if (k < nsteps && i < a.nq) {
-            q = a.q[i];
+            q = ldq(a, i);
             h0 = a.hot[2 * i];
             h1 = a.hot[2 * i + 1];
         } else {
@@ -706,7 +721,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     auto raw = [&](int64_t k, float4& q, uint4& cd, uint32_t& D) {
         const int64_t i = (cstart_ + k * cstep) * 64 + lane;
         if (k < nsteps && i < a.nq) {
-            q = a.q[i];
+            q = ldq(a, i);
             cd = a.cand[i];
             D = PCP_CACHE3 ? cd.w : a.dlb[i];
         } else {
@@ -734,7 +749,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
         const int64_t k1 = min(k0 + (int64_t)kFlush, nsteps);
         // centre: the stretch's first query under the current pose (wave-uniform)
         float ccx, ccy, ccz;
-        xform(a, a.q[(cstart_ + k0 * cstep) * 64], ccx, ccy, ccz);
+        xform(a, ldq(a, (cstart_ + k0 * cstep) * 64), ccx, ccy, ccz);
         ccx = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccx)));
         ccy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccy)));
         ccz = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccz)));
@@ -1184,7 +1199,7 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
     float4 qn = make_float4(0.f, 0.f, 0.f, 0.f);
     if (gw * QPC + slot < n) {
         in_ = list ? (int64_t)list[gw * QPC + slot] : gw * QPC + slot;
-        qn = a.q[in_];
+        qn = ldq(a, in_);
     }
     for (int64_t c = gw; c * QPC < n; c += nwaves) {  // grid-stride (an XCD split measured slower here)
         const int64_t j = c * QPC + slot;
@@ -1193,7 +1208,7 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
         const float4 qraw = qn;
         if (j + QPC * nwaves < n) {  // prefetch the next chunk's query
             in_ = list ? (int64_t)list[j + QPC * nwaves] : j + QPC * nwaves;
-            qn = a.q[in_];
+            qn = ldq(a, in_);
         }
         float qx = 0.f, qy = 0.f, qz = 0.f, fx = 0.f, fy = 0.f, fz = 0.f, dout = 0.f;
         int bx = 0, by = 0, bz = 0;
@@ -1640,7 +1655,7 @@ struct TileQ {
 __device__ __forceinline__ TileQ tile_load_query(const IcpArgs& a, int64_t i) {
     const GridDesc& g = a.g;
     TileQ t;
-    xform(a, a.q[i], t.x, t.y, t.z);
+    xform(a, ldq(a, i), t.x, t.y, t.z);
     t.fx = cell_f<float>(g, t.x, 0);
     t.fy = cell_f<float>(g, t.y, 1);
     t.fz = cell_f<float>(g, t.z, 2);
@@ -1855,7 +1870,7 @@ __device__ __forceinline__ void ring_run(IcpArgs& a, double (*s_acc)[kAcc], cons
         int64_t i = 0;
         if (valid) {
             i = a.ring_all ? j : list[j];
-            xform(a, a.q[i], qx, qy, qz);
+            xform(a, ldq(a, i), qx, qy, qz);
             // provisional: the cache's best (refreshed by the search pass), an upper bound
             const uint4 cd = a.cand[i];
             const CacheBest cbst = cache_best(a.tp, cd, qx, qy, qz);
@@ -2006,8 +2021,8 @@ __global__ void k_scatter_corr(IcpArgs a, int32_t* idx, float* d2) {
     load_pose(a);
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.nq;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const float4 qq = a.q[i];
-        const int oq = __float_as_int(qq.w);
+        const float4 qq = ldq(a, i);
+        const int oq = a.qidx[i];
         float x, y, z;
         xform(a, qq, x, y, z);
         const CacheBest w = cache_best(a.tp, a.cand[i], x, y, z);  // the settled winner is cached
@@ -2038,8 +2053,8 @@ __global__ void k_fill_keys(uint64_t* keys, int64_t n) {
 __global__ void k_make_keys(IcpArgs a, uint32_t offset, uint64_t* keys) {
     load_pose(a);
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.nq; i += (int64_t)gridDim.x * blockDim.x) {
-        const float4 qq = a.q[i];
-        const int oq = __float_as_int(qq.w);
+        const float4 qq = ldq(a, i);
+        const int oq = a.qidx[i];
         float x, y, z;
         xform(a, qq, x, y, z);
         const CacheBest w = cache_best(a.tp, a.cand[i], x, y, z);
@@ -2050,15 +2065,16 @@ __global__ void k_make_keys(IcpArgs a, uint32_t offset, uint64_t* keys) {
 
 // accumulators over the queries whose global winner lies in [lo, hi) (this rank's shard);
 // float products are exact in fp64, so only the summation order differs from the oracle
-__global__ void __launch_bounds__(256) k_acc_keys(const float4* q, int64_t n, const uint64_t* keys, uint64_t lo,
+__global__ void __launch_bounds__(256) k_acc_keys(const QXyz* q, const int32_t* qidx, int64_t n, const uint64_t* keys,
+                                                  uint64_t lo,
                                                   uint64_t hi, const float* shard, size_t stride_f, IcpArgs a,
                                                   double* partials) {
     double acc[kAcc - 1];
 #pragma unroll
     for (int k = 0; k < kAcc - 1; k++) acc[k] = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float4 qq = q[i];
-        const uint64_t key = keys[__float_as_int(qq.w)];
+        const float4 qq = make_float4(q[i].x, q[i].y, q[i].z, 0.f);
+        const uint64_t key = keys[qidx[i]];
         if (key == kNoKey) continue;
         const uint64_t g = key & 0xffffffffull;
         if (g < lo || g >= hi) continue;
@@ -2266,6 +2282,15 @@ struct BrickHead {
     }
 };
 
+// the sorted {x, y, z, bits(index)} records -> 12-byte xyz + index arrays
+__global__ void k_split_queries(const float4* qs, int64_t n, QXyz* q, int32_t* qi) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 v = qs[i];
+        q[i] = QXyz{v.x, v.y, v.z};
+        qi[i] = __float_as_int(v.w);
+    }
+}
+
 // number of finite queries = first position of the sentinel key in the sorted keys
 // (a single-address atomic per wave costs ~9 ms at 50M queries; this costs nothing)
 __global__ void k_first_at_least(const uint32_t* sorted, int64_t n, uint32_t key, unsigned long long* out) {
@@ -2404,6 +2429,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.g = tg->g;
     a.tp = (const float4*)tg->pts;
     a.q = icp->q;
+    a.qidx = icp->qidx;
     a.nq = icp->nq;
     a.nchunks = (icp->nq + kIcpBlock - 1) / kIcpBlock;
     HostPose hp{};
@@ -2636,6 +2662,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     // sort the query set once by target-grid brick (stable radix sort, record as payload)
     hipStream_t st = ctx->stream;
     float4* qs = nullptr;
+    pcp::QXyz* q3 = nullptr;  // the sorted records split: 12-byte xyz + original index
+    int32_t* qi = nullptr;
     int64_t nfin = 0;
     int32_t* bst = nullptr;  // query bricks (dense target grids, tile engine)
     int64_t nbk = 0;
@@ -2698,13 +2726,22 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
                     rc = pcp::set_error(ctx, PCP_ERR_HIP, "query bricks");
             }
         }
+        if (!rc) rc = pcp::dmalloc(ctx, &q3, nq + 1);
+        if (!rc) rc = pcp::dmalloc(ctx, &qi, nq + 1);
+        if (!rc && nfin > 0) {
+            hipLaunchKernelGGL(pcp::k_split_queries, dim3(pcp::grid_for(nfin, 256)), dim3(256), 0, st, (const float4*)qs,
+                               nfin, q3, qi);
+            if (hipGetLastError() != hipSuccess) rc = pcp::set_error(ctx, PCP_ERR_HIP, "query split");
+        }
         pcp::dfree(ctx, k0);
         pcp::dfree(ctx, k1);
         pcp::dfree(ctx, r0);
         pcp::dfree(ctx, d_cnt);
         pcp::dfree(ctx, tmp);
+        pcp::dfree(ctx, qs);  // (stream-ordered: the cache hands it out again only to later work)
         if (rc) {
-            pcp::dfree(ctx, qs);
+            pcp::dfree(ctx, q3);
+            pcp::dfree(ctx, qi);
             pcp::dfree(ctx, bst);
             return rc;
         }
@@ -2716,7 +2753,8 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     icp->target = target;
     icp->nq = nfin;
     icp->nq_in = nq;
-    icp->q = qs;
+    icp->q = q3;
+    icp->qidx = qi;
     icp->bstart = bst;
     icp->nbk = nbk;
     int dev_cus = 256;  // one attribute query (the whole hipDeviceProp_t costs ~0.1 ms per create)
@@ -2806,6 +2844,7 @@ int pcp_icp_destroy(pcp_icp* icp) {
     if (!icp) return PCP_ERR_ARG;
     (void)hipSetDevice(icp->owner->device);
     pcp::dfree(icp->owner, icp->q);
+    pcp::dfree(icp->owner, icp->qidx);
     pcp::dfree(icp->owner, icp->partials);
     pcp::dfree(icp->owner, icp->acc);
     pcp::dfree(icp->owner, icp->cand);
@@ -2996,7 +3035,7 @@ int pcp_icp_accumulate_keys(pcp_ctx* ctx, pcp_icp* icp, const double T[16], cons
         a.t[r] = (float)T[4 * r + 3];
     }
     const int nb = (int)std::min<int64_t>(std::max<int64_t>(1, (icp->nq + 255) / 256), icp->nb_fast + icp->nb_ring);
-    hipLaunchKernelGGL(pcp::k_acc_keys, dim3(nb), dim3(256), 0, ctx->stream, icp->q, icp->nq, keys_dev,
+    hipLaunchKernelGGL(pcp::k_acc_keys, dim3(nb), dim3(256), 0, ctx->stream, icp->q, icp->qidx, icp->nq, keys_dev,
                        (uint64_t)lo, (uint64_t)hi, shard_xyz_dev, shard_stride_bytes / sizeof(float), a,
                        icp->partials);
     hipLaunchKernelGGL(pcp::k_sum_partials, dim3(1), dim3(256), 0, ctx->stream, (const double*)icp->partials, nb,
