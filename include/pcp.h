@@ -77,6 +77,9 @@ int         pcp_sync(pcp_ctx* ctx);
  * native frames to stderr, then chain to the previously installed handler (no reference
  * counterpart; the reference process has no fault reporting). */
 int         pcp_fault_report_install(void);
+/* Build provenance: SHA-1 of the sources libpcp.so was built from (csrc sources and headers,
+ * include/pcp.h, the Makefile, in sorted name order); tests compare it with the tree. */
+const char* pcp_build_id(void);
 
 int pcp_malloc(pcp_ctx* ctx, void** dev_ptr, size_t bytes);
 int pcp_free(pcp_ctx* ctx, void* dev_ptr);

@@ -98,6 +98,7 @@ SIGNATURES = [
     ("pcp_icp_last_fallback", _i32, [_vp, _P(_i64)]),
     ("pcp_icp_last_searched", _i32, [_vp, _P(_i64)]),
     ("pcp_fault_report_install", _i32, []),
+    ("pcp_build_id", C.c_char_p, []),
     ("pcp_get_rot_icp", _i32, [_vp, _vp, _i64, _i32, _vp, _i64, _i32, _P(_f64), _f32, _i32, _i32,
                                _f64, _P(_f32)]),
 ]

@@ -10,7 +10,7 @@ cd "${SRC:-$root/pointcloudprocess_amd/csrc}"  # SRC: another checkout, e.g. a g
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-result -Wno-unused-value -munsafe-fp-atomics"
 objs=()
 for f in *.hip *.cpp; do
-  /opt/rocm/bin/hipcc $FLAGS "$@" -x hip -c "$f" -o "$out/obj/$f.o" &
+  /opt/rocm/bin/hipcc $FLAGS -DPCP_SRC_SHA='"variant"' "$@" -x hip -c "$f" -o "$out/obj/$f.o" &
   objs+=("$out/obj/$f.o")
 done
 wait
