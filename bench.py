@@ -428,6 +428,7 @@ def main():
                 "fallback_frac": round(r["fallback_frac"], 5),
             },
             "alt_modes": alt or None,
+            "build_id": _lib.load().pcp_build_id().decode(),  # SHA-1 of the libpcp sources (provenance)
             "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(args, T_true, synth),
         }
         print(json.dumps(line), flush=True)

@@ -327,6 +327,7 @@ def main(args):
         "config": {"workload": info["workload"], "parallelism": f"x{world} independent batches, no collective"},
         "device_ms_per_step": round(timer.avg, 3),
         "roofline": roof(timer.avg) if roof else None,
+        "build_id": ctx.lib.pcp_build_id().decode(),  # SHA-1 of the libpcp sources (provenance)
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
