@@ -59,14 +59,27 @@ def _oracle():
     return _ORA["ora"]
 
 
-def _threads():
-    """The baselines' `cores`: every CPU of the process's affinity set, capped at the cgroup CPU
-    quota when there is one (more threads than the quota only time-slice: on the GPU box 256
-    affinity CPUs share a 16-CPU quota, and the C4 leg measured 3x slower at 256 threads)."""
+def _thread_options():
+    """Thread counts the CPU legs try: every CPU of the process's affinity set, and that count
+    capped at the cgroup CPU quota when there is one.  Which is faster depends on the leg (on
+    the GPU box, 256 affinity CPUs share a 16-CPU quota: the C4 leg ran 3x slower at 256
+    threads, the brute-force C2 leg 2x faster), so each leg reports the faster."""
     import bench
     naff = len(os.sched_getaffinity(0))
     quota = bench.cpu_info()[3]
-    return max(1, min(naff, int(quota))) if quota else naff
+    cap = max(1, min(naff, int(quota))) if quota else naff
+    return sorted({cap, naff})
+
+
+def _fastest(run):
+    """(seconds, threads, {threads: seconds}) of run(nthreads) over _thread_options()."""
+    times = {}
+    for th in _thread_options():
+        t0 = time.perf_counter()
+        run(th)
+        times[th] = time.perf_counter() - t0
+    th = min(times, key=times.get)
+    return times[th], th, {k: round(v, 3) for k, v in times.items()}
 
 
 def _cpu_meta(rec):
@@ -133,13 +146,14 @@ def cfg_c1(ctx, args, rank, timer):
         ora = _oracle()
         host = ops.cloud_to_host(cloud)
         qh = q.cpu().numpy()
-        t0 = time.perf_counter()
-        vox, _ = ora.voxel_filter(host, 0.1)
-        vx = np.stack([vox["x"], vox["y"], vox["z"]], 1)
-        ora.KdTree(vx).knn(qh, 1, nthreads=_threads())
-        dt = time.perf_counter() - t0
-        return {"value": round(n / dt / 1e6, 3), "unit": "Mpoints/s", "cores": _threads(), "kind": "port",
-                "sample": "the whole C1 workload: oracle voxel filter (1 thread) + kd-tree build + 1-NN (OpenMP)"}
+        def run(th):
+            vox, _ = ora.voxel_filter(host, 0.1)
+            vx = np.stack([vox["x"], vox["y"], vox["z"]], 1)
+            ora.KdTree(vx).knn(qh, 1, nthreads=th)
+        dt, th, tried = _fastest(run)
+        return {"value": round(n / dt / 1e6, 3), "unit": "Mpoints/s", "cores": th, "kind": "port",
+                "sample": f"the whole C1 workload: oracle voxel filter (1 thread) + kd-tree build + 1-NN (OpenMP, "
+                          f"the faster of {sorted(tried)} threads: seconds {tried})"}
     return step, info, cpu
 
 
@@ -169,12 +183,11 @@ def cfg_c2(ctx, args, rank, timer):
         t0 = time.perf_counter()
         tree = ora.KdTree(th)
         tb = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        tree.knn(qs, 8, nthreads=_threads())
-        dt = time.perf_counter() - t0
-        return {"value": round(len(qs) / dt / 1e6, 3), "unit": "Mqueries/s", "cores": _threads(), "kind": "port",
+        dt, th, tried = _fastest(lambda th: tree.knn(qs, 8, nthreads=th))
+        return {"value": round(len(qs) / dt / 1e6, 3), "unit": "Mqueries/s", "cores": th, "kind": "port",
                 "sample": f"oracle kd-tree (FLANN contract) over the same 1M targets: {len(qs)} queries k=8 in "
-                          f"{dt:.2f} s (build {tb:.2f} s, not in value)"}
+                          f"{dt:.2f} s on {th} threads (seconds per thread count {tried}; build {tb:.2f} s, not in "
+                          f"value)"}
     return step, info, cpu
 
 
@@ -219,12 +232,11 @@ def cfg_c3(ctx, args, rank, timer):
         vox, _ = ora.voxel_filter(host, 0.05)
         tv = time.perf_counter() - t0
         vx = np.stack([vox["x"], vox["y"], vox["z"]], 1)
-        t0 = time.perf_counter()
-        ora.normals_knn(vx, 32, nthreads=_threads())
-        tn = time.perf_counter() - t0
-        return {"value": round(s / (tv + tn) / 1e6, 3), "unit": "Mpoints/s", "cores": _threads(), "kind": "port",
+        tn, th, tried = _fastest(lambda th: ora.normals_knn(vx, 32, nthreads=th))
+        return {"value": round(s / (tv + tn) / 1e6, 3), "unit": "Mpoints/s", "cores": th, "kind": "port",
                 "sample": f"the first {s} points: oracle voxel filter {tv:.2f} s (1 thread) + kd-tree normals k=32 "
-                          f"over its {len(vx)} centroids {tn:.2f} s (OpenMP)"}
+                          f"over its {len(vx)} centroids {tn:.2f} s (OpenMP on {th} threads; seconds per thread "
+                          f"count {tried})"}
     return step, info, cpu
 
 
@@ -271,14 +283,15 @@ def cfg_c5(ctx, args, rank, timer):
         tree = ora.KdTree(xh)
         tb = time.perf_counter() - t0
         qs = np.sort(np.random.default_rng(5).choice(ns, s, replace=False)).astype(np.int32)
-        t0 = time.perf_counter()
-        cnt, _ = tree.radius_normals(qs, 0.2, nthreads=_threads())
-        dt = time.perf_counter() - t0
-        return {"value": round(s / dt / 1e6, 4), "unit": "Mpoints/s", "cores": _threads(), "kind": "port",
+        res = {}
+        dt, th, tried = _fastest(lambda th: res.update(c=tree.radius_normals(qs, 0.2, nthreads=th)[0]))
+        cnt = res["c"]
+        return {"value": round(s / dt / 1e6, 4), "unit": "Mpoints/s", "cores": th, "kind": "port",
                 "sample": f"{s} random points of a {ns}-pt tile of the same scene at the same density "
                           f"({side_s:.0f} x {side_s:.0f} m): oracle kd-tree radiusSearch r=0.2 (sorted rows) + fp64 F1 "
-                          f"per point, OpenMP over points (ora_radius_normals_batch), nbar {cnt.mean():.1f}, in "
-                          f"{dt:.2f} s; kd-tree build {tb:.1f} s not in value"}
+                          f"per point, OpenMP over points (ora_radius_normals_batch) on {th} threads (seconds per "
+                          f"thread count {tried}), nbar {cnt.mean():.1f}, in {dt:.2f} s; kd-tree build {tb:.1f} s "
+                          f"not in value"}
     return step, info, cpu
 
 
