@@ -31,3 +31,11 @@ def test_shim_parity_driver():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
     print(r.stdout[-4000:], r.stderr[-2000:])
     assert r.returncode == 0 and "all checks passed" in r.stdout
+
+
+def test_shim_request_combiner_host():
+    """The combiner that merges concurrent per-point searches (host logic, no GPU)."""
+    subprocess.check_call(["make", "-s", "-C", CPP, "_build/combiner_test"])
+    r = subprocess.run([os.path.join(CPP, "_build", "combiner_test")], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0 and "all checks passed" in r.stdout
