@@ -148,5 +148,12 @@ struct pcp_index {
     int is_h16 = 0;
     uint2* h16 = nullptr;
     uint32_t* cell = nullptr;
+    // the last radius count's sorted-order row lengths (padded to 4) and caller -> sorted
+    // position, for the fill that follows it (same radius and n_owned)
+    int32_t* h16_cnt_s = nullptr;
+    int32_t* h16_inv = nullptr;
+    int64_t h16_inv_cap = 0;
+    float h16_last_r = -1.f;
+    int64_t h16_last_owned = -1;
     pcp_ctx* owner = nullptr;
 };

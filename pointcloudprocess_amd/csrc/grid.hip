@@ -624,6 +624,8 @@ int pcp_index_destroy(pcp_index* ix) {
     pcp::dfree(ix->owner, ix->pos_of_j);
     pcp::dfree(ix->owner, ix->h16);
     pcp::dfree(ix->owner, ix->cell);
+    pcp::dfree(ix->owner, ix->h16_cnt_s);
+    pcp::dfree(ix->owner, ix->h16_inv);
     pcp_ctx* owner = ix->owner;
     delete ix;
     pcp::ctx_release(owner);

@@ -109,7 +109,9 @@ __global__ __launch_bounds__(kB) void k_h16_rows_to_caller(const int32_t* inv, i
         const int64_t c = w * 64 + lane;
         if (lane < rows) {
             s_dst[wid][lane] = offsets[c];
-            s_src[wid][lane] = soff[inv[c]];
+            // an empty row (e.g. a caller point the build dropped as non-finite) has no staged
+            // row and no inverse entry: never read inv for it
+            s_src[wid][lane] = offsets[c + 1] > offsets[c] ? soff[inv[c]] : 0;
         }
         if (lane == 0) s_dst[wid][rows] = offsets[w * 64 + rows];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -134,15 +136,22 @@ __global__ __launch_bounds__(kB) void k_h16_rows_to_caller(const int32_t* inv, i
     }
 }
 
+// count pass (FILL = false): count[caller] = the row length; with cnt_s, also the row length
+// padded to 4 at the sorted position (0 for points that are not queries) and inv[caller] = s,
+// which the fill pass then takes instead of gathering them back from the caller offsets
 template <bool FILL>
 __global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, const int64_t* __restrict__ offsets,
                                                    const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
-                                                   pcp_plane* __restrict__ out_nrm) {
+                                                   pcp_plane* __restrict__ out_nrm, int32_t* __restrict__ cnt_s = nullptr,
+                                                   int32_t* __restrict__ inv = nullptr) {
     const GridDesc& g = a.g;
     const uint2* __restrict__ rec = a.rec;
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < a.n; s += (int64_t)gridDim.x * blockDim.x) {
         const int32_t caller = a.mapping[s];
-        if (caller >= a.n_owned) continue;
+        if (caller >= a.n_owned) {
+            if (!FILL && cnt_s) cnt_s[s] = 0;
+            continue;
+        }
         const uint2 qr = a.rec[s];
         const float qx = h_lo(qr.x), qy = h_hi(qr.x), qz = h_lo(qr.y);
         const uint32_t cid = a.cell[s];
@@ -223,6 +232,10 @@ __global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, co
         if (!PCP_H16_NOSTORE && FILL && (cnt & 3u)) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
         if (!FILL) {
             count[caller] = (int32_t)cnt;
+            if (cnt_s) {
+                cnt_s[s] = (int32_t)((cnt + 3u) & ~3u);  // 16-byte aligned staging rows
+                inv[caller] = (int32_t)s;
+            }
         } else if (out_nrm) {
             pcp_plane pl{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
             if (cnt > 0) {
@@ -317,9 +330,23 @@ int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_
     PCP_HIP(ctx, hipMemsetAsync(count_dev, 0, (size_t)n_owned * sizeof(int32_t), ctx->stream));
     if (ix->n == 0) return PCP_OK;
     const H16Args a = make_args(ix, radius, n_owned);
+    // keep the sorted-order row lengths and the inverse map for the fill of the same query set
+    pcp_index* ixm = const_cast<pcp_index*>(ix);
+    ixm->h16_last_r = -1.f;
+    if (!ixm->h16_cnt_s) PCP_TRY(dmalloc(ix->owner, &ixm->h16_cnt_s, (size_t)ix->n));
+    if (ixm->h16_inv_cap < n_owned) {
+        dfree(ix->owner, ixm->h16_inv);
+        ixm->h16_inv = nullptr;
+        ixm->h16_inv_cap = 0;
+        PCP_TRY(dmalloc(ix->owner, &ixm->h16_inv, (size_t)n_owned));
+        ixm->h16_inv_cap = n_owned;
+    }
     hipLaunchKernelGGL(k_h16_radius<false>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, count_dev,
-                       (const int64_t*)nullptr, (const int32_t*)nullptr, (int32_t*)nullptr, (pcp_plane*)nullptr);
+                       (const int64_t*)nullptr, (const int32_t*)nullptr, (int32_t*)nullptr, (pcp_plane*)nullptr,
+                       ixm->h16_cnt_s, ixm->h16_inv);
     PCP_LAUNCH_CHECK(ctx);
+    ixm->h16_last_r = radius;
+    ixm->h16_last_owned = n_owned;
     return PCP_OK;
 }
 
@@ -345,20 +372,27 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
         ~Free() { dfree(c, *a); dfree(c, *b); dfree(c, *d); dfree(c, *e); dfree(c, *f); }
     } fr{ctx, &ids, &cnt_s, &inv, &tmp, &soff};
     PCP_TRY(dmalloc(ctx, &ids, (size_t)ix->n));
-    PCP_TRY(dmalloc(ctx, &cnt_s, (size_t)ix->n));
-    PCP_TRY(dmalloc(ctx, &inv, (size_t)n_owned));
     PCP_TRY(dmalloc(ctx, &soff, (size_t)ix->n + 1));
     PCP_TRY(dmalloc(ctx, &tmp, (size_t)total + 3 * (size_t)n_owned + 4));  // rows padded to 4
     hipLaunchKernelGGL(k_h16_ids, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, (const int32_t*)ix->mapping,
                        global_id_dev, ix->n, ids);
-    hipLaunchKernelGGL(k_h16_sorted_counts, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream,
-                       (const int32_t*)ix->mapping, ix->n, n_owned, offsets_dev, cnt_s, inv);
+    // the sorted-order row lengths and the inverse map: kept by the count pass of this radius and
+    // query set, else gathered back from the caller offsets
+    const int32_t *cnt_use = ix->h16_cnt_s, *inv_use = ix->h16_inv;
+    if (!(ix->h16_cnt_s && ix->h16_last_r == radius && ix->h16_last_owned == n_owned)) {
+        PCP_TRY(dmalloc(ctx, &cnt_s, (size_t)ix->n));
+        PCP_TRY(dmalloc(ctx, &inv, (size_t)n_owned));
+        hipLaunchKernelGGL(k_h16_sorted_counts, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream,
+                           (const int32_t*)ix->mapping, ix->n, n_owned, offsets_dev, cnt_s, inv);
+        cnt_use = cnt_s;
+        inv_use = inv;
+    }
     PCP_LAUNCH_CHECK(ctx);
-    PCP_TRY(scan_i32_to_i64(ctx, cnt_s, ix->n, soff, nullptr));
+    PCP_TRY(scan_i32_to_i64(ctx, cnt_use, ix->n, soff, nullptr));
     hipLaunchKernelGGL(k_h16_radius<true>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, (int32_t*)nullptr,
                        (const int64_t*)soff, (const int32_t*)ids, tmp, normals_dev);
     hipLaunchKernelGGL(k_h16_rows_to_caller, dim3(grid_for(n_owned, kB, 1 << 16)), dim3(kB), 0, ctx->stream,
-                       (const int32_t*)inv, n_owned, (const int64_t*)soff, offsets_dev, (const int32_t*)tmp, idx_dev);
+                       inv_use, n_owned, (const int64_t*)soff, offsets_dev, (const int32_t*)tmp, idx_dev);
     PCP_LAUNCH_CHECK(ctx);
     return PCP_OK;
 }

@@ -107,3 +107,32 @@ def test_h16_slab_halo_split_matches(ctx, scene):
         bad += int((d >= R + EPS).sum())
         bad += len(set(tree.query_ball_point(x64[q], R - EPS)) - set(row.tolist()))
     assert bad == 0 and len(keys) > 10000
+
+
+def test_h16_fill_after_another_count(ctx, scene):
+    """The fill takes the sorted-order row lengths its count pass kept; after a count of another
+    radius in between it must gather them back from the offsets it is given -- same rows,
+    same normals, byte for byte."""
+    import ctypes as C
+    from pointcloudprocess_amd import ops
+    xyz = scene[:400_000]
+    ix = ops.H16Index(ctx, torch.from_numpy(xyz).to(ctx.device), cell_size=R)
+    offs, idx, nrm = ix.radius_normals(R)  # count + fill (the kept lengths)
+    n = xyz.shape[0]
+    lib = ctx.lib
+    cnt = torch.empty(n, dtype=torch.int32, device=ctx.device)
+    ctx.check(lib.pcp_h16_radius_count(ctx.h, ix.h, float(R), n, C.c_void_p(cnt.data_ptr())))
+    offs2 = torch.empty(n + 1, dtype=torch.int64, device=ctx.device)
+    total = C.c_int64()
+    ctx.check(lib.pcp_scan_counts(ctx.h, C.c_void_p(cnt.data_ptr()), n, C.c_void_p(offs2.data_ptr()), C.byref(total)))
+    cnt_b = torch.empty(n, dtype=torch.int32, device=ctx.device)  # another radius: the kept lengths change
+    ctx.check(lib.pcp_h16_radius_count(ctx.h, ix.h, float(R * 0.5), n, C.c_void_p(cnt_b.data_ptr())))
+    idx2 = torch.empty(max(total.value, 1), dtype=torch.int32, device=ctx.device)
+    nrm2 = torch.empty((n, 6), dtype=torch.float32, device=ctx.device)
+    ctx.check(lib.pcp_h16_radius_fill(ctx.h, ix.h, float(R), n, C.c_void_p(offs2.data_ptr()), None,
+                                      C.c_void_p(idx2.data_ptr()), C.c_void_p(nrm2.data_ptr())))
+    torch.cuda.synchronize()
+    assert torch.equal(offs2.cpu(), offs.cpu())
+    assert torch.equal(idx2[:total.value].cpu(), idx.cpu())
+    assert torch.equal(nrm2.cpu().view(torch.int32), nrm.cpu().view(torch.int32))
+    ix.close()
