@@ -38,6 +38,12 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_KNN_BATCH
 #define PCP_KNN_BATCH 4
 #endif
+#ifndef PCP_COOP_FLAT  // far pass: 1 = a batch's occupied-brick rows dealt over the lanes
+#define PCP_COOP_FLAT 1
+#endif
+#ifndef PCP_NORMALS_NEAR_DEFAULT  // tiled normals: 1 = the lane-per-query near pass before the far pass
+#define PCP_NORMALS_NEAR_DEFAULT 1
+#endif
 template <int K>
 struct KnnVisitor {
     static constexpr int U = K <= 16 ? PCP_KNN_BATCH : 2;
@@ -246,6 +252,10 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     farb = max(farb, max(by - (g.nb[1] - 1), -by));
     farb = max(farb, max(bz - (g.nb[2] - 1), -bz));
     const int sbmax = farb + max(g.nb[0], max(g.nb[1], g.nb[2]));
+#if PCP_COOP_FLAT
+    __shared__ int4 s_flat[kB / 64][64 * 8];  // per wave: a batch's occupied bricks {x, y, z, slot}
+    int4* const flat = s_flat[threadIdx.x >> 6];
+#endif
     // rings closer than `farb` lie wholly outside the grid (a query far away from it)
     if (tk) tk[0] = clock64();
     for (int sb = farb; sb <= sbmax; sb++) {
@@ -286,6 +296,7 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
         // bricks t = lane + 64 u: the occupancy words of a batch are loaded together (mostly
         // empty bricks around isolated queries: one dependent load each would serialise)
         constexpr int kBB = 8;
+        static_assert(kBB == 8, "s_flat holds 64 * 8 bricks per wave");
         for (int64_t base = 0; base < total; base += 64 * kBB) {  // wave-uniform trip count
             const int64_t t0 = base + lane;
             int bxs[kBB], bys[kBB], bzs[kBB];
@@ -314,6 +325,53 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
                 bxs[u] = xb; bys[u] = yb; bzs[u] = zb;
                 occ[u] = live ? g.brick[((int64_t)zb * g.nb[1] + yb) * g.nb[0] + xb] : -1;
             }
+#if PCP_COOP_FLAT
+            // The batch's occupied bricks are listed in LDS and their 16 (y, z) rows dealt
+            // round-robin over the lanes: a lane's rows are independent load chains, where the
+            // per-lane walk below serialises 16 rows per occupied brick slot.
+            uint32_t nocc = 0;
+#pragma unroll
+            for (int u = 0; u < kBB; u++) {
+                const uint64_t m = __ballot(occ[u] >= 0);
+                if (occ[u] >= 0) {
+                    const uint32_t at = nocc + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    flat[at] = make_int4(bxs[u], bys[u], bzs[u], occ[u]);
+                }
+                nocc += (uint32_t)__popcll(m);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t it = (uint32_t)lane; it < 16 * nocc; it += 64) {
+                const int4 bk = flat[it >> 4];
+                const int y = 4 * bk.y + (int)(it & 3), z = 4 * bk.z + (int)((it >> 2) & 3);
+                if (y >= g.n[1] || z >= g.n[2]) continue;
+                const double cyz2 = sq_gap(axis_gap<double>(z, cz, lz), mc) + sq_gap(axis_gap<double>(y, cy, ly), mc);
+                if (cyz2 * h2 > v.bound()) continue;
+                const bool yzin = abs(z - cz) <= kCellRings && abs(y - cy) <= kCellRings;
+                int xa = 4 * bk.x, xe = min(4 * bk.x + 3, g.n[0] - 1);
+                while (xa <= xe && (cyz2 + sq_gap(axis_gap<double>(xa, cx, lx), mc)) * h2 > v.bound()) xa++;
+                while (xe >= xa && (cyz2 + sq_gap(axis_gap<double>(xe, cx, lx), mc)) * h2 > v.bound()) xe--;
+                if (xa > xe) continue;
+                const int64_t r0 = g.dense ? dense_id(g, 0, y, z) : (int64_t)bk.w * 64 + local_of(0, y, z);
+                auto run = [&](int x0, int x1) {  // cells [x0, x1] of this row
+                    if (x0 > x1) return;
+                    const int64_t c0 = g.dense ? r0 + x0 : r0 + (x0 & 3);
+                    const uint32_t st = g.cstart[c0], en = g.cstart[c0 + (x1 - x0) + 1];
+                    if (en > st) v.visit(st, en);
+                };
+                if (yzin) {
+                    run(xa, min(xe, cx - kCellRings - 1));
+                    run(max(xa, cx + kCellRings + 1), xe);
+                } else {
+                    run(xa, xe);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next batch rewrites flat[]
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
 #pragma unroll 1
             for (int u = 0; u < kBB; u++) {
                 if (occ[u] < 0) continue;  // empty or pruned brick
@@ -351,6 +409,7 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
                     }
                 }
             }
+#endif
             // tighten the shared bound mid-shell (the exact k-th is refreshed per shell)
             if (kk <= 64) v.shared = fmin(v.shared, wave_kth_of_bests<K>(v.top, kk, lane));
         }
@@ -896,8 +955,10 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
             for (int i = 0; i <= M; i++) t[i] = kMax;
             // keys: the float bits of the integer d2 (relative precision 2^-12 after the index
             // bits, whatever the step) | list index
-            auto insert = [&](uint32_t d, uint32_t e) {
-                const uint32_t x = (__float_as_uint((float)d) & ~(uint32_t)(kTileCap - 1)) | e;
+            auto key = [&](uint32_t d, uint32_t e) {
+                return (__float_as_uint((float)d) & ~(uint32_t)(kTileCap - 1)) | e;
+            };
+            auto insert = [&](uint32_t x) {
 #pragma unroll
                 for (int i = M; i >= 1; i--) t[i] = umed3_(t[i - 1], t[i], x);
                 t[0] = min(t[0], x);
@@ -908,11 +969,11 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
 #pragma unroll
                 for (int u = 0; u < 4; u++) p[u] = s_u[e + u];
 #pragma unroll
-                for (int u = 0; u < 4; u++) insert(qd2(qxy, qz, p[u].x, (int)p[u].y), e + u);
+                for (int u = 0; u < 4; u++) insert(key(qd2(qxy, qz, p[u].x, (int)p[u].y), e + u));
             }
             for (; e < total; e++) {
                 const uint2 pp = s_u[e];
-                insert(qd2(qxy, qz, pp.x, (int)pp.y), e);
+                insert(key(qd2(qxy, qz, pp.x, (int)pp.y), e));
             }
             if (!mine) continue;  // (no wave-wide operation follows)
             // exact FLANN re-rank of the kept candidates
@@ -1353,13 +1414,20 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tb, k0, k1, v0, order, (size_t)ix->n, 0u, bits, ctx->stream));
         FarBuf fb2;  // the near pass's own deferred queries
         PCP_TRY(fb2.alloc(ctx, ix->n));
+        // the tile's uncertified queries: the lane-per-query near pass (cell rings), its own
+        // deferrals then the wave-per-query pass; or (PCP_NORMALS_NEAR=0) all of them straight
+        // to the wave-per-query pass -- a few thousand queries fill few waves one lane each
+        const char* nenv = getenv("PCP_NORMALS_NEAR");
+        const bool near_pass = nenv ? atoi(nenv) != 0 : PCP_NORMALS_NEAR_DEFAULT;
 #define LAUNCH_TILE(KV)                                                                                          \
         hipLaunchKernelGGL((k_normals_tile<KV>), dim3(nbt), dim3(64), 0, ctx->stream, ix->g, pts, ix->mapping,      \
                            ix->identity, ix->n, kk, tile_R, mc, out, n_out, fb.f, st, order);                     \
-        hipLaunchKernelGGL((k_normals<KV, false>), dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts,   \
-                           ix->mapping, ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb2.f, fb.f);       \
+        if (near_pass)                                                                                            \
+            hipLaunchKernelGGL((k_normals<KV, false>), dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g,    \
+                               pts, ix->mapping, ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb2.f, fb.f); \
         hipLaunchKernelGGL((k_normals_coop<KV>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts,            \
-                           ix->mapping, ix->identity, ix->pos_of_j, kk, mc, out, n_out, fb2.f, st ? st + 4 : nullptr)
+                           ix->mapping, ix->identity, ix->pos_of_j, kk, mc, out, n_out, near_pass ? fb2.f : fb.f,  \
+                           st ? st + 4 : nullptr)
         switch (K) {
             case 1: case 4: LAUNCH_TILE(4); break;
             case 8: LAUNCH_TILE(8); break;

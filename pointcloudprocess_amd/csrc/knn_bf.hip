@@ -40,6 +40,9 @@ constexpr int kBlock = 64 * kWaves;
 #ifndef PCP_BF_TILE
 #define PCP_BF_TILE 1024
 #endif
+#ifndef PCP_BF_SIGN  // 1: thresholds in the MFMA's C operand, sign-bit hit test; 0: compares
+#define PCP_BF_SIGN 1
+#endif
 constexpr int kTile = PCP_BF_TILE;     // targets staged in LDS per step
 constexpr int kPerThread = kTile / kBlock;
 
@@ -159,6 +162,33 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
 #pragma unroll
             for (int i = 0; i < L; i++) { ls[b][r][i] = INFINITY; lt[b][r][i] = -1; }
         }
+#if PCP_BF_SIGN
+    // The filter rides in the MFMA: C = -thr per row, so an output is negative exactly when the
+    // score is below the row's threshold (as of the MFMA's issue; thresholds only fall, so a
+    // stale one lets more through), and the common path's hit test is two ORs of the sign bits
+    // instead of four compares.  A hit re-scores its target on the VALU from the staged record
+    // and this lane's rows' -2q (the same fp32 fma chain as the MFMA's K = 4 product), so the
+    // lists never hold a score that passed through the threshold subtraction.
+    f32x4 nthr[QB];
+    float qm[QB][4][3];
+#pragma unroll
+    for (int b = 0; b < QB; b++) {
+        nthr[b] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int64_t qi = qbase + b * 16 + grp * 4 + r;
+#pragma unroll
+            for (int c3 = 0; c3 < 3; c3++) {
+                float v = 0.f;
+                if (qi < a.nq) {
+                    const double c = dptr(a.q, a.qstride, qi)[c3];
+                    v = isfinite(c) ? -2.f * (float)c : 0.f;
+                }
+                qm[b][r][c3] = v;
+            }
+        }
+    }
+#endif
     // wave-uniform fp32 score error bound E (largest |q| of the wave's queries)
     float ew;
     {
@@ -195,16 +225,23 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
         if (tt + 1 < ntiles) fetch((tt + 1) * kTile);
         const int tb = (int)(tt * kTile);
         const float* tf = (const float*)tile;
+#if !PCP_BF_SIGN
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#endif
         // software pipeline: the MFMAs of sub-tile s+1 are in flight while the scores of
         // sub-tile s are tested, so the matrix pipe never waits on the selection VALU work
         f32x4 cn[QB];
         float bnext;  // B fragment of sub-tile s+2, read from LDS a step ahead of its MFMA
+#if PCP_BF_SIGN
+#define PCP_BF_C(b) nthr[b]
+#else
+#define PCP_BF_C(b) z
+#endif
         {
             const float bf0 = tf[cls * 4 + grp];
             bnext = tf[(16 + cls) * 4 + grp];
 #pragma unroll
-            for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf0, z, 0, 0, 0);
+            for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf0, PCP_BF_C(b), 0, 0, 0);
         }
 #pragma unroll 2
         for (int sub = 0; sub < kTile / 16; sub++) {
@@ -215,9 +252,34 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
                 const float bfrag = bnext;
                 if (sub + 2 < kTile / 16) bnext = tf[((sub + 2) * 16 + cls) * 4 + grp];
 #pragma unroll
-                for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfrag, z, 0, 0, 0);
+                for (int b = 0; b < QB; b++)
+                    cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfrag, PCP_BF_C(b), 0, 0, 0);
             }
             // one combined test per step; the insertion path runs only when a lane has a hit
+#if PCP_BF_SIGN
+            uint32_t sg = 0;
+#pragma unroll
+            for (int b = 0; b < QB; b++)
+                sg |= __float_as_uint(c[b][0]) | __float_as_uint(c[b][1]) | __float_as_uint(c[b][2]) |
+                      __float_as_uint(c[b][3]);
+            if ((int32_t)sg < 0) {
+                const int tidx = tb + sub * 16 + cls;
+                const float4 p = tile[sub * 16 + cls];
+#pragma unroll
+                for (int b = 0; b < QB; b++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        if ((int32_t)__float_as_uint(c[b][r]) >= 0) continue;
+                        const float x = __fmaf_rn(qm[b][r][2], p.z, __fmaf_rn(qm[b][r][1], p.y,
+                                                  __fmaf_rn(qm[b][r][0], p.x, p.w)));
+                        if (x < thr[b][r]) {
+                            list_insert<L>(ls[b][r], lt[b][r], x, tidx);
+                            thr[b][r] = fminf(ls[b][r][L - 1], thr[b][r]);
+                            nthr[b][r] = -thr[b][r];
+                        }
+                    }
+            }
+#else
             bool hit = false;
 #pragma unroll
             for (int b = 0; b < QB; b++)
@@ -236,7 +298,9 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
                         }
                     }
             }
+#endif
         }
+#undef PCP_BF_C
         // refresh theta after tiles 1, 2, 4, 8, ... (rank of each class best in its group)
         if (use_theta && ((tt + 1) & tt) == 0) {
 #pragma unroll
@@ -255,6 +319,9 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
                     for (int o = 1; o < 16; o <<= 1) cand = fminf(cand, __shfl_xor(cand, o, 64));
                     const float t2 = cand + 2.f * ew;
                     if (cand != INFINITY) thr[b][r] = fminf(thr[b][r], t2 + fabsf(t2) * 1e-6f);
+#if PCP_BF_SIGN
+                    nthr[b][r] = -thr[b][r];
+#endif
                 }
         }
     }
@@ -421,7 +488,8 @@ int pcp_knn_bruteforce(pcp_ctx* ctx, const double* t, size_t tstride, int64_t nt
         a.kk = (int)std::min<double>((double)k, nfin);
         // 32 unit roundoffs of (|p| + |q|)^2: casts to fp32, |p|^2 in fp32 and the 4-term
         // fma chain each contribute a few
-        a.E2 = 32.0 * std::ldexp(1.0, -24);
+        // (PCP_BF_SIGN: 8 more for the threshold subtraction inside the filter's MFMA)
+        a.E2 = (PCP_BF_SIGN ? 40.0 : 32.0) * std::ldexp(1.0, -24);
         a.pmax = std::sqrt(pmax2);
         a.oidx = oidx; a.od2 = od2; a.fb = fb; a.fb_count = fbc;
         if (hipMemsetAsync(fbc, 0, sizeof(uint32_t), st) != hipSuccess) rc = set_error(ctx, PCP_ERR_HIP, "memset");
