@@ -40,6 +40,9 @@ constexpr int kBlock = 64 * kWaves;
 #ifndef PCP_BF_TILE
 #define PCP_BF_TILE 1024
 #endif
+#ifndef PCP_BF_UNROLL  // sub-tile steps per unrolled loop body
+#define PCP_BF_UNROLL 2
+#endif
 #ifndef PCP_BF_SIGN  // 1: thresholds in the MFMA's C operand, sign-bit hit test; 0: compares
 #define PCP_BF_SIGN 1
 #endif
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
 #pragma unroll
             for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf0, PCP_BF_C(b), 0, 0, 0);
         }
-#pragma unroll 2
+#pragma unroll PCP_BF_UNROLL
         for (int sub = 0; sub < kTile / 16; sub++) {
             f32x4 c[QB];
 #pragma unroll
