@@ -41,7 +41,7 @@ constexpr int kBlock = 64 * kWaves;
 #define PCP_BF_TILE 1024
 #endif
 #ifndef PCP_BF_UNROLL  // sub-tile steps per unrolled loop body
-#define PCP_BF_UNROLL 2
+#define PCP_BF_UNROLL 4
 #endif
 #ifndef PCP_BF_SIGN  // 1: thresholds in the MFMA's C operand, sign-bit hit test; 0: compares
 #define PCP_BF_SIGN 1
