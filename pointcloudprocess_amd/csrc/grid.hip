@@ -146,6 +146,31 @@ __global__ void k_brick_flag(int32_t* brick, int64_t nb) {
         brick[i] = brick[i] ? 0 : -1;
 }
 
+// dense fp64 grids, after the cell starts: an occupied brick's word becomes the mask of its
+// 16 (y, z) cell rows that hold points (bit yo | zo << 2, >= 1), so the far pass visits only
+// those rows instead of one cstart round trip per row; empty bricks stay -1
+__global__ void k_brick_rows(GridDesc g, int32_t* brick) {
+    const int64_t nb = (int64_t)g.nb[0] * g.nb[1] * g.nb[2];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nb;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (brick[i] < 0) continue;
+        const int xb = (int)(i % g.nb[0]), yb = (int)((i / g.nb[0]) % g.nb[1]), zb = (int)(i / ((int64_t)g.nb[0] * g.nb[1]));
+        const int x0 = 4 * xb, x1 = min(4 * xb + 3, g.n[0] - 1);
+        uint32_t st[16], en[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int y = 4 * yb + (r & 3), z = 4 * zb + (r >> 2);
+            const bool in = y < g.n[1] && z < g.n[2];
+            st[r] = in ? g.cstart[dense_id(g, x0, y, z)] : 0u;
+            en[r] = in ? g.cstart[dense_id(g, x1, y, z) + 1] : 0u;
+        }
+        int32_t m = 0;
+#pragma unroll
+        for (int r = 0; r < 16; r++) m |= en[r] > st[r] ? (1 << r) : 0;
+        brick[i] = m;
+    }
+}
+
 __global__ void k_brick_bits(const int32_t* brick, int64_t nb, uint32_t* bits) {
     int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (w >= (nb + 31) / 32) return;
@@ -565,6 +590,8 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         dfree(ctx, lo);
         dfree(ctx, d_ne);
         g.cstart = count;
+        if (g.dense && is_f64 && n > 0)
+            hipLaunchKernelGGL(k_brick_rows, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, g, ix->brick);
         ix->g = g;
         ix->cstart = count;
         count = nullptr;

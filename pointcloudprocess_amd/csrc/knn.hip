@@ -38,6 +38,12 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_KNN_BATCH
 #define PCP_KNN_BATCH 4
 #endif
+#ifndef PCP_COOP_KTH_BISECT  // far pass: shared bound by counting bisection (1) or the exact k-th merge (0)
+#define PCP_COOP_KTH_BISECT 1
+#endif
+#ifndef PCP_COOP_VISIT_BATCH  // far pass: point loads in flight per visit step
+#define PCP_COOP_VISIT_BATCH 1
+#endif
 #ifndef PCP_COOP_FLAT  // far pass: 1 = a batch's occupied-brick rows dealt over the lanes
 #define PCP_COOP_FLAT 1
 #endif
@@ -145,7 +151,18 @@ struct CoopVisitor {
     __device__ double bound() const { return fmin(top.kth(), shared) * (1.0 + 1e-12); }
     __device__ double ubound() const { return shared * (1.0 + 1e-12); }
     __device__ void visit(uint32_t s, uint32_t e) {
-        for (uint32_t t = s; t < e; t++) {
+        constexpr int U = PCP_COOP_VISIT_BATCH;
+        uint32_t t = s;
+        if (U > 1) {
+            for (; t + U <= e; t += U) {
+                double4 p[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) p[u] = pts[t + u];
+#pragma unroll
+                for (int u = 0; u < U; u++) top.push(l2_simple(qx, qy, qz, p[u]), (int)p[u].w);
+            }
+        }
+        for (; t < e; t++) {
             const double4 p = pts[t];
             top.push(l2_simple(qx, qy, qz, p), (int)p.w);
         }
@@ -175,6 +192,28 @@ __device__ double global_kth(const TopK<K>& top, int kk, int lane) {
         kth = bd;
     }
     return kth;
+}
+
+// An upper bound on the wave's exact k-th d2 within 2^-20 of it, without copying the lists:
+// the smallest tau (a double whose low word is all ones) with at least kk list entries <= tau,
+// by bisection on tau's high word; each step counts the entries with one compare per slot into
+// a lane mask and popcounts (SALU), no cross-lane moves.  +inf when fewer than kk are finite.
+template <int K>
+__device__ double kth_bound(const TopK<K>& top, int kk) {
+    auto count = [&](double t) {
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < K; i++) c += __popcll(__ballot(i < kk && top.d[i] <= t));
+        return c;
+    };
+    if (count(DBL_MAX) < kk) return INFINITY;
+    uint32_t lo = 0, hi = 0x7fefffffu;  // DBL_MAX's high word
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (count(__hiloint2double((int)mid, (int)0xffffffffu)) >= kk) hi = mid;
+        else lo = mid + 1;
+    }
+    return __hiloint2double((int)hi, (int)0xffffffffu);
 }
 
 // An upper bound on the wave's exact k-th d2, cheap enough to refresh inside a shell: the
@@ -214,7 +253,7 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     uint32_t t = 0;  // the wave's cell / brick counter: item t belongs to lane t % 64
     for (int s = 0; s <= smax + 1; s++) {
         if (s > 0) {
-            v.shared = global_kth<K>(v.top, kk, lane);
+            v.shared = PCP_COOP_KTH_BISECT ? fmin(v.shared, kth_bound<K>(v.top, kk)) : global_kth<K>(v.top, kk, lane);
             const double rmin = (double)(s - 1) + dmin - mc;
             if (rmin > 0 && rmin * rmin * h2 > v.ubound()) return;
         }
@@ -253,15 +292,17 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     farb = max(farb, max(bz - (g.nb[2] - 1), -bz));
     const int sbmax = farb + max(g.nb[0], max(g.nb[1], g.nb[2]));
 #if PCP_COOP_FLAT
-    __shared__ int4 s_flat[kB / 64][64 * 8];  // per wave: a batch's occupied bricks {x, y, z, slot}
+    __shared__ int4 s_flat[kB / 64][64 * 8];  // per wave: a batch's occupied bricks {x, y, z, word}
+    __shared__ uint16_t s_rows[kB / 64][64 * 8 * 16];  // per wave: their non-empty rows (brick << 4 | row)
     int4* const flat = s_flat[threadIdx.x >> 6];
+    uint16_t* const rows = s_rows[threadIdx.x >> 6];
 #endif
     // rings closer than `farb` lie wholly outside the grid (a query far away from it)
     if (tk) tk[0] = clock64();
     for (int sb = farb; sb <= sbmax; sb++) {
         if (shells) (*shells)++;
         const long long c0 = tk ? (long long)clock64() : 0;
-        v.shared = global_kth<K>(v.top, kk, lane);
+        v.shared = PCP_COOP_KTH_BISECT ? fmin(v.shared, kth_bound<K>(v.top, kk)) : global_kth<K>(v.top, kk, lane);
         if (tk) tk[1] += (long long)clock64() - c0;
         if (sb > 0) {
             const double rmin = (double)(4 * (sb - 1)) + bdmin - mc;
@@ -298,9 +339,13 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
         constexpr int kBB = 8;
         static_assert(kBB == 8, "s_flat holds 64 * 8 bricks per wave");
         for (int64_t base = 0; base < total; base += 64 * kBB) {  // wave-uniform trip count
+            const long long cb0 = tk ? (long long)clock64() : 0;
             const int64_t t0 = base + lane;
             int bxs[kBB], bys[kBB], bzs[kBB];
             int32_t occ[kBB];
+#if PCP_COOP_FLAT
+            uint32_t msk[kBB], bat[kBB];  // row masks and flat[] positions of this lane's bricks
+#endif
 #pragma unroll
             for (int u = 0; u < kBB; u++) {
                 const int64_t t = t0 + 64 * u;
@@ -325,11 +370,15 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
                 bxs[u] = xb; bys[u] = yb; bzs[u] = zb;
                 occ[u] = live ? g.brick[((int64_t)zb * g.nb[1] + yb) * g.nb[0] + xb] : -1;
             }
+            const long long cb1 = tk ? (long long)clock64() : 0;
+            if (tk) tk[2] += cb1 - cb0;  // brick coordinates, pruning and occupancy loads
 #if PCP_COOP_FLAT
-            // The batch's occupied bricks are listed in LDS and their 16 (y, z) rows dealt
-            // round-robin over the lanes: a lane's rows are independent load chains, where the
-            // per-lane walk below serialises 16 rows per occupied brick slot.
-            uint32_t nocc = 0;
+            // The batch's occupied bricks are listed in LDS, then their rows that hold points
+            // (the brick word's row mask on dense fp64 grids; all 16 rows otherwise) as one flat
+            // item list dealt round-robin over the lanes: every lane's round is one row's
+            // cstart round trip, and empty rows cost none.
+            uint32_t nocc = 0, nrow = 0;
+            uint32_t myrows = 0;
 #pragma unroll
             for (int u = 0; u < kBB; u++) {
                 const uint64_t m = __ballot(occ[u] >= 0);
@@ -337,13 +386,38 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
                     const uint32_t at = nocc + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                     flat[at] = make_int4(bxs[u], bys[u], bzs[u], occ[u]);
+                    bat[u] = at;
+                    const uint32_t rm = (g.dense && occ[u] > 0) ? (uint32_t)occ[u] & 0xffffu : 0xffffu;
+                    msk[u] = rm;
+                    myrows += (uint32_t)__popc(rm);
+                } else {
+                    msk[u] = 0u;
                 }
                 nocc += (uint32_t)__popcll(m);
+            }
+            // exclusive scan of the lanes' row counts -> this lane's first row slot
+            uint32_t incl = myrows;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t tv = (uint32_t)__shfl_up((int)incl, o, 64);
+                if (lane >= o) incl += tv;
+            }
+            nrow = (uint32_t)__shfl((int)incl, 63, 64);
+            uint32_t slot = incl - myrows;
+#pragma unroll
+            for (int u = 0; u < kBB; u++) {
+                uint32_t rm = msk[u];
+                while (rm) {
+                    const uint32_t r = (uint32_t)__builtin_ctz(rm);
+                    rm &= rm - 1u;
+                    rows[slot++] = (uint16_t)((bat[u] << 4) | r);
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (uint32_t it = (uint32_t)lane; it < 16 * nocc; it += 64) {
+            for (uint32_t ir = (uint32_t)lane; ir < nrow; ir += 64) {
+                const uint32_t it = rows[ir];
                 const int4 bk = flat[it >> 4];
                 const int y = 4 * bk.y + (int)(it & 3), z = 4 * bk.z + (int)((it >> 2) & 3);
                 if (y >= g.n[1] || z >= g.n[2]) continue;
@@ -410,8 +484,11 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
                 }
             }
 #endif
+            const long long cb2 = tk ? (long long)clock64() : 0;
+            if (tk) tk[3] += cb2 - cb1;  // the occupied bricks' rows and points
             // tighten the shared bound mid-shell (the exact k-th is refreshed per shell)
             if (kk <= 64) v.shared = fmin(v.shared, wave_kth_of_bests<K>(v.top, kk, lane));
+            if (tk) tk[4] += (long long)clock64() - cb2;
         }
     }
 }
@@ -481,7 +558,7 @@ __global__ __launch_bounds__(kB) void k_normals_coop(GridDesc g, const double4* 
         v.top.init(kk);
         int shells = 0;
         const long long t0 = dbg ? (long long)clock64() : 0;
-        long long tk[2] = {t0, 0};
+        long long tk[5] = {t0, 0, 0, 0, 0};
         coop_search<K>(g, mc, v, lane, kk, dbg ? &shells : nullptr, dbg ? tk : nullptr);
         if (dbg && lane == 0) {  // PCP_KNN_DEBUG: shells walked and cycles per deferred query
             const unsigned long long dt = (unsigned long long)((long long)clock64() - t0);
@@ -492,7 +569,12 @@ __global__ __launch_bounds__(kB) void k_normals_coop(GridDesc g, const double4* 
             atomicMax(dbg + 4, dt);
             atomicAdd(dbg + 9, (unsigned long long)(tk[0] - t0));  // ring phase
             atomicAdd(dbg + 10, (unsigned long long)tk[1]);        // global_kth in the shells
-            if (dt >= dbg[4]) {  // the slowest query's coordinates (racy, debugging only)
+            if (dt >= dbg[4]) {  // the slowest query's coordinates and phases (racy, debugging only)
+                dbg[11] = (unsigned long long)(tk[0] - t0);
+                dbg[12] = (unsigned long long)tk[1];
+                dbg[13] = (unsigned long long)tk[2];
+                dbg[14] = (unsigned long long)tk[3];
+                dbg[15] = (unsigned long long)tk[4];
                 dbg[5] = (unsigned long long)__double_as_longlong(qp.x);
                 dbg[6] = (unsigned long long)__double_as_longlong(qp.y);
                 dbg[7] = (unsigned long long)__double_as_longlong(qp.z);
@@ -1386,8 +1468,8 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
     if (ix->g.dense && tile_R > 0) {
         unsigned long long* st = nullptr;
         if (getenv("PCP_KNN_DEBUG")) {
-            PCP_TRY(dmalloc(ctx, &st, 16));
-            PCP_HIP(ctx, hipMemsetAsync(st, 0, 16 * sizeof(unsigned long long), ctx->stream));
+            PCP_TRY(dmalloc(ctx, &st, 32));
+            PCP_HIP(ctx, hipMemsetAsync(st, 0, 32 * sizeof(unsigned long long), ctx->stream));
         }
         const unsigned nbt = (unsigned)std::min<int64_t>((ix->n + 63) / 64, 1 << 20);
         // brick order of the queries: (brick key, sorted position) radix-sorted
@@ -1450,6 +1532,10 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
             hipMemcpy(qd, st + 9, sizeof(qd), hipMemcpyDeviceToHost);
             unsigned long long ph[2] = {0, 0};
             hipMemcpy(ph, st + 13, sizeof(ph), hipMemcpyDeviceToHost);
+            unsigned long long sl[5] = {0, 0, 0, 0, 0};
+            hipMemcpy(sl, st + 15, sizeof(sl), hipMemcpyDeviceToHost);
+            fprintf(stderr, "pcp_normals_knn coop: the slowest query's cycles: ring phase %llu, shells' exact k-th %llu, "
+                    "brick occupancy %llu, rows and points %llu, mid-shell bounds %llu\n", sl[0], sl[1], sl[2], sl[3], sl[4]);
             fprintf(stderr, "pcp_normals_knn coop: cycles per query: ring phase %.0f, global_kth in shells %.0f\n",
                     cd[0] ? (double)ph[0] / cd[0] : 0.0, cd[0] ? (double)ph[1] / cd[0] : 0.0);
             fprintf(stderr, "pcp_normals_knn coop: the slowest query at (%.3f, %.3f, %.3f), last k-th d2 %.4f; grid o (%.2f %.2f %.2f) h %.4f n %d %d %d\n",
