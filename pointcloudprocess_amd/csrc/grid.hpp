@@ -207,4 +207,55 @@ __device__ __forceinline__ bool ring_search(const GridDesc& g, T qx, T qy, T qz,
     return true;
 }
 
+// Dense grids, queries inside the grid: the cell window of ring_search's phase 1 (Chebyshev
+// radius kCellRings) walked by (y, z) rows instead of cells -- each row's cells within the
+// bound are one contiguous point range, so a row costs one cstart round trip where the cell
+// walk pays one per cell.  Rows go nearest plane first (0, -1, +1, ...), so the bound falls
+// early.  Returns false when the bound still reaches past the window (the caller defers the
+// query to the far pass), exactly ring_search's FAR = false contract.
+template <typename Vis>
+__device__ __forceinline__ bool row_window_search(const GridDesc& g, double qx, double qy, double qz, double mc,
+                                                  Vis& vis) {
+    constexpr int R = kCellRings;
+    const double fx = cell_f<double>(g, qx, 0), fy = cell_f<double>(g, qy, 1), fz = cell_f<double>(g, qz, 2);
+    const int cx = (int)floor(fx), cy = (int)floor(fy), cz = (int)floor(fz);
+    const double lx = fx - cx, ly = fy - cy, lz = fz - cz;
+    const double h2 = g.h * g.h, inv_h2 = 1.0 / h2;
+    for (int oz = 0; oz <= 2 * R; oz++) {
+        const int dz = (oz & 1) ? -((oz + 1) >> 1) : (oz >> 1);
+        const int z = cz + dz;
+        if (z < 0 || z >= g.n[2]) continue;
+        const double gz2 = sq_gap(axis_gap<double>(z, cz, lz), mc);
+        if (gz2 * h2 > vis.bound()) continue;
+        for (int oy = 0; oy <= 2 * R; oy++) {
+            const int dy = (oy & 1) ? -((oy + 1) >> 1) : (oy >> 1);
+            const int y = cy + dy;
+            if (y < 0 || y >= g.n[1]) continue;
+            const double gyz2 = gz2 + sq_gap(axis_gap<double>(y, cy, ly), mc);
+            const double lim = vis.bound() * inv_h2 - gyz2;  // remaining x extent^2 (cells)
+            if (lim < 0.0) continue;
+            int xa = cx - R, xb = cx + R;  // the whole window row while the bound is that wide
+            if (lim < (double)((R + 2) * (R + 2))) {
+                const double rx = sqrt(lim) * (1.0 + 1e-12) + mc;
+                xa = max((int)floor(fx - rx), xa);
+                xb = min((int)floor(fx + rx), xb);
+            }
+            xa = max(xa, 0);
+            xb = min(xb, g.n[0] - 1);
+            if (xa > xb) continue;
+            const int64_t c = dense_id(g, xa, y, z);
+            const uint32_t s = g.cstart[c], e = g.cstart[c + (xb - xa + 1)];
+            if (e > s) vis.visit(s, e);
+        }
+    }
+    // the window covers the grid: nothing lies outside it
+    if (cx - R <= 0 && cx + R >= g.n[0] - 1 && cy - R <= 0 && cy + R >= g.n[1] - 1 && cz - R <= 0 &&
+        cz + R >= g.n[2] - 1)
+        return true;
+    // every point outside the window lies at least R + dmin - mc cells away
+    const double dmin = fmin(fmin(fmin(lx, 1 - lx), fmin(ly, 1 - ly)), fmin(lz, 1 - lz));
+    const double rmin = (double)R + dmin - mc;
+    return rmin > 0.0 && rmin * rmin * h2 > vis.bound();
+}
+
 }  // namespace pcp

@@ -44,6 +44,9 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_COOP_VISIT_BATCH  // far pass: point loads in flight per visit step
 #define PCP_COOP_VISIT_BATCH 1
 #endif
+#ifndef PCP_NEAR_ROWS  // normals near pass on dense grids: 1 = row walk of the cell window, 0 = cell rings
+#define PCP_NEAR_ROWS 1
+#endif
 #ifndef PCP_COOP_FLAT  // far pass: 1 = a batch's occupied-brick rows dealt over the lanes
 #define PCP_COOP_FLAT 1
 #endif
@@ -811,7 +814,15 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
         v.pts = pts;
         v.qx = qp.x; v.qy = qp.y; v.qz = qp.z;
         v.top.init(kk);
-        if (!ring_search<double, KnnVisitor<K>, FAR>(g, v.qx, v.qy, v.qz, mc, v)) {
+        // the near pass over the tiled kernel's uncertified queries, on dense grids, walks the
+        // window by rows (the queries are indexed points, so they lie inside the grid).  Not for
+        // every point: a large k over a dense neighbourhood fills its list faster cell by cell
+        // (measured: k = 32 over all 8.86M C3 points 32.7 -> 67.0 ms by rows; the tile's 10.9K
+        // uncertified rows 0.3 ms faster, k = 8 0.3 ms)
+        const bool done = (!FAR && in.list && g.dense && PCP_NEAR_ROWS)
+                              ? row_window_search<KnnVisitor<K>>(g, v.qx, v.qy, v.qz, mc, v)
+                              : ring_search<double, KnnVisitor<K>, FAR>(g, v.qx, v.qy, v.qz, mc, v);
+        if (!done) {
             defer(far, s);
             continue;
         }
@@ -866,7 +877,7 @@ __device__ __forceinline__ uint32_t qd2(uint32_t qxy, int qz, uint32_t pxy, int 
     asm("v_pk_sub_i16 %0, %1, %2" : "=v"(dxy) : "v"(qxy), "v"(pxy));
     const int dz = qz - pz;
     int r;
-    asm("v_dot2_i32_i16 %0, %1, %1, %2" : "=v"(r) : "v"(dxy), "v"(dz * dz));
+    asm("v_dot2_i32_i16 %0, %1, %1, %2" : "=v"(r) : "v"(dxy), "v"(__mul24(dz, dz)));  // |dz| < 2^14: v_mul_i32_i24, full rate
     return (uint32_t)r;
 }
 __device__ __forceinline__ int wmin_i(int v) {
