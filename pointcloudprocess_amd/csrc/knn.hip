@@ -801,7 +801,9 @@ __global__ void k_plane_default(pcp_plane* out, int64_t n) {
 // queries = the indexed points themselves, walked in the index's spatial order
 // `in` (near pass only): the sorted positions to process (the tiled kernel's uncertified
 // queries), or every point when in.list is null
-template <int K, bool FAR>
+// ROWS (the near pass over the tiled kernel's uncertified queries): the row walk below; its
+// own instantiation, so the all-points ring path does not carry its registers
+template <int K, bool FAR, bool ROWS = false>
 __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, const int32_t* mapping, int identity,
                                                 const int32_t* pos_of_j, int64_t n, int kk, double mc,
                                                 pcp_plane* out, int64_t n_out, FarList far,
@@ -819,7 +821,7 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
         // every point: a large k over a dense neighbourhood fills its list faster cell by cell
         // (measured: k = 32 over all 8.86M C3 points 32.7 -> 67.0 ms by rows; the tile's 10.9K
         // uncertified rows 0.3 ms faster, k = 8 0.3 ms)
-        const bool done = (!FAR && in.list && g.dense && PCP_NEAR_ROWS)
+        const bool done = (ROWS && !FAR && g.dense)
                               ? row_window_search<KnnVisitor<K>>(g, v.qx, v.qy, v.qz, mc, v)
                               : ring_search<double, KnnVisitor<K>, FAR>(g, v.qx, v.qy, v.qz, mc, v);
         if (!done) {
@@ -1516,7 +1518,8 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         hipLaunchKernelGGL((k_normals_tile<KV>), dim3(nbt), dim3(64), 0, ctx->stream, ix->g, pts, ix->mapping,      \
                            ix->identity, ix->n, kk, tile_R, mc, out, n_out, fb.f, st, order);                     \
         if (near_pass)                                                                                            \
-            hipLaunchKernelGGL((k_normals<KV, false>), dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g,    \
+            hipLaunchKernelGGL((k_normals<KV, false, PCP_NEAR_ROWS != 0>), dim3(blocks_for(ix->n)), dim3(kB), 0,     \
+                               ctx->stream, ix->g,                                                              \
                                pts, ix->mapping, ix->identity, ix->pos_of_j, ix->n, kk, mc, out, n_out, fb2.f, fb.f); \
         hipLaunchKernelGGL((k_normals_coop<KV>), dim3(kFarBlocks), dim3(kB), 0, ctx->stream, ix->g, pts,            \
                            ix->mapping, ix->identity, ix->pos_of_j, kk, mc, out, n_out, near_pass ? fb2.f : fb.f,  \
