@@ -44,6 +44,9 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_COOP_VISIT_BATCH  // far pass: point loads in flight per visit step
 #define PCP_COOP_VISIT_BATCH 1
 #endif
+#ifndef PCP_TILE_MORTON  // tiled normals: queries in Morton order inside each brick (1) or index order (0)
+#define PCP_TILE_MORTON 1
+#endif
 #ifndef PCP_NEAR_ROWS  // normals near pass on dense grids: 1 = row walk of the cell window, 0 = cell rings
 #define PCP_NEAR_ROWS 1
 #endif
@@ -949,14 +952,36 @@ __device__ __forceinline__ TileBox tile_box(const GridDesc& g, int cx, int cy, i
 // inside a brick), so that a wave's 64 queries are neighbours in all three axes -- in the index's
 // row-major order the points of one x-row of a facade are metres apart
 constexpr int kTileBrick = 3;  // log2 brick edge (cells)
-__global__ void k_brick_keys(GridDesc g, const double4* pts, int64_t n, uint32_t* key, uint32_t* pos) {
+// Inside a brick the key continues with `lb` bits of a Morton code of the point's position
+// (cell and sub-cell: 2^(lb/3) steps per brick edge), so a wave's 64 queries form a compact
+// patch instead of a run along one x-row of cells (lb = 0: index order inside the brick).
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // bits b -> 3b
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x30000ffu;
+    v = (v | (v << 8)) & 0x300f00fu;
+    v = (v | (v << 4)) & 0x30c30c3u;
+    v = (v | (v << 2)) & 0x9249249u;
+    return v;
+}
+__global__ void k_brick_keys(GridDesc g, const double4* pts, int64_t n, int lb, uint32_t* key, uint32_t* pos) {
     const int nbx = (g.n[0] + 7) >> kTileBrick, nby = (g.n[1] + 7) >> kTileBrick;
+    const int sub = lb / 3 - kTileBrick;  // sub-cell bits per axis (>= 0 when lb > 0)
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
         const double4 p = pts[s];
-        const int cx = clampi(cell_i<double>(g, p.x, 0), 0, g.n[0] - 1) >> kTileBrick;
-        const int cy = clampi(cell_i<double>(g, p.y, 1), 0, g.n[1] - 1) >> kTileBrick;
-        const int cz = clampi(cell_i<double>(g, p.z, 2), 0, g.n[2] - 1) >> kTileBrick;
-        key[s] = (uint32_t)(((int64_t)cz * nby + cy) * nbx + cx);
+        const double fx = cell_f<double>(g, p.x, 0), fy = cell_f<double>(g, p.y, 1), fz = cell_f<double>(g, p.z, 2);
+        const int cx = clampi((int)floor(fx), 0, g.n[0] - 1), cy = clampi((int)floor(fy), 0, g.n[1] - 1),
+                  cz = clampi((int)floor(fz), 0, g.n[2] - 1);
+        uint32_t k = (uint32_t)(((int64_t)(cz >> kTileBrick) * nby + (cy >> kTileBrick)) * nbx + (cx >> kTileBrick));
+        if (lb > 0) {
+            const double sc = (double)(1 << sub);
+            auto loc = [&](double f, int c) {  // position in the brick, 2^(3 + sub) steps
+                const int q = (c & ((1 << kTileBrick) - 1)) << sub;
+                const int t = (int)((f - (double)c) * sc);
+                return (uint32_t)(q + (t < 0 ? 0 : (t >= (1 << sub) ? (1 << sub) - 1 : t)));
+            };
+            k = (k << lb) | spread3(loc(fx, cx)) | (spread3(loc(fy, cy)) << 1) | (spread3(loc(fz, cz)) << 2);
+        }
+        key[s] = k;
         pos[s] = (uint32_t)s;
     }
 }
@@ -1499,11 +1524,16 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         PCP_TRY(dmalloc(ctx, &k1, ix->n));
         PCP_TRY(dmalloc(ctx, &v0, ix->n));
         PCP_TRY(dmalloc(ctx, &order, ix->n));
-        hipLaunchKernelGGL(k_brick_keys, dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->n, k0, v0);
         const int64_t nbr = (int64_t)((ix->g.n[0] + 7) >> kTileBrick) * ((ix->g.n[1] + 7) >> kTileBrick) *
                             ((ix->g.n[2] + 7) >> kTileBrick);
         unsigned bits = 1;
         while (bits < 32 && ((int64_t)1 << bits) < nbr) bits++;
+        // Morton bits inside the brick: cell + sub-cell (12) when the key still fits 32 bits
+        int lb = 0;
+        if (PCP_TILE_MORTON) lb = bits + 12 <= 32 ? 12 : (bits + 9 <= 32 ? 9 : 0);
+        hipLaunchKernelGGL(k_brick_keys, dim3(blocks_for(ix->n)), dim3(kB), 0, ctx->stream, ix->g, pts, ix->n, lb, k0,
+                           v0);
+        bits += (unsigned)lb;
         PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, order, (size_t)ix->n, 0u, bits, ctx->stream));
         PCP_TRY(dmalloc(ctx, (char**)&tmp, tb));
         PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tb, k0, k1, v0, order, (size_t)ix->n, 0u, bits, ctx->stream));
