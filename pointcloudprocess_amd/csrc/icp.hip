@@ -156,13 +156,6 @@ struct IcpArgs {
     uint2* dbgfz;       // kDbgCount: chunk freeze model state
 };
 
-// 32-bit dense cell ids (ICP grids: pcp_icp_create keeps every cell id below 2^32), one
-// 32-bit multiply-add chain instead of 64-bit v_mad_u64_u32 sequences per row
-__device__ __forceinline__ uint32_t dense_plane32(const GridDesc& g) { return (uint32_t)g.n[0] * (uint32_t)g.n[1]; }
-__device__ __forceinline__ uint32_t dense_id32(const GridDesc& g, int cx, int cy, int cz) {
-    return ((uint32_t)cz * (uint32_t)g.n[1] + (uint32_t)cy) * (uint32_t)g.n[0] + (uint32_t)cx;
-}
-
 // sorted query i as {x, y, z, 0}
 __device__ __forceinline__ float4 ldq(const IcpArgs& a, int64_t i) {
     const QXyz v = a.q[i];
@@ -404,8 +397,8 @@ __device__ __forceinline__ void box_search(const GridDesc& g, const float4* tp, 
             const int xa = max((int)floorf(fx - rx), 0), xb = min((int)floorf(fx + rx), g.n[0] - 1);
             if (xa > xb) continue;
             if (g.dense) {
-                const uint32_t c = dense_id32(g, xa, y, z);
-                b.scan_g<G>(tp, g.cstart[c], g.cstart[c + (uint32_t)(xb - xa + 1)], qx, qy, qz, sub);
+                const int64_t c = dense_id(g, xa, y, z);
+                b.scan_g<G>(tp, g.cstart[c], g.cstart[c + (xb - xa + 1)], qx, qy, qz, sub);
             } else {
                 for (int x = xa; x <= xb; x++) {
                     uint32_t s, e;
@@ -1237,16 +1230,13 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
         // the octant's 4 x-rows (y = by + (r & 1), z = bz + (r >> 1)), cells [xa, xb]
         const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
         uint32_t rs[4], rn[4];
-        // the 4 rows' cell ids from one 32-bit id (pcp_icp_create bounds the cells below 2^32;
-        // wrapped intermediates of rows outside the grid are never loaded)
-        const uint32_t c00 = dense_id32(g, xa, by, bz);
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int y = by + (r & 1), z = bz + (r >> 1);
             const bool in = scanq && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
-            const uint32_t cc = c00 + ((r & 1) ? (uint32_t)g.n[0] : 0u) + ((r >> 1) ? dense_plane32(g) : 0u);
+            const int64_t cc = in ? dense_id(g, xa, y, z) : 0;
             rs[r] = in ? g.cstart[cc] : 0u;
-            rn[r] = in ? g.cstart[cc + (uint32_t)(xb - xa + 1)] : 0u;
+            rn[r] = in ? g.cstart[cc + (xb - xa + 1)] : 0u;
         }
 #pragma unroll
         for (int r = 0; r < 4; r++) rn[r] -= rs[r];
