@@ -318,9 +318,16 @@ def main():
         torch.cuda.synchronize()
         result = {}
 
+        spans = []  # (before build, after build + query sort, after the iterations) per timed step
+
         def one_step(timed):
             st = {}
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
+            if timed:
+                ev[0].record()
             eng = D.GpuEngine(ctx, tile_t, tile_q, cell_size=args.cell)
+            if timed:
+                ev[1].record()
             if mode == "sharded":
                 err, T = D.run_target_sharded_dev(eng, np.eye(4), args.rmax, args.iters, bounds,
                                                   exchange=exch if timed else None)
@@ -331,6 +338,8 @@ def main():
                                             exchange=exch if timed else None, out_stats=st)
             ms, nl = eng.icp.kernel_ms()
             if timed:
+                ev[2].record()
+                spans.append(ev)
                 kernel["ms"] += ms
                 kernel["launches"] += nl
                 kernel["fallback"] += st.get("fallback", 0.0)
@@ -349,6 +358,15 @@ def main():
         barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
         exch_ms = (sum(a.elapsed_time(b) for a, b in exch) / len(exch)) if exch else 0.0
+        # where a rank's step goes (the strong-scaling model: the pre-iteration span is the part
+        # that does not shrink with the slab): every rank's averages, gathered by a SUM of slots
+        pre = sum(e[0].elapsed_time(e[1]) for e in spans) / max(len(spans), 1)
+        its = sum(e[1].elapsed_time(e[2]) for e in spans) / max(len(spans), 1)
+        slots = torch.zeros(2 * world, dtype=torch.float64, device=dev)
+        slots[2 * rank], slots[2 * rank + 1] = pre, its
+        if world > 1:
+            dist.all_reduce(slots, op=dist.ReduceOp.SUM)
+        slots = slots.cpu().tolist()
         rec = {
             "value": units * args.iters * steps / dt / 1e6,
             "ms_per_step": dt / steps * 1e3,
@@ -360,6 +378,8 @@ def main():
             "units_per_launch": result["nq"],
             "queries_all_ranks": sum_over_ranks(float(result["nq"])),
             "fallback_frac": kernel["fallback"] / max(1.0, result["nq"] * kernel["launches"]),
+            "per_rank": [{"rank": r, "pre_iteration_ms": round(slots[2 * r], 3),
+                          "iterations_ms": round(slots[2 * r + 1], 3)} for r in range(world)],
         }
         rec.update({k: v for k, v in info.items() if k != "guard_ok"})
         del tile_t, tile_q
@@ -400,8 +420,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic street scene (ground+facades+poles, seeded); query = independent "
                     "resample moved by a known rigid motion",
-            "config": {"workload": "C4: 50M-vs-50M get_rot_icp/point_cloud_closure ICP, 20 iters "
-                                   "(index build + query sort + iterations per step)",
+            "config": {"workload": f"C4: {n / 1e6:g}M-vs-{n / 1e6:g}M get_rot_icp/point_cloud_closure ICP, "
+                                   f"{args.iters} iters (index build + query sort + iterations per step)"
+                                   + (" per rank" if args.mode == "weak" else ""),
                        "points_per_cloud": n, "iters": args.iters, "rmax_m": args.rmax,
                        "cell_m": args.cell, "mode": args.mode, "parallelism": par[args.mode]},
             "icp_iter_per_s": round(r["icp_iter_per_s"], 3),
@@ -409,6 +430,7 @@ def main():
             "icp_max_abs_T_err_vs_truth": float(np.abs(r["T"] - T_true).max()),
             "halo_guard_ok": r["guard_ok"],
             "exchange_ms_per_iter": round(r["exchange_ms_per_iter"], 4),
+            "per_rank": r["per_rank"],
             "roofline": {
                 "bound": "hbm",
                 "kernel": "+".join(ICP_KERNELS) + " (one ICP iteration; aggregate of the three passes and "

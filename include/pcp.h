@@ -125,7 +125,12 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_
  * as global_id_dev[caller] (or the caller index when NULL), and optionally one F1 plane per
  * row (calculate_plan_parameter(cloud, radius), calculate_feature.h:15) from fp32 sums.
  * Distances are fp32 of fp16 offsets: pairs within 3e-4 m of the radius may differ from an
- * exact search. */
+ * exact search.
+ * Threading: the count keeps its sorted-order row lengths in the index for the fill of the
+ * same (radius, n_owned) that follows it, so count -> fill pairs on ONE index must not
+ * interleave across threads or streams (serialize them, or give each caller its own index);
+ * a fill whose count was superseded still returns the right rows (it gathers the lengths
+ * back from its offsets) only when the interleaving count finished before it started. */
 int pcp_index_build_h16(pcp_ctx* ctx, const float* xyz_dev, size_t stride_bytes, int64_t n,
                         double cell_size, pcp_index** out);
 int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* index, float radius, int64_t n_owned,

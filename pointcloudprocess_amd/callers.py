@@ -159,7 +159,8 @@ def do_mul_frame_icp(ctx, line, stamp_file, start_index, end_index, grid, valid_
     updated in place, at the first entry of each stamp as get_cloud_rot_with_stamp does);
     stamp_file: stamp -> PCD path; grid: the CloudGrid map cache.  load_cloud(path) -> (n, 48)
     uint8 device records, or (records, is_dense) (default: pcd.load_pcd_ex, which reports
-    is_dense as the reference's reader does).  The joint frame's is_dense is the AND of the
+    is_dense as the reference's reader does); a plain tensor counts as dense when its xyz are
+    all finite.  The joint frame's is_dense is the AND of the
     loaded clouds' (PointCloud::operator+=, point_cloud.h:130-147).  Returns (dis, rot) of
     the joint registration."""
     import torch
@@ -178,7 +179,10 @@ def do_mul_frame_icp(ctx, line, stamp_file, start_index, end_index, grid, valid_
     _frame_walk(line, end_index, +1, valid_count, min_icp_threshold, stamp_file, frames)
     loaded = [load_cloud(p) for _, p in frames]  # (:754-765)
     clouds = [c[0] if isinstance(c, tuple) else c for c in loaded]
-    dense = all(c[1] if isinstance(c, tuple) else True for c in loaded)  # operator+= (point_cloud.h:143-146)
+    def _finite(rec):  # a plain tensor carries no flag: its is_dense is the data's finiteness
+        xyz = rec.view(torch.float64).reshape(-1, 6)[:, :3]
+        return bool(torch.isfinite(xyz).all())
+    dense = all(c[1] if isinstance(c, tuple) else _finite(c) for c in loaded)  # operator+= (point_cloud.h:143-146)
     frame = torch.cat(clouds) if clouds else torch.empty((0, 48), dtype=torch.uint8, device=ctx.device)
     frame = frame.clone()
     frame[:, 32:36] = torch.tensor([0, 0, 255, 0], dtype=torch.uint8, device=ctx.device)  # change_cloud_rgb 255,0,0

@@ -263,19 +263,53 @@ bool g_fault_installed = false;
 
 void fault_write(const char* s) { (void)!write(2, s, std::strlen(s)); }
 
+// async-signal-safe formatting (no snprintf in the handler): decimal and hex into a caller buffer
+char* fault_dec(char* p, unsigned long v) {
+    char t[24];
+    int n = 0;
+    do { t[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    while (n) *p++ = t[--n];
+    return p;
+}
+char* fault_hex(char* p, unsigned long v) {
+    *p++ = '0';
+    *p++ = 'x';
+    char t[20];
+    int n = 0;
+    do { t[n++] = "0123456789abcdef"[v & 15]; v >>= 4; } while (v);
+    while (n) *p++ = t[--n];
+    return p;
+}
+char* fault_str(char* p, const char* s, const char* end) {
+    while (*s && p < end) *p++ = *s++;
+    return p;
+}
+
 void fault_handler(int sig, siginfo_t* si, void* ucv) {
-    char buf[512];
+    char buf[1024];
+    const char* const end = buf + sizeof(buf) - 2;
     void* pc = nullptr;
 #if defined(__x86_64__)
     pc = (void*)((ucontext_t*)ucv)->uc_mcontext.gregs[REG_RIP];
 #endif
+    // dladdr reads the loader's already-built link map (no allocation on glibc); best effort
     Dl_info di{};
     const bool named = pc && dladdr(pc, &di) && di.dli_fname;
-    std::snprintf(buf, sizeof(buf), "[pcp fault] signal %d at address %p, pc %p in %s (%s+0x%lx)\n", sig,
-                  si ? si->si_addr : nullptr, pc, named ? di.dli_fname : "?",
-                  named && di.dli_sname ? di.dli_sname : "?",
-                  named ? (unsigned long)((char*)pc - (char*)(di.dli_sname ? di.dli_saddr : di.dli_fbase)) : 0ul);
-    fault_write(buf);
+    char* p = fault_str(buf, "[pcp fault] signal ", end);
+    p = fault_dec(p, (unsigned long)sig);
+    p = fault_str(p, " at address ", end);
+    p = fault_hex(p, (unsigned long)(si ? si->si_addr : nullptr));
+    p = fault_str(p, ", pc ", end);
+    p = fault_hex(p, (unsigned long)pc);
+    p = fault_str(p, " in ", end);
+    p = fault_str(p, named ? di.dli_fname : "?", end);
+    p = fault_str(p, " (", end);
+    p = fault_str(p, named && di.dli_sname ? di.dli_sname : "?", end);
+    p = fault_str(p, "+", end);
+    p = fault_hex(p, named ? (unsigned long)((char*)pc - (char*)(di.dli_sname ? di.dli_saddr : di.dli_fbase)) : 0ul);
+    *p++ = ')';
+    *p++ = '\n';
+    (void)!write(2, buf, (size_t)(p - buf));
     void* frames[48];
     const int n = backtrace(frames, 48);
     backtrace_symbols_fd(frames, n, 2);
@@ -300,6 +334,20 @@ void fault_handler(int sig, siginfo_t* si, void* ucv) {
 
 extern "C" int pcp_fault_report_install(void) {
     if (g_fault_installed) return PCP_OK;
+    // backtrace() loads libgcc's unwinder (malloc, dlopen) on its first call: do that here, not
+    // inside a handler that may have interrupted malloc
+    void* warm[2];
+    (void)backtrace(warm, 2);
+    // an alternate stack for this thread, so a stack overflow still reaches the report (kept
+    // if one is already installed, e.g. by Python's faulthandler)
+    stack_t cur{};
+    if (sigaltstack(nullptr, &cur) == 0 && (cur.ss_flags & SS_DISABLE)) {
+        static char alt[64 * 1024];
+        stack_t ss{};
+        ss.ss_sp = alt;
+        ss.ss_size = sizeof(alt);
+        (void)sigaltstack(&ss, nullptr);
+    }
     for (size_t k = 0; k < sizeof(kFaultSigs) / sizeof(kFaultSigs[0]); k++) {
         struct sigaction sa{};
         sa.sa_sigaction = fault_handler;

@@ -2770,7 +2770,11 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     const int64_t nchunks64 = (icp->nq + 63) / 64;
     icp->fb_seg = ((nchunks64 + nwaves_l - 1) / nwaves_l) * 64;
     // tile engine: two workgroups per CU (LDS-bound), each a contiguous range of query bricks
-    icp->nb_tile = (int)std::max<int64_t>(1, std::min<int64_t>(icp->nbk, (int64_t)dev_cus * 2));
+    // (capped at nb_fast: a tile workgroup writes its accumulators into the octant pass's partials
+    // region, which holds nb_fast blocks; sparse queries over many bricks would otherwise spill into
+    // the fallback pass's region and past the allocation)
+    icp->nb_tile = (int)std::max<int64_t>(
+        1, std::min<int64_t>({icp->nbk, (int64_t)dev_cus * 2, (int64_t)icp->nb_fast}));
     icp->engine_tile = engine_tile;
     icp->ver_dense = PCP_VER_DENSE;
     if (const char* vd = std::getenv("PCP_VER_DENSE")) icp->ver_dense = std::max(0, std::min(64, std::atoi(vd)));

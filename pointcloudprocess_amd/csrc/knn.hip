@@ -47,6 +47,9 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_TILE_MORTON  // tiled normals: queries in Morton order inside each brick (1) or index order (0)
 #define PCP_TILE_MORTON 1
 #endif
+#ifndef PCP_TILE_LANE_DEFAULT  // tiled normals: each lane scans its own window (1) or the union box (0)
+#define PCP_TILE_LANE_DEFAULT 1
+#endif
 #ifndef PCP_NEAR_ROWS  // normals near pass on dense grids: 1 = row walk of the cell window, 0 = cell rings
 #define PCP_NEAR_ROWS 1
 #endif
@@ -871,6 +874,15 @@ constexpr int kTileCap = 2048;   // union points per wave (11-bit list index)
 constexpr int kTileRows = 256;   // (y, z) rows per wave
 constexpr int kTileQ = 16383;    // 14-bit fixed-point coordinates: squared distances fit in int32
 constexpr int kTileExt = 96;     // box extent (cells) cap: keeps the fixed-point step fine
+constexpr int kLaneR = 2;        // largest window half-width of the per-lane window scan
+// (dy, dz) of row i of a 5 x 5 (y, z) window, rows by squared distance (the first 9 are the 3 x 3
+// window): (dy + 2) | (dz + 2) << 3 in 6-bit fields, 10 to a word (i is wave-uniform: scalar ops)
+__device__ __forceinline__ void window_row(int i, int& dy, int& dz) {
+    const uint64_t w = i < 10 ? 0x50964b6ca6914d2ull : (i < 20 ? 0x8438c860c702890ull : 0x804901ull);
+    const uint32_t v = (uint32_t)(w >> (6 * (i % 10))) & 63u;
+    dy = (int)(v & 7u) - 2;
+    dz = (int)(v >> 3) - 2;
+}
 __device__ __forceinline__ uint32_t umed3_(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -990,7 +1002,8 @@ template <int K>
 __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* pts, const int32_t* mapping,
                                                      int identity, int64_t n, int kk, int R, double mc,
                                                      pcp_plane* out, int64_t n_out, FarList far,
-                                                     unsigned long long* stats, const uint32_t* order) {
+                                                     unsigned long long* stats, const uint32_t* order,
+                                                     int lane_mode) {
     constexpr int M = K + 4;
     constexpr uint32_t kMax = 0xffffffffu;
     __shared__ uint2 s_u[kTileCap];
@@ -1083,19 +1096,114 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                 for (int i = M; i >= 1; i--) t[i] = umed3_(t[i - 1], t[i], x);
                 t[0] = min(t[0], x);
             };
-            uint32_t e = 0;
-            for (; e + 4 <= total; e += 4) {
-                uint2 p[4];
+            // Per-lane windows (lane_mode, R <= kLaneR): each lane scans only the rows of ITS OWN
+            // (2R+1)^2 (y, z) window -- the x-range of its +-R cells, nearest rows first -- from
+            // the staged list, instead of every point of the wave's union box (a compact patch's
+            // union box holds 4-10x a lane's window).  The lanes walk their own row lists (kept in
+            // LDS after the staged points) in lockstep with per-lane LDS addresses, and the
+            // insertion network runs only when some lane's key is below its current (M+1)-th
+            // (insertion of a larger key is a no-op on every slot).  Every window point not kept
+            // has a key >= the final (M+1)-th, so the list bound below is unchanged; the box-face
+            // bound becomes the lane's window faces.
+            bool lane_path = false;
+            const bool act = mine && valid;
+            const int wx0 = max(cx - R, b.x0), wx1 = min(cx + R, b.x1);
+            if (lane_mode && R <= kLaneR) {
+                constexpr int kW = (2 * kLaneR + 1) * (2 * kLaneR + 1);
+                const int nwin = R >= 2 ? 25 : (R == 1 ? 9 : 1);
+                // the LDS run [a, b) of window row i, or a == b (empty / outside the box)
+                auto row_run = [&](int i, uint32_t& a, uint32_t& e2) {
+                    int y, z;
+                    window_row(i, y, z);
+                    y += cy;
+                    z += cz;
+                    a = e2 = 0;
+                    if (act && i < nwin && y >= b.y0 && y <= b.y1 && z >= b.z0 && z <= b.z1) {
+                        const int r = (y - b.y0) + (z - b.z0) * b.ny;
+                        const uint32_t ca = g.cstart[dense_id(g, wx0, y, z)];
+                        const uint32_t cb = g.cstart[dense_id(g, wx1, y, z) + 1];
+                        a = s_rb[r] + (ca - s_rs[r]);
+                        e2 = a + (cb - ca);
+                    }
+                };
+                int nr = 0;  // pass 1: this lane's non-empty rows
+#pragma unroll 5
+                for (int i = 0; i < kW; i++) {
+                    uint32_t a, e2;
+                    row_run(i, a, e2);
+                    nr += e2 > a ? 1 : 0;
+                }
+                int excl = nr;
 #pragma unroll
-                for (int u = 0; u < 4; u++) p[u] = s_u[e + u];
-#pragma unroll
-                for (int u = 0; u < 4; u++) insert(key(qd2(qxy, qz, p[u].x, (int)p[u].y), e + u));
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t2 = __shfl_up(excl, o, 64);
+                    if (lane >= o) excl += t2;
+                }
+                const int tot_rows = __shfl(excl, 63, 64);
+                excl -= nr;
+                lane_path = 2 * total + (uint32_t)tot_rows <= 2u * kTileCap;
+                if (lane_path) {
+                    uint32_t* s_w = reinterpret_cast<uint32_t*>(s_u) + 2 * total;
+                    int j = excl;  // pass 2 (the cell starts again, now from the caches): write them
+#pragma unroll 5
+                    for (int i = 0; i < kW; i++) {
+                        uint32_t a, e2;
+                        row_run(i, a, e2);
+                        if (e2 > a) s_w[j++] = a | (e2 << 16);
+                    }
+                    wave_lds_fence();
+                    uint32_t rp = (uint32_t)excl, rend = (uint32_t)(excl + nr);
+                    uint32_t e = 0, ee = 0;
+                    for (;;) {
+                        if (e >= ee && rp < rend) {
+                            const uint32_t wr = s_w[rp++];
+                            e = wr & 0xffffu;
+                            ee = wr >> 16;
+                        }
+                        const bool on = e < ee;
+                        if (__ballot(on) == 0) break;
+                        const uint2 pp = s_u[on ? e : 0u];
+                        const uint32_t x = on ? key(qd2(qxy, qz, pp.x, (int)pp.y), e) : kMax;
+                        e += on ? 1u : 0u;
+                        if (__ballot(x < t[M]) != 0) insert(x);
+                    }
+                    if (stats && lane == 0) atomicAdd(stats + 20, 1ull);
+                }
             }
-            for (; e < total; e++) {
-                const uint2 pp = s_u[e];
-                insert(key(qd2(qxy, qz, pp.x, (int)pp.y), e));
+            if (!lane_path) {
+                uint32_t e = 0;
+                for (; e + 4 <= total; e += 4) {
+                    uint2 p[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) p[u] = s_u[e + u];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) insert(key(qd2(qxy, qz, p[u].x, (int)p[u].y), e + u));
+                }
+                for (; e < total; e++) {
+                    const uint2 pp = s_u[e];
+                    insert(key(qd2(qxy, qz, pp.x, (int)pp.y), e));
+                }
+                if (stats && lane == 0) atomicAdd(stats + 21, 1ull);
             }
             if (!mine) continue;  // (no wave-wide operation follows)
+            // the faces of the scanned region (the box, or the lane's window) that have grid cells
+            // beyond them bound every point outside the list (taken before the re-rank, so that
+            // only b2 stays live across it)
+            int fx0 = b.x0, fx1 = b.x1, fy0 = b.y0, fy1 = b.y1, fz0 = b.z0, fz1 = b.z1;
+            if (lane_path) {
+                fx0 = wx0; fx1 = wx1;
+                fy0 = max(cy - R, b.y0); fy1 = min(cy + R, b.y1);
+                fz0 = max(cz - R, b.z0); fz1 = min(cz + R, b.z1);
+            }
+            double bd = INFINITY;
+            if (fx0 > 0) bd = fmin(bd, q.x - (g.o[0] + (double)fx0 * g.h));
+            if (fx1 < g.n[0] - 1) bd = fmin(bd, g.o[0] + (double)(fx1 + 1) * g.h - q.x);
+            if (fy0 > 0) bd = fmin(bd, q.y - (g.o[1] + (double)fy0 * g.h));
+            if (fy1 < g.n[1] - 1) bd = fmin(bd, g.o[1] + (double)(fy1 + 1) * g.h - q.y);
+            if (fz0 > 0) bd = fmin(bd, q.z - (g.o[2] + (double)fz0 * g.h));
+            if (fz1 < g.n[2] - 1) bd = fmin(bd, g.o[2] + (double)(fz1 + 1) * g.h - q.z);
+            bd -= mc * g.h + 1e-12 * (fabs(q.x) + fabs(q.y) + fabs(q.z) + 1.0);
+            const double b2 = bd > 0.0 ? bd * bd * (1.0 - 1e-12) : (bd == INFINITY ? INFINITY : 0.0);
             // exact FLANN re-rank of the kept candidates
             double D[M];
             uint32_t P[M];
@@ -1136,16 +1244,6 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                     }
                 }
             }
-            // the box faces that have grid cells beyond them bound every point outside the list
-            double bd = INFINITY;
-            if (b.x0 > 0) bd = fmin(bd, q.x - ox);
-            if (b.x1 < g.n[0] - 1) bd = fmin(bd, ox + (double)(b.x1 - b.x0 + 1) * g.h - q.x);
-            if (b.y0 > 0) bd = fmin(bd, q.y - oy);
-            if (b.y1 < g.n[1] - 1) bd = fmin(bd, oy + (double)(b.y1 - b.y0 + 1) * g.h - q.y);
-            if (b.z0 > 0) bd = fmin(bd, q.z - oz);
-            if (b.z1 < g.n[2] - 1) bd = fmin(bd, oz + (double)(b.z1 - b.z0 + 1) * g.h - q.z);
-            bd -= mc * g.h + 1e-12 * (fabs(q.x) + fabs(q.y) + fabs(q.z) + 1.0);
-            const double b2 = bd > 0.0 ? bd * bd * (1.0 - 1e-12) : (bd == INFINITY ? INFINITY : 0.0);
             double dk = INFINITY;
 #pragma unroll
             for (int i = 0; i < M; i++)
@@ -1544,9 +1642,11 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         // to the wave-per-query pass -- a few thousand queries fill few waves one lane each
         const char* nenv = getenv("PCP_NORMALS_NEAR");
         const bool near_pass = nenv ? atoi(nenv) != 0 : PCP_NORMALS_NEAR_DEFAULT;
+        const char* lenv = getenv("PCP_TILE_LANE");  // A/B: 0 = every lane scans the union box
+        const int lane_mode = lenv ? atoi(lenv) : PCP_TILE_LANE_DEFAULT;
 #define LAUNCH_TILE(KV)                                                                                          \
         hipLaunchKernelGGL((k_normals_tile<KV>), dim3(nbt), dim3(64), 0, ctx->stream, ix->g, pts, ix->mapping,      \
-                           ix->identity, ix->n, kk, tile_R, mc, out, n_out, fb.f, st, order);                     \
+                           ix->identity, ix->n, kk, tile_R, mc, out, n_out, fb.f, st, order, lane_mode);          \
         if (near_pass)                                                                                            \
             hipLaunchKernelGGL((k_normals<KV, false, PCP_NEAR_ROWS != 0>), dim3(blocks_for(ix->n)), dim3(kB), 0,     \
                                ctx->stream, ix->g,                                                              \
@@ -1589,6 +1689,10 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
             fprintf(stderr, "pcp_normals_knn tile: k=%d R=%d n=%lld uncertified lanes: by the list bound %llu, by the "
                     "box %llu; oversized-wave lanes: rows %llu, points %llu; deferred %u\n", k, tile_R,
                     (long long)ix->n, h[0], h[2], h[1], h[3], c);
+            unsigned long long lp[2] = {0, 0};
+            hipMemcpy(lp, st + 20, sizeof(lp), hipMemcpyDeviceToHost);
+            fprintf(stderr, "pcp_normals_knn tile: groups scanned by lane windows %llu, by the union box %llu\n", lp[0],
+                    lp[1]);
             dfree(ctx, st);
         }
         return PCP_OK;

@@ -61,8 +61,8 @@ def test_correspondence_bit_exact(ctx, cell):
 @pytest.mark.parametrize("engine", ["tile", "cache"])
 def test_registration_exact_every_iteration(ctx, engine, monkeypatch):
     """Both engines over a registration: correspondences bit-exact and accumulators equal to the
-    oracle's direct sums at every iteration (the LDS-tiled streaming search, the default, and
-    the cached verify / octant / ring passes, PCP_ICP_ENGINE=cache)."""
+    oracle's direct sums at every iteration (the cached verify / octant / ring passes, the
+    default, and the opt-in LDS-tiled streaming search, PCP_ICP_ENGINE=tile)."""
     monkeypatch.setenv("PCP_ICP_ENGINE", engine)
     from pointcloudprocess_amd import ops, synth
     T_true = synth.rigid()
@@ -86,6 +86,30 @@ def test_registration_exact_every_iteration(ctx, engine, monkeypatch):
         rc, dT = ops.icp_solve(gacc)
         assert rc == 0
         T = dT @ T
+    icp.close()
+    index.close()
+
+
+def test_tile_engine_sparse_queries(ctx, monkeypatch):
+    """Few queries spread over many query bricks (nbk far above ceil(nq / 256)): the tile
+    engine's workgroups must stay inside the octant pass's partials region."""
+    from pointcloudprocess_amd import ops, synth
+    monkeypatch.setenv("PCP_ICP_ENGINE", "tile")
+    T_true = synth.rigid()
+    tgt, _ = _pair(400_000, 43, T_true)
+    q = synth.apply_inverse(synth.street_scene(5_000, 44, extent=(50.0, 50.0)), T_true)
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+    icp = ops.ICP(index, q.to(ctx.device))
+    oi = ora.F32Index(tgt.numpy())
+    for T in (np.eye(4), T_true):
+        acc, ci, cd = icp.step(T, 0.25, corr=True)
+        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+        ei, ed = oi.correspond(q.numpy(), R, t, 0.25)
+        assert np.array_equal(ci.cpu().numpy(), ei)
+        eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
+        gacc = acc.cpu().numpy()
+        assert gacc[0] == eacc[0]
+        assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * np.abs(eacc[:23]).max())
     icp.close()
     index.close()
 
