@@ -17,7 +17,10 @@
 // quantisation bound); tests exclude that band.  Rows are in index (scan) order, the
 // reference's unsorted mode.  Normals: fp32 sums of the neighbours' offsets from the query
 // (n, S, S S^T), the covariance formed in fp64, then the F1 eigen core (pca.hpp).
+#include <algorithm>
+#include <climits>
 #include <cmath>
+#include <cstdlib>
 
 #include "grid.hpp"
 #include "pca.hpp"
@@ -28,6 +31,9 @@ namespace {
 constexpr int kB = 256;
 #ifndef PCP_H16_BATCH  // candidate records loaded per batch in the row passes
 #define PCP_H16_BATCH 4
+#endif
+#ifndef PCP_H16_TILE_DEFAULT  // 1: the LDS-staged row kernels (k_h16_tile); 0: one lane per point, global loads
+#define PCP_H16_TILE_DEFAULT 1
 #endif
 #ifndef PCP_H16_NOSTORE  // profiling variant: the fill pass without its row stores
 #define PCP_H16_NOSTORE 0
@@ -136,98 +142,40 @@ __global__ __launch_bounds__(kB) void k_h16_rows_to_caller(const int32_t* inv, i
     }
 }
 
-// count pass (FILL = false): count[caller] = the row length; with cnt_s, also the row length
-// padded to 4 at the sorted position (0 for points that are not queries) and inv[caller] = s,
-// which the fill pass then takes instead of gathering them back from the caller offsets
+// A query's running row: its hit count and, in the fill pass, the hits staged four to a 16-byte
+// store into its sorted-order row (rows padded to 4) and the fp32 sums of the hits' offsets
+// from the query (the F1 plane's n, S, S S^T), in visiting (= index) order.
 template <bool FILL>
-__global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, const int64_t* __restrict__ offsets,
-                                                   const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
-                                                   pcp_plane* __restrict__ out_nrm, int32_t* __restrict__ cnt_s = nullptr,
-                                                   int32_t* __restrict__ inv = nullptr) {
-    const GridDesc& g = a.g;
-    const uint2* __restrict__ rec = a.rec;
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < a.n; s += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t caller = a.mapping[s];
-        if (caller >= a.n_owned) {
-            if (!FILL && cnt_s) cnt_s[s] = 0;
-            continue;
-        }
-        const uint2 qr = a.rec[s];
-        const float qx = h_lo(qr.x), qy = h_hi(qr.x), qz = h_lo(qr.y);
-        const uint32_t cid = a.cell[s];
-        const int cx = (int)(cid % (uint32_t)g.n[0]);
-        const int cy = (int)((cid / (uint32_t)g.n[0]) % (uint32_t)g.n[1]);
-        const int cz = (int)(cid / ((uint32_t)g.n[0] * (uint32_t)g.n[1]));
-        // distances to the faces of the query's cell (offsets can round a hair outside [0, h])
-        const float gxl = fmaxf(qx, 0.f), gxr = fmaxf(a.hf - qx, 0.f);
-        const float gyl = fmaxf(qy, 0.f), gyr = fmaxf(a.hf - qy, 0.f);
-        const float gzl = fmaxf(qz, 0.f), gzr = fmaxf(a.hf - qz, 0.f);
-        int64_t o = 0;
-        if (FILL) o = offsets[s];  // the sorted-order staging rows
-        uint32_t cnt = 0;
-        int32_t sink = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        float S0 = 0.f, S1 = 0.f, S2 = 0.f, S00 = 0.f, S01 = 0.f, S02 = 0.f, S11 = 0.f, S12 = 0.f, S22 = 0.f;
-        for (int dz = -1; dz <= 1; dz++) {
-            const int z = cz + dz;
-            if (z < 0 || z >= g.n[2]) continue;
-            const float gz = dz < 0 ? gzl : (dz > 0 ? gzr : 0.f);
-            for (int dy = -1; dy <= 1; dy++) {
-                const int y = cy + dy;
-                if (y < 0 || y >= g.n[1]) continue;
-                const float gy = dy < 0 ? gyl : (dy > 0 ? gyr : 0.f);
-                const float gyz = __fmaf_rn(gy, gy, gz * gz);
-                if (gyz >= a.rcut2) continue;
-                const int xa = (cx > 0 && __fmaf_rn(gxl, gxl, gyz) < a.rcut2) ? cx - 1 : cx;
-                const int xb = (cx + 1 < g.n[0] && __fmaf_rn(gxr, gxr, gyz) < a.rcut2) ? cx + 1 : cx;
-                const int64_t c0 = dense_id(g, xa, y, z), cq = dense_id(g, cx, y, z);
-                const uint32_t k0 = g.cstart[c0], k1 = g.cstart[c0 + (xb - xa + 1)];
-                const uint32_t b1 = g.cstart[cq], b2 = g.cstart[cq + 1];  // the query's x column
-                const float ey = (float)dy * a.hf - qy, ez = (float)dz * a.hf - qz;
-                // batches of NB candidates: the loads are issued together (the hit path's stores
-                // would otherwise order every later load behind them)
-                constexpr int NB = PCP_H16_BATCH;
-                for (uint32_t k = k0; k < k1; k += NB) {
-                    uint2 pr[NB];
-                    int32_t idv[NB];
-#pragma unroll
-                    for (int u = 0; u < NB; u++) {
-                        const uint32_t kk = min(k + (uint32_t)u, k1 - 1u);
-                        pr[u] = rec[kk];
-                        if (FILL) idv[u] = ids[kk];
-                    }
-#pragma unroll
-                    for (int u = 0; u < NB; u++) {
-                        const uint32_t kk = k + (uint32_t)u;
-                        const float dxc = kk < b1 ? -a.hf : (kk < b2 ? 0.f : a.hf);
-                        const float dx = dxc + (h_lo(pr[u].x) - qx);
-                        const float dy_ = ey + h_hi(pr[u].x);
-                        const float dz_ = ez + h_lo(pr[u].y);
-                        const float d2 = __fmaf_rn(dz_, dz_, __fmaf_rn(dy_, dy_, dx * dx));
-                        if (kk < k1 && d2 < a.r2) {
-                            if (FILL) {
+struct H16Acc {
+    int64_t o = 0;  // the row's start in the staging rows (fill)
+    uint32_t cnt = 0;
+    int32_t sink = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    float S0 = 0.f, S1 = 0.f, S2 = 0.f, S00 = 0.f, S01 = 0.f, S02 = 0.f, S11 = 0.f, S12 = 0.f, S22 = 0.f;
+    __device__ __forceinline__ void hit(float dx, float dy, float dz, int32_t id, int32_t* __restrict__ out_idx) {
+        if (FILL) {
 #if PCP_H16_NOSTORE
-                                sink ^= idv[u];
+            sink ^= id;
 #else
-                                // four hits per 16-byte store (the staging rows are padded to 4)
-                                const int32_t id = idv[u];
-                                const uint32_t slot = cnt & 3u;
-                                w0 = slot == 0 ? id : w0;
-                                w1 = slot == 1 ? id : w1;
-                                w2 = slot == 2 ? id : w2;
-                                w3 = slot == 3 ? id : w3;
-                                if (slot == 3) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
+            const uint32_t slot = cnt & 3u;
+            w0 = slot == 0 ? id : w0;
+            w1 = slot == 1 ? id : w1;
+            w2 = slot == 2 ? id : w2;
+            w3 = slot == 3 ? id : w3;
+            if (slot == 3) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
 #endif
-                                S0 += dx; S1 += dy_; S2 += dz_;
-                                S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy_, S01); S02 = __fmaf_rn(dx, dz_, S02);
-                                S11 = __fmaf_rn(dy_, dy_, S11); S12 = __fmaf_rn(dy_, dz_, S12); S22 = __fmaf_rn(dz_, dz_, S22);
-                            }
-                            cnt++;
-                        }
-                    }
-                }
-
-            }
+            S0 += dx; S1 += dy; S2 += dz;
+            S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy, S01); S02 = __fmaf_rn(dx, dz, S02);
+            S11 = __fmaf_rn(dy, dy, S11); S12 = __fmaf_rn(dy, dz, S12); S22 = __fmaf_rn(dz, dz, S22);
         }
+        cnt++;
+    }
+    // count: the row length (caller order) and, with cnt_s, the padded length at the sorted
+    // position + the inverse map; fill: the last partial store and the plane
+    __device__ __forceinline__ void finish(const H16Args& a, int64_t s, int32_t caller, int cx, int cy, int cz, float qx,
+                                           float qy, float qz, int32_t* count, int32_t* __restrict__ out_idx,
+                                           pcp_plane* __restrict__ out_nrm, int32_t* __restrict__ cnt_s,
+                                           int32_t* __restrict__ inv) {
+        const GridDesc& g = a.g;
         if (PCP_H16_NOSTORE && FILL && sink == 0x7fffffff) out_idx[o] = sink;
         if (!PCP_H16_NOSTORE && FILL && (cnt & 3u)) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
         if (!FILL) {
@@ -253,6 +201,301 @@ __global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, co
             out_nrm[caller] = pl;
         }
     }
+};
+
+// count pass (FILL = false): count[caller] = the row length; with cnt_s, also the row length
+// padded to 4 at the sorted position (0 for points that are not queries) and inv[caller] = s,
+// which the fill pass then takes instead of gathering them back from the caller offsets.
+// One query (sorted position s, an owned point) with global candidate loads: the per-lane kernel
+// and the tile kernel's lanes whose neighbourhood does not fit its LDS.
+template <bool FILL>
+__device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t caller, int32_t* count,
+                                          const int64_t* __restrict__ offsets, const int32_t* __restrict__ ids,
+                                          int32_t* __restrict__ out_idx, pcp_plane* __restrict__ out_nrm,
+                                          int32_t* __restrict__ cnt_s, int32_t* __restrict__ inv) {
+    const GridDesc& g = a.g;
+    const uint2* __restrict__ rec = a.rec;
+    const uint2 qr = a.rec[s];
+    const float qx = h_lo(qr.x), qy = h_hi(qr.x), qz = h_lo(qr.y);
+    const uint32_t cid = a.cell[s];
+    const int cx = (int)(cid % (uint32_t)g.n[0]);
+    const int cy = (int)((cid / (uint32_t)g.n[0]) % (uint32_t)g.n[1]);
+    const int cz = (int)(cid / ((uint32_t)g.n[0] * (uint32_t)g.n[1]));
+    // distances to the faces of the query's cell (offsets can round a hair outside [0, h])
+    const float gxl = fmaxf(qx, 0.f), gxr = fmaxf(a.hf - qx, 0.f);
+    const float gyl = fmaxf(qy, 0.f), gyr = fmaxf(a.hf - qy, 0.f);
+    const float gzl = fmaxf(qz, 0.f), gzr = fmaxf(a.hf - qz, 0.f);
+    H16Acc<FILL> acc;
+    if (FILL) acc.o = offsets[s];  // the sorted-order staging rows
+    for (int dz = -1; dz <= 1; dz++) {
+        const int z = cz + dz;
+        if (z < 0 || z >= g.n[2]) continue;
+        const float gz = dz < 0 ? gzl : (dz > 0 ? gzr : 0.f);
+        for (int dy = -1; dy <= 1; dy++) {
+            const int y = cy + dy;
+            if (y < 0 || y >= g.n[1]) continue;
+            const float gy = dy < 0 ? gyl : (dy > 0 ? gyr : 0.f);
+            const float gyz = __fmaf_rn(gy, gy, gz * gz);
+            if (gyz >= a.rcut2) continue;
+            const int xa = (cx > 0 && __fmaf_rn(gxl, gxl, gyz) < a.rcut2) ? cx - 1 : cx;
+            const int xb = (cx + 1 < g.n[0] && __fmaf_rn(gxr, gxr, gyz) < a.rcut2) ? cx + 1 : cx;
+            const int64_t c0 = dense_id(g, xa, y, z), cq = dense_id(g, cx, y, z);
+            const uint32_t k0 = g.cstart[c0], k1 = g.cstart[c0 + (xb - xa + 1)];
+            const uint32_t b1 = g.cstart[cq], b2 = g.cstart[cq + 1];  // the query's x column
+            const float ey = (float)dy * a.hf - qy, ez = (float)dz * a.hf - qz;
+            // batches of NB candidates: the loads are issued together (the hit path's stores
+            // would otherwise order every later load behind them)
+            constexpr int NB = PCP_H16_BATCH;
+            for (uint32_t k = k0; k < k1; k += NB) {
+                uint2 pr[NB];
+                int32_t idv[NB];
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const uint32_t kk = min(k + (uint32_t)u, k1 - 1u);
+                    pr[u] = rec[kk];
+                    if (FILL) idv[u] = ids[kk];
+                }
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const uint32_t kk = k + (uint32_t)u;
+                    const float dxc = kk < b1 ? -a.hf : (kk < b2 ? 0.f : a.hf);
+                    const float dx = dxc + (h_lo(pr[u].x) - qx);
+                    const float dy_ = ey + h_hi(pr[u].x);
+                    const float dz_ = ez + h_lo(pr[u].y);
+                    const float d2 = __fmaf_rn(dz_, dz_, __fmaf_rn(dy_, dy_, dx * dx));
+                    if (kk < k1 && d2 < a.r2) acc.hit(dx, dy_, dz_, FILL ? idv[u] : 0, out_idx);
+                }
+            }
+
+        }
+    }
+    acc.finish(a, s, caller, cx, cy, cz, qx, qy, qz, count, out_idx, out_nrm, cnt_s, inv);
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, const int64_t* __restrict__ offsets,
+                                                   const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
+                                                   pcp_plane* __restrict__ out_nrm, int32_t* __restrict__ cnt_s = nullptr,
+                                                   int32_t* __restrict__ inv = nullptr) {
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < a.n; s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t caller = a.mapping[s];
+        if (caller >= a.n_owned) {
+            if (!FILL && cnt_s) cnt_s[s] = 0;
+            continue;
+        }
+        h16_point<FILL>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
+    }
+}
+
+// ---- LDS-staged form (the default): a wave takes 64 consecutive sorted points -- cell order,
+// so runs along x-rows of cells -- stages every point of the union of their 3x3x3 cell
+// neighbourhoods into LDS once (coalesced row runs of the dense table, fp16 offsets widened to
+// fp32 once per staged point, plus the reported id in the fill pass), and each lane then walks
+// ITS OWN pruned cells of that list: a per-lane list of (LDS run, cell offset) entries in
+// ascending cell order (so rows stay in index order), built after the staged points.  The
+// per-candidate arithmetic is the per-lane kernel's (same formula, same visiting order): rows
+// and normals are identical to it, while the candidate loads are LDS reads instead of one
+// scattered global load per lane and candidate (the address path bound the per-lane form).
+// A wave whose union box does not fit splits at its runs of lanes in one (y, z) row of cells;
+// a run that still does not fit takes the per-lane global search.
+constexpr int kH16Cap = 1024;    // staged points per wave (16 B each: fp32 offsets + id)
+constexpr int kH16Rows = 192;    // (y, z) rows of a staged box
+struct H16Box {
+    int x0, x1, y0, y1, z0, z1, ny, nrow;
+    uint32_t total;  // points in the box (0xffffffff: too many rows)
+};
+__device__ __forceinline__ int h16_wmin(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int h16_wmax(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ void h16_wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// the union of the 3x3x3 neighbourhoods of the lanes with `in` set; with `write`, each (y, z)
+// row's run of the dense table (global start, LDS start) into s_rs / s_rb
+__device__ __forceinline__ H16Box h16_box(const GridDesc& g, int cx, int cy, int cz, bool in, int lane,
+                                          uint32_t* s_rs, uint32_t* s_rb, bool write) {
+    H16Box b;
+    b.x0 = max(h16_wmin(in ? cx : INT_MAX) - 1, 0), b.x1 = min(h16_wmax(in ? cx : INT_MIN) + 1, g.n[0] - 1);
+    b.y0 = max(h16_wmin(in ? cy : INT_MAX) - 1, 0), b.y1 = min(h16_wmax(in ? cy : INT_MIN) + 1, g.n[1] - 1);
+    b.z0 = max(h16_wmin(in ? cz : INT_MAX) - 1, 0), b.z1 = min(h16_wmax(in ? cz : INT_MIN) + 1, g.n[2] - 1);
+    b.ny = b.y1 - b.y0 + 1;
+    b.nrow = b.ny * (b.z1 - b.z0 + 1);
+    b.total = 0xffffffffu;
+    if (b.nrow > kH16Rows || b.x1 < b.x0) return b;
+    uint32_t carry = 0;
+    for (int r0 = 0; r0 < b.nrow; r0 += 64) {
+        const int r = r0 + lane;
+        uint32_t st = 0, cnt = 0;
+        if (r < b.nrow) {
+            const int y = b.y0 + r % b.ny, z = b.z0 + r / b.ny;
+            st = g.cstart[dense_id(g, b.x0, y, z)];
+            cnt = g.cstart[dense_id(g, b.x1, y, z) + 1] - st;
+        }
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        if (write && r < b.nrow) {
+            s_rs[r] = st;
+            s_rb[r] = carry + inc - cnt;
+        }
+        carry += __shfl(inc, 63, 64);
+    }
+    if (write && lane == 0) s_rb[b.nrow] = carry;
+    b.total = carry;
+    return b;
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(64) void k_h16_tile(H16Args a, int32_t* count, const int64_t* __restrict__ offsets,
+                                                 const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
+                                                 pcp_plane* __restrict__ out_nrm, int32_t* __restrict__ cnt_s,
+                                                 int32_t* __restrict__ inv, unsigned long long* stats) {
+    __shared__ float4 s_p[kH16Cap];
+    __shared__ uint32_t s_rs[kH16Rows], s_rb[kH16Rows + 1];
+    const GridDesc& g = a.g;
+    const int lane = threadIdx.x;
+    for (int64_t c = blockIdx.x; c * 64 < a.n; c += gridDim.x) {
+        const int64_t s = c * 64 + lane;
+        const bool valid = s < a.n;
+        const int32_t caller = valid ? a.mapping[s] : INT_MAX;
+        const bool act = valid && caller < a.n_owned;
+        if (!FILL && valid && !act && cnt_s) cnt_s[s] = 0;
+        uint2 qr = make_uint2(0u, 0u);
+        uint32_t cid = 0;
+        if (act) {
+            qr = a.rec[s];
+            cid = a.cell[s];
+        }
+        const float qx = h_lo(qr.x), qy = h_hi(qr.x), qz = h_lo(qr.y);
+        const int cx = (int)(cid % (uint32_t)g.n[0]);
+        const int cy = (int)((cid / (uint32_t)g.n[0]) % (uint32_t)g.n[1]);
+        const int cz = (int)(cid / ((uint32_t)g.n[0] * (uint32_t)g.n[1]));
+        // groups: the whole wave when its box fits, else its runs of lanes in one (y, z) row
+        int grp = 0, G = 1;
+        bool over = false;  // this lane's group does not fit: the global search
+        if (h16_box(g, cx, cy, cz, act, lane, s_rs, s_rb, false).total > (uint32_t)kH16Cap) {
+            const uint32_t row = cid / (uint32_t)g.n[0];  // (y, z) row id
+            const uint32_t prev = (uint32_t)__shfl_up((int)row, 1, 64);
+            const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+            const uint64_t heads = __ballot(lane == 0 || row != prev);
+            grp = __popcll(heads & below) - 1;
+            G = __popcll(heads);
+            for (int gi = 0; gi < G; gi++) {
+                const bool in = act && grp == gi;
+                if (!__ballot(in)) continue;
+                if (h16_box(g, cx, cy, cz, in, lane, s_rs, s_rb, false).total > (uint32_t)kH16Cap)
+                    over = over || grp == gi;
+            }
+        }
+        if (stats && lane == 0) {
+            atomicAdd(stats + 0, (unsigned long long)G);
+            atomicAdd(stats + 1, (unsigned long long)__popcll(__ballot(over && act)));
+        }
+        for (int gi = 0; gi < G; gi++) {
+            const bool mine = act && grp == gi && !over;
+            if (!__ballot(mine)) continue;
+            h16_wave_fence();  // the previous group's readers are done with the LDS
+            const H16Box b = h16_box(g, cx, cy, cz, mine, lane, s_rs, s_rb, true);
+            const uint32_t total = b.total;
+            h16_wave_fence();
+            const int nrow = b.nrow;
+            for (uint32_t e = lane; e < total; e += 64) {
+                int r = 0;
+#pragma unroll
+                for (int stp = 128; stp > 0; stp >>= 1)
+                    r = (r + stp < nrow && s_rb[r + stp] <= e) ? r + stp : r;
+                const uint32_t pos = s_rs[r] + (e - s_rb[r]);
+                const uint2 pr = a.rec[pos];
+                s_p[e] = make_float4(h_lo(pr.x), h_hi(pr.x), h_lo(pr.y), FILL ? __int_as_float(ids[pos]) : 0.f);
+            }
+            // the lane's cells: rows pruned by the query's distance to the cell faces (as the
+            // per-lane form), each as (LDS run start, end, cell offset + 1 per axis) in ascending
+            // cell order; pass 1 counts them, pass 2 (from the caches) writes them
+            const float gxl = fmaxf(qx, 0.f), gxr = fmaxf(a.hf - qx, 0.f);
+            const float gyl = fmaxf(qy, 0.f), gyr = fmaxf(a.hf - qy, 0.f);
+            const float gzl = fmaxf(qz, 0.f), gzr = fmaxf(a.hf - qz, 0.f);
+            uint32_t* const s_w = reinterpret_cast<uint32_t*>(s_p) + 4 * total;
+            auto cells = [&](bool write, int j) {
+                int m = 0;
+                for (int dz = -1; dz <= 1; dz++) {
+                    const int z = cz + dz;
+                    const float gz = dz < 0 ? gzl : (dz > 0 ? gzr : 0.f);
+                    for (int dy = -1; dy <= 1; dy++) {
+                        const int y = cy + dy;
+                        const float gy = dy < 0 ? gyl : (dy > 0 ? gyr : 0.f);
+                        const float gyz = __fmaf_rn(gy, gy, gz * gz);
+                        if (!mine || z < 0 || z >= g.n[2] || y < 0 || y >= g.n[1] || gyz >= a.rcut2) continue;
+                        const bool xl = cx > 0 && __fmaf_rn(gxl, gxl, gyz) < a.rcut2;
+                        const bool xr = cx + 1 < g.n[0] && __fmaf_rn(gxr, gxr, gyz) < a.rcut2;
+                        const int64_t cq = dense_id(g, cx, y, z);
+                        const uint32_t b1 = g.cstart[cq], b2 = g.cstart[cq + 1];
+                        const uint32_t b0 = xl ? g.cstart[cq - 1] : b1, b3 = xr ? g.cstart[cq + 2] : b2;
+                        const int r = (y - b.y0) + (z - b.z0) * b.ny;
+                        const uint32_t base = s_rb[r] - s_rs[r];  // LDS index = global position + base
+                        const uint32_t code = (uint32_t)(dy + 1) << 24 | (uint32_t)(dz + 1) << 26;
+                        if (b1 > b0) { if (write) s_w[j + m] = (b0 + base) | (b1 + base) << 11 | code; m++; }
+                        if (b2 > b1) { if (write) s_w[j + m] = (b1 + base) | (b2 + base) << 11 | code | 1u << 22; m++; }
+                        if (b3 > b2) { if (write) s_w[j + m] = (b2 + base) | (b3 + base) << 11 | code | 2u << 22; m++; }
+                    }
+                }
+                return m;
+            };
+            const int nc = cells(false, 0);
+            int excl = nc;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t2 = __shfl_up(excl, o, 64);
+                if (lane >= o) excl += t2;
+            }
+            const int tot = __shfl(excl, 63, 64);
+            excl -= nc;
+            if (4 * total + (uint32_t)tot > 4u * kH16Cap) {  // no room for the cell lists
+                if (mine) h16_point<FILL>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
+                if (stats && lane == 0) atomicAdd(stats + 2, 1ull);
+                continue;
+            }
+            cells(true, excl);
+            h16_wave_fence();
+            H16Acc<FILL> acc;
+            if (FILL && mine) acc.o = offsets[s];
+            uint32_t rp = (uint32_t)excl, rend = (uint32_t)(excl + nc);
+            uint32_t e = 0, ee = 0;
+            float dxc = 0.f, ey = 0.f, ez = 0.f;
+            for (;;) {
+                if (e >= ee && rp < rend) {
+                    const uint32_t w = s_w[rp++];
+                    e = w & 0x7ffu;
+                    ee = (w >> 11) & 0x7ffu;
+                    dxc = (float)((int)((w >> 22) & 3u) - 1) * a.hf;
+                    ey = (float)((int)((w >> 24) & 3u) - 1) * a.hf - qy;
+                    ez = (float)((int)((w >> 26) & 3u) - 1) * a.hf - qz;
+                }
+                const bool on = e < ee;
+                if (__ballot(on) == 0) break;
+                const float4 p = s_p[on ? e : 0u];
+                const float dx = dxc + (p.x - qx);
+                const float dy_ = ey + p.y;
+                const float dz_ = ez + p.z;
+                const float d2 = __fmaf_rn(dz_, dz_, __fmaf_rn(dy_, dy_, dx * dx));
+                if (on && d2 < a.r2) acc.hit(dx, dy_, dz_, __float_as_int(p.w), out_idx);
+                e += on ? 1u : 0u;
+            }
+            if (mine) acc.finish(a, s, caller, cx, cy, cz, qx, qy, qz, count, out_idx, out_nrm, cnt_s, inv);
+        }
+        if (over && act) h16_point<FILL>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
+    }
 }
 
 __global__ void k_h16_plane_default(pcp_plane* out, int64_t n) {
@@ -274,6 +517,13 @@ H16Args make_args(const pcp_index* ix, float r, int64_t n_owned) {
     a.rcut2 = rc * rc;
     return a;
 }
+
+// the LDS-staged kernel (1, default) or the per-lane global one (PCP_H16_TILE=0, for A/B)
+bool h16_tile_mode() {
+    const char* e = getenv("PCP_H16_TILE");
+    return e ? atoi(e) != 0 : PCP_H16_TILE_DEFAULT != 0;
+}
+unsigned tile_blocks(int64_t n) { return (unsigned)std::min<int64_t>(std::max<int64_t>((n + 63) / 64, 1), 1 << 20); }
 
 int check_query(pcp_ctx* ctx, const pcp_index* ix, float r, int64_t n_owned) {
     if (!ix || !ix->is_h16) return set_error(ctx, PCP_ERR_ARG, "not an fp16 (pcp_index_build_h16) index");
@@ -341,9 +591,14 @@ int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_
         PCP_TRY(dmalloc(ix->owner, &ixm->h16_inv, (size_t)n_owned));
         ixm->h16_inv_cap = n_owned;
     }
-    hipLaunchKernelGGL(k_h16_radius<false>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, count_dev,
-                       (const int64_t*)nullptr, (const int32_t*)nullptr, (int32_t*)nullptr, (pcp_plane*)nullptr,
-                       ixm->h16_cnt_s, ixm->h16_inv);
+    if (h16_tile_mode())
+        hipLaunchKernelGGL(k_h16_tile<false>, dim3(tile_blocks(ix->n)), dim3(64), 0, ctx->stream, a, count_dev,
+                           (const int64_t*)nullptr, (const int32_t*)nullptr, (int32_t*)nullptr, (pcp_plane*)nullptr,
+                           ixm->h16_cnt_s, ixm->h16_inv, (unsigned long long*)nullptr);
+    else
+        hipLaunchKernelGGL(k_h16_radius<false>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, count_dev,
+                           (const int64_t*)nullptr, (const int32_t*)nullptr, (int32_t*)nullptr, (pcp_plane*)nullptr,
+                           ixm->h16_cnt_s, ixm->h16_inv);
     PCP_LAUNCH_CHECK(ctx);
     ixm->h16_last_r = radius;
     ixm->h16_last_owned = n_owned;
@@ -389,8 +644,13 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
     }
     PCP_LAUNCH_CHECK(ctx);
     PCP_TRY(scan_i32_to_i64(ctx, cnt_use, ix->n, soff, nullptr));
-    hipLaunchKernelGGL(k_h16_radius<true>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, (int32_t*)nullptr,
-                       (const int64_t*)soff, (const int32_t*)ids, tmp, normals_dev);
+    if (h16_tile_mode())
+        hipLaunchKernelGGL(k_h16_tile<true>, dim3(tile_blocks(ix->n)), dim3(64), 0, ctx->stream, a, (int32_t*)nullptr,
+                           (const int64_t*)soff, (const int32_t*)ids, tmp, normals_dev, (int32_t*)nullptr,
+                           (int32_t*)nullptr, (unsigned long long*)nullptr);
+    else
+        hipLaunchKernelGGL(k_h16_radius<true>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a,
+                           (int32_t*)nullptr, (const int64_t*)soff, (const int32_t*)ids, tmp, normals_dev);
     hipLaunchKernelGGL(k_h16_rows_to_caller, dim3(grid_for(n_owned, kB, 1 << 16)), dim3(kB), 0, ctx->stream,
                        inv_use, n_owned, (const int64_t*)soff, offsets_dev, (const int32_t*)tmp, idx_dev);
     PCP_LAUNCH_CHECK(ctx);

@@ -24,3 +24,11 @@ for r in rows:
         other[k] = other.get(k, 0.0) + d(r)
 for k, v in sorted(other.items(), key=lambda kv: -kv[1])[:12]:
     print(f"  other {v:9.0f} us  {k}")
+# the pre-iteration span (index build + query sort) of that registration, by kernel
+pre = {}
+for r in rows:
+    if prev <= int(r["Start_Timestamp"]) < start:
+        k = r["Kernel_Name"].split("(")[0][:70]
+        pre[k] = pre.get(k, 0.0) + d(r)
+for k, v in sorted(pre.items(), key=lambda kv: -kv[1])[:16]:
+    print(f"  pre   {v:9.0f} us  {k}")
