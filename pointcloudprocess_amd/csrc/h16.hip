@@ -35,6 +35,9 @@ constexpr int kB = 256;
 #ifndef PCP_H16_TILE_DEFAULT  // 1: the LDS-staged row kernels (k_h16_tile); 0: one lane per point, global loads
 #define PCP_H16_TILE_DEFAULT 1
 #endif
+#ifndef PCP_H16_DIRECT_DEFAULT  // tile fill: rows straight to caller order through an LDS row buffer
+#define PCP_H16_DIRECT_DEFAULT 0
+#endif
 #ifndef PCP_H16_NOSTORE  // profiling variant: the fill pass without its row stores
 #define PCP_H16_NOSTORE 0
 #endif
@@ -145,14 +148,19 @@ __global__ __launch_bounds__(kB) void k_h16_rows_to_caller(const int32_t* inv, i
 // A query's running row: its hit count and, in the fill pass, the hits staged four to a 16-byte
 // store into its sorted-order row (rows padded to 4) and the fp32 sums of the hits' offsets
 // from the query (the F1 plane's n, S, S S^T), in visiting (= index) order.
-template <bool FILL>
+template <bool FILL, bool DIRECT = false>
 struct H16Acc {
-    int64_t o = 0;  // the row's start in the staging rows (fill)
+    int64_t o = 0;  // the row's start: in the staging rows, or (DIRECT) in the caller rows
     uint32_t cnt = 0;
     int32_t sink = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
     float S0 = 0.f, S1 = 0.f, S2 = 0.f, S00 = 0.f, S01 = 0.f, S02 = 0.f, S11 = 0.f, S12 = 0.f, S22 = 0.f;
     __device__ __forceinline__ void hit(float dx, float dy, float dz, int32_t id, int32_t* __restrict__ out_idx) {
-        if (FILL) {
+        if (FILL && DIRECT) {
+            out_idx[o + cnt] = id;  // caller order: one 4-byte store per hit (the tile kernel's rare path)
+            S0 += dx; S1 += dy; S2 += dz;
+            S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy, S01); S02 = __fmaf_rn(dx, dz, S02);
+            S11 = __fmaf_rn(dy, dy, S11); S12 = __fmaf_rn(dy, dz, S12); S22 = __fmaf_rn(dz, dz, S22);
+        } else if (FILL) {
 #if PCP_H16_NOSTORE
             sink ^= id;
 #else
@@ -169,6 +177,13 @@ struct H16Acc {
         }
         cnt++;
     }
+    // the fill's sums and count of a hit whose id is stored elsewhere (the tile kernel's LDS rows)
+    __device__ __forceinline__ void hit_sums_only(float dx, float dy, float dz) {
+        S0 += dx; S1 += dy; S2 += dz;
+        S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy, S01); S02 = __fmaf_rn(dx, dz, S02);
+        S11 = __fmaf_rn(dy, dy, S11); S12 = __fmaf_rn(dy, dz, S12); S22 = __fmaf_rn(dz, dz, S22);
+        cnt++;
+    }
     // count: the row length (caller order) and, with cnt_s, the padded length at the sorted
     // position + the inverse map; fill: the last partial store and the plane
     __device__ __forceinline__ void finish(const H16Args& a, int64_t s, int32_t caller, int cx, int cy, int cz, float qx,
@@ -176,8 +191,9 @@ struct H16Acc {
                                            pcp_plane* __restrict__ out_nrm, int32_t* __restrict__ cnt_s,
                                            int32_t* __restrict__ inv) {
         const GridDesc& g = a.g;
-        if (PCP_H16_NOSTORE && FILL && sink == 0x7fffffff) out_idx[o] = sink;
-        if (!PCP_H16_NOSTORE && FILL && (cnt & 3u)) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
+        if (PCP_H16_NOSTORE && FILL && !DIRECT && sink == 0x7fffffff) out_idx[o] = sink;
+        if (!PCP_H16_NOSTORE && FILL && !DIRECT && (cnt & 3u))
+            *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
         if (!FILL) {
             count[caller] = (int32_t)cnt;
             if (cnt_s) {
@@ -208,7 +224,7 @@ struct H16Acc {
 // which the fill pass then takes instead of gathering them back from the caller offsets.
 // One query (sorted position s, an owned point) with global candidate loads: the per-lane kernel
 // and the tile kernel's lanes whose neighbourhood does not fit its LDS.
-template <bool FILL>
+template <bool FILL, bool DIRECT = false>
 __device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t caller, int32_t* count,
                                           const int64_t* __restrict__ offsets, const int32_t* __restrict__ ids,
                                           int32_t* __restrict__ out_idx, pcp_plane* __restrict__ out_nrm,
@@ -225,8 +241,8 @@ __device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t c
     const float gxl = fmaxf(qx, 0.f), gxr = fmaxf(a.hf - qx, 0.f);
     const float gyl = fmaxf(qy, 0.f), gyr = fmaxf(a.hf - qy, 0.f);
     const float gzl = fmaxf(qz, 0.f), gzr = fmaxf(a.hf - qz, 0.f);
-    H16Acc<FILL> acc;
-    if (FILL) acc.o = offsets[s];  // the sorted-order staging rows
+    H16Acc<FILL, DIRECT> acc;
+    if (FILL) acc.o = DIRECT ? offsets[caller] : offsets[s];  // the caller rows, or the sorted-order staging rows
     for (int dz = -1; dz <= 1; dz++) {
         const int z = cz + dz;
         if (z < 0 || z >= g.n[2]) continue;
@@ -357,13 +373,16 @@ __device__ __forceinline__ H16Box h16_box(const GridDesc& g, int cx, int cy, int
     return b;
 }
 
-template <bool FILL>
+template <bool FILL, bool DIRECT = false>
 __global__ __launch_bounds__(64) void k_h16_tile(H16Args a, int32_t* count, const int64_t* __restrict__ offsets,
                                                  const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
                                                  pcp_plane* __restrict__ out_nrm, int32_t* __restrict__ cnt_s,
                                                  int32_t* __restrict__ inv, unsigned long long* stats) {
-    __shared__ float4 s_p[kH16Cap];
-    __shared__ uint32_t s_rs[kH16Rows], s_rb[kH16Rows + 1];
+    // staged points (<= kH16Cap), then the lanes' cell lists, then (DIRECT) the row buffer
+    constexpr int kCap = DIRECT ? 3 * kH16Cap / 2 : kH16Cap;
+    __shared__ float4 s_p[kCap];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rs[kH16Rows];  // (DIRECT: 64 int64 caller starts)
+    __shared__ uint32_t s_rb[kH16Rows + 1];
     const GridDesc& g = a.g;
     const int lane = threadIdx.x;
     for (int64_t c = blockIdx.x; c * 64 < a.n; c += gridDim.x) {
@@ -461,15 +480,41 @@ __global__ __launch_bounds__(64) void k_h16_tile(H16Args a, int32_t* count, cons
             }
             const int tot = __shfl(excl, 63, 64);
             excl -= nc;
-            if (4 * total + (uint32_t)tot > 4u * kH16Cap) {  // no room for the cell lists
-                if (mine) h16_point<FILL>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
+            if (4 * total + (uint32_t)tot > 4u * kCap) {  // no room for the cell lists
+                if (mine) h16_point<FILL, DIRECT>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
                 if (stats && lane == 0) atomicAdd(stats + 2, 1ull);
                 continue;
             }
             cells(true, excl);
+            // DIRECT fill: the rows go straight to their caller positions.  Each lane's hits are
+            // appended (as 16-bit staged-list indices) to its run of an LDS row buffer after the
+            // cell lists -- the run's length is its count, known from the count pass -- and the
+            // wave then writes the 64 rows flat, lane t taking elements t, t + 64, ... (consecutive
+            // lanes, consecutive addresses of one row: full-line writes), instead of staging rows
+            // in sorted order and copying them to caller order in another pass.  A group whose rows
+            // do not fit stores each hit at its caller position from the lane.
+            int64_t dst = 0;
+            uint32_t rcnt = 0, rb = 0, rtot = 0;
+            bool rbuf = false;
+            uint16_t* const s_h = reinterpret_cast<uint16_t*>(s_w + tot);
+            if (DIRECT) {
+                if (mine) {
+                    dst = offsets[caller];
+                    rcnt = (uint32_t)(offsets[caller + 1] - dst);
+                }
+                uint32_t inc = rcnt;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t t2 = __shfl_up(inc, o, 64);
+                    if (lane >= o) inc += t2;
+                }
+                rtot = __shfl(inc, 63, 64);
+                rb = inc - rcnt;
+                rbuf = 4 * total + (uint32_t)tot + (rtot + 1) / 2 <= 4u * kCap;
+            }
             h16_wave_fence();
-            H16Acc<FILL> acc;
-            if (FILL && mine) acc.o = offsets[s];
+            H16Acc<FILL, DIRECT> acc;
+            if (FILL && mine) acc.o = DIRECT ? dst : offsets[s];
             uint32_t rp = (uint32_t)excl, rend = (uint32_t)(excl + nc);
             uint32_t e = 0, ee = 0;
             float dxc = 0.f, ey = 0.f, ez = 0.f;
@@ -489,12 +534,34 @@ __global__ __launch_bounds__(64) void k_h16_tile(H16Args a, int32_t* count, cons
                 const float dy_ = ey + p.y;
                 const float dz_ = ez + p.z;
                 const float d2 = __fmaf_rn(dz_, dz_, __fmaf_rn(dy_, dy_, dx * dx));
-                if (on && d2 < a.r2) acc.hit(dx, dy_, dz_, __float_as_int(p.w), out_idx);
+                if (on && d2 < a.r2) {
+                    if (DIRECT && rbuf) {  // (the row length is the count pass's: never past it)
+                        if (acc.cnt < rcnt) s_h[rb + acc.cnt] = (uint16_t)e;
+                        acc.hit_sums_only(dx, dy_, dz_);
+                    } else if (!DIRECT || acc.cnt < rcnt) {
+                        acc.hit(dx, dy_, dz_, __float_as_int(p.w), out_idx);
+                    }
+                }
                 e += on ? 1u : 0u;
+            }
+            if (DIRECT && rbuf) {
+                // the wave writes its rows: per-lane (LDS start, caller start) staged, then flat
+                uint32_t* const s_rb0 = s_rb;  // reuse: the box's row table is no longer read
+                int64_t* const s_dst = reinterpret_cast<int64_t*>(s_rs);
+                h16_wave_fence();
+                s_rb0[lane] = rb;
+                if (lane == 0) s_rb0[64] = rtot;
+                s_dst[lane] = dst;
+                h16_wave_fence();
+                int r = 0;
+                for (uint32_t t = lane; t < rtot; t += 64) {
+                    while (s_rb0[r + 1] <= t) r++;
+                    out_idx[s_dst[r] + (t - s_rb0[r])] = __float_as_int(s_p[s_h[t]].w);
+                }
             }
             if (mine) acc.finish(a, s, caller, cx, cy, cz, qx, qy, qz, count, out_idx, out_nrm, cnt_s, inv);
         }
-        if (over && act) h16_point<FILL>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
+        if (over && act) h16_point<FILL, DIRECT>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
     }
 }
 
@@ -522,6 +589,12 @@ H16Args make_args(const pcp_index* ix, float r, int64_t n_owned) {
 bool h16_tile_mode() {
     const char* e = getenv("PCP_H16_TILE");
     return e ? atoi(e) != 0 : PCP_H16_TILE_DEFAULT != 0;
+}
+// the tile fill writes rows straight to caller order (1) or stages them for the copy pass (0);
+// PCP_H16_DIRECT for A/B
+bool h16_direct_mode() {
+    const char* e = getenv("PCP_H16_DIRECT");
+    return e ? atoi(e) != 0 : PCP_H16_DIRECT_DEFAULT != 0;
 }
 unsigned tile_blocks(int64_t n) { return (unsigned)std::min<int64_t>(std::max<int64_t>((n + 63) / 64, 1), 1 << 20); }
 
@@ -627,10 +700,17 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
         ~Free() { dfree(c, *a); dfree(c, *b); dfree(c, *d); dfree(c, *e); dfree(c, *f); }
     } fr{ctx, &ids, &cnt_s, &inv, &tmp, &soff};
     PCP_TRY(dmalloc(ctx, &ids, (size_t)ix->n));
-    PCP_TRY(dmalloc(ctx, &soff, (size_t)ix->n + 1));
-    PCP_TRY(dmalloc(ctx, &tmp, (size_t)total + 3 * (size_t)n_owned + 4));  // rows padded to 4
     hipLaunchKernelGGL(k_h16_ids, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, (const int32_t*)ix->mapping,
                        global_id_dev, ix->n, ids);
+    if (h16_tile_mode() && h16_direct_mode()) {  // rows straight into the caller's CSR (no staging, no copy)
+        hipLaunchKernelGGL((k_h16_tile<true, true>), dim3(tile_blocks(ix->n)), dim3(64), 0, ctx->stream, a,
+                           (int32_t*)nullptr, offsets_dev, (const int32_t*)ids, idx_dev, normals_dev, (int32_t*)nullptr,
+                           (int32_t*)nullptr, (unsigned long long*)nullptr);
+        PCP_LAUNCH_CHECK(ctx);
+        return PCP_OK;
+    }
+    PCP_TRY(dmalloc(ctx, &soff, (size_t)ix->n + 1));
+    PCP_TRY(dmalloc(ctx, &tmp, (size_t)total + 3 * (size_t)n_owned + 4));  // rows padded to 4
     // the sorted-order row lengths and the inverse map: kept by the count pass of this radius and
     // query set, else gathered back from the caller offsets
     const int32_t *cnt_use = ix->h16_cnt_s, *inv_use = ix->h16_inv;
@@ -645,7 +725,7 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
     PCP_LAUNCH_CHECK(ctx);
     PCP_TRY(scan_i32_to_i64(ctx, cnt_use, ix->n, soff, nullptr));
     if (h16_tile_mode())
-        hipLaunchKernelGGL(k_h16_tile<true>, dim3(tile_blocks(ix->n)), dim3(64), 0, ctx->stream, a, (int32_t*)nullptr,
+        hipLaunchKernelGGL((k_h16_tile<true, false>), dim3(tile_blocks(ix->n)), dim3(64), 0, ctx->stream, a, (int32_t*)nullptr,
                            (const int64_t*)soff, (const int32_t*)ids, tmp, normals_dev, (int32_t*)nullptr,
                            (int32_t*)nullptr, (unsigned long long*)nullptr);
     else

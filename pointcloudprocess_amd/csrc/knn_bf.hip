@@ -46,6 +46,9 @@ constexpr int kBlock = 64 * kWaves;
 #ifndef PCP_BF_SIGN  // 1: thresholds in the MFMA's C operand, sign-bit hit test; 0: compares
 #define PCP_BF_SIGN 1
 #endif
+#ifndef PCP_BF_GROUP  // sub-tiles per hit test (1: every step)
+#define PCP_BF_GROUP 1
+#endif
 constexpr int kTile = PCP_BF_TILE;     // targets staged in LDS per step
 constexpr int kPerThread = kTile / kBlock;
 
@@ -246,6 +249,66 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
 #pragma unroll
             for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf0, PCP_BF_C(b), 0, 0, 0);
         }
+#if PCP_BF_SIGN && PCP_BF_GROUP > 1
+        // the hit test once per PCP_BF_GROUP sub-tiles, software-pipelined by whole groups: the
+        // next group's MFMAs are issued (independent: C = -thr, no accumulation) before this
+        // group's 4 x SG outputs are OR-ed into one sign word (v_or3_b32), so no test waits on an
+        // MFMA issued just before it; only a group with a hit walks its sub-tiles one by one
+        constexpr int SG = PCP_BF_GROUP;
+        constexpr int NSUB = kTile / 16;
+        static_assert(NSUB % SG == 0, "sub-tiles per group");
+        f32x4 gn[SG][QB];
+#pragma unroll
+        for (int u = 0; u < SG; u++) {
+            const float bfr = tf[(u * 16 + cls) * 4 + grp];
+#pragma unroll
+            for (int b = 0; b < QB; b++) gn[u][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfr, nthr[b], 0, 0, 0);
+        }
+        for (int sub0 = 0; sub0 < NSUB; sub0 += SG) {
+            f32x4 cg[SG][QB];
+#pragma unroll
+            for (int u = 0; u < SG; u++)
+#pragma unroll
+                for (int b = 0; b < QB; b++) cg[u][b] = gn[u][b];
+            if (sub0 + SG < NSUB) {
+#pragma unroll
+                for (int u = 0; u < SG; u++) {
+                    const float bfr = tf[((sub0 + SG + u) * 16 + cls) * 4 + grp];
+#pragma unroll
+                    for (int b = 0; b < QB; b++)
+                        gn[u][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfr, nthr[b], 0, 0, 0);
+                }
+            }
+            uint32_t sg = 0;
+#pragma unroll
+            for (int u = 0; u < SG; u++)
+#pragma unroll
+                for (int b = 0; b < QB; b++)
+                    sg |= __float_as_uint(cg[u][b][0]) | __float_as_uint(cg[u][b][1]) | __float_as_uint(cg[u][b][2]) |
+                          __float_as_uint(cg[u][b][3]);
+            if ((int32_t)sg < 0) {
+#pragma unroll
+                for (int u = 0; u < SG; u++) {
+                    const int sub = sub0 + u;
+                    const int tidx = tb + sub * 16 + cls;
+                    const float4 p = tile[sub * 16 + cls];
+#pragma unroll
+                    for (int b = 0; b < QB; b++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            if ((int32_t)__float_as_uint(cg[u][b][r]) >= 0) continue;
+                            const float x = __fmaf_rn(qm[b][r][2], p.z, __fmaf_rn(qm[b][r][1], p.y,
+                                                      __fmaf_rn(qm[b][r][0], p.x, p.w)));
+                            if (x < thr[b][r]) {
+                                list_insert<L>(ls[b][r], lt[b][r], x, tidx);
+                                thr[b][r] = fminf(ls[b][r][L - 1], thr[b][r]);
+                                nthr[b][r] = -thr[b][r];
+                            }
+                        }
+                }
+            }
+        }
+#else
 #pragma unroll PCP_BF_UNROLL
         for (int sub = 0; sub < kTile / 16; sub++) {
             f32x4 c[QB];
@@ -303,6 +366,7 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
             }
 #endif
         }
+#endif
 #undef PCP_BF_C
         // refresh theta after tiles 1, 2, 4, 8, ... (rank of each class best in its group)
         if (use_theta && ((tt + 1) & tt) == 0) {

@@ -136,3 +136,34 @@ def test_h16_fill_after_another_count(ctx, scene):
     assert torch.equal(idx2[:total.value].cpu(), idx.cpu())
     assert torch.equal(nrm2.cpu().view(torch.int32), nrm.cpu().view(torch.int32))
     ix.close()
+
+
+def test_h16_tile_matches_per_lane_kernel(ctx, scene, monkeypatch):
+    """The LDS-staged row kernels (default) against the per-lane global-load kernels
+    (PCP_H16_TILE=0): same rows in the same order and the same normals, byte for byte (same
+    per-candidate arithmetic and visiting order); both are checked against the oracle above."""
+    from pointcloudprocess_amd import ops
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PCP_H16_TILE", mode)
+        ix = ops.H16Index(ctx, torch.from_numpy(scene).to(ctx.device), cell_size=R)
+        offs, idx, nrm = ix.radius_normals(R)
+        out[mode] = (offs.cpu(), idx.cpu(), nrm.cpu().view(torch.int32))
+        ix.close()
+    for a, b in zip(out["1"], out["0"]):
+        assert torch.equal(a, b)
+
+
+def test_h16_direct_fill_matches_staged(ctx, scene, monkeypatch):
+    """The tile fill writing rows straight to caller order through its LDS row buffer
+    (PCP_H16_DIRECT=1) against the staged rows + copy pass (0): byte-identical CSR and normals."""
+    from pointcloudprocess_amd import ops
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PCP_H16_DIRECT", mode)
+        ix = ops.H16Index(ctx, torch.from_numpy(scene).to(ctx.device), cell_size=R)
+        offs, idx, nrm = ix.radius_normals(R)
+        out[mode] = (offs.cpu(), idx.cpu(), nrm.cpu().view(torch.int32))
+        ix.close()
+    for a, b in zip(out["1"], out["0"]):
+        assert torch.equal(a, b)

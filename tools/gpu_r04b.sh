@@ -1,30 +1,23 @@
-# Round-4 GPU call: the whole GPU suite (incl. the full-size C2/C3/C5 parity tests), a C3 A/B of the
-# per-lane window scan (PCP_TILE_LANE 1 vs 0, interleaved) with its debug counters, the C4 bench
-# line and kernel trace, and counters of the C2/C3/C5 lines: HBM traffic (FETCH_SIZE / WRITE_SIZE
-# passes) and the SQ instruction / cycle set (two passes) per kernel.
+# Round-4 GPU call B: the 2-rank one-GPU rehearsal (per-rank pre-iteration / iterations spans in the
+# line), a C2 A/B of the grouped hit test (variants/bfg4, PCP_BF_GROUP=4, interleaved, with the
+# brute-force tests on the variant), then the PMC passes of the C3/C5/C2 lines (HBM traffic and the
+# SQ instruction / cycle set per kernel).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/${TAG:-r04a}; mkdir -p $O
-if [ -z "$NOTEST" ]; then
-timeout -k 10 1100 python3 -u -m pytest tests -m gpu -x -v -s --timeout 900 --timeout-method thread ${TESTS:-} > $O/gpu_tests.log 2>&1
+O=gpurun_out/${TAG:-r04b}; mkdir -p $O
+if [ -z "$NOREH" ]; then
+PCP_BENCH_DEVICE=0 PCP_BENCH_BACKEND=gloo timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --points 5000000 --no-cpu > $O/rehearsal_2rank.json 2> $O/rehearsal_2rank.err
 fi
-if [ -z "$NOAB" ]; then
-PCP_KNN_DEBUG=1 timeout -k 10 200 python3 -u bench.py --config C3 --no-cpu --steps 1 --warmup 0 > $O/c3_debug.json 2> $O/c3_debug.err
+if [ -z "$NOC2" ] && [ -f variants/bfg4/libpcp.so ]; then
+PCP_LIB=$GRAFT_REPO_ROOT/variants/bfg4/libpcp.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_bruteforce.py -x -q --timeout 120 --timeout-method thread > $O/c2_bfg4_tests.log 2>&1
 for i in 1 2; do
-  for l in 1 0; do
-    PCP_TILE_LANE=$l timeout -k 10 200 python3 -u bench.py --config C3 --no-cpu --steps 5 >> $O/c3_ab_lane$l.jsonl 2>> $O/c3_ab.err
-  done
-done
-for i in 1 2; do
-  for t in 1 0 D; do
-    if [ $t = D ]; then T=1; DI=1; else T=$t; DI=0; fi
-    PCP_H16_TILE=$T PCP_H16_DIRECT=$DI timeout -k 10 200 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_tile$t.jsonl 2>> $O/c5_ab.err
+  for v in default bfg4; do
+    if [ $v = default ]; then L=""; else L=$GRAFT_REPO_ROOT/variants/$v/libpcp.so; fi
+    PCP_LIB=$L timeout -k 10 200 python3 -u bench.py --config C2 --no-cpu --steps 5 >> $O/c2_ab_$v.jsonl 2>> $O/c2_ab.err
   done
 done
 fi
-timeout -k 10 300 python3 -u bench.py --no-cpu --steps 5 > $O/bench_C4.json 2> $O/bench_C4.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu --steps 2 --warmup 1 > $O/trace_bench.log 2>&1
-python3 tools/trace_iters.py $O/trace > $O/per_iteration.txt 2>&1 || true
 if [ -z "$NOPMC" ]; then
 sq1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_VALU"
 sq2="SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU_MFMA_F32 SQ_WAVES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
