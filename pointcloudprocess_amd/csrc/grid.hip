@@ -296,6 +296,28 @@ __global__ void k_cell_keys_rec(GridDesc g, const float* cxyz, size_t stride_f, 
     }
 }
 
+// (PCP_TSORT_IDX variant of the fp32 build) the cell key and the point's own index; the sorted
+// records are gathered once afterwards (k_gather_rec) instead of riding through every radix pass
+__global__ void k_cell_keys_idx(GridDesc g, const float* cxyz, size_t stride_f, int64_t n, uint32_t* key,
+                                uint32_t* idx) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int cx, cy, cz;
+        cell_of_point<float>(g, cxyz + stride_f * i, cx, cy, cz);
+        key[i] = (uint32_t)cell_id(g, cx, cy, cz);
+        idx[i] = (uint32_t)i;
+    }
+}
+__global__ void k_gather_rec(const float* cxyz, size_t stride_f, const int32_t* mapping, const uint32_t* idx,
+                             int64_t n, float4* rec) {
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = idx[s];
+        const float* p = cxyz + stride_f * i;
+        rec[s] = make_float4(p[0], p[1], p[2], __int_as_float(mapping ? mapping[i] : (int32_t)i));
+    }
+}
+
 // Radix-sort build: key = cell id (cstart index) of each compacted point, value = its
 // internal index.  A stable LSD sort then yields cell order with ties in input order
 // (deterministic); dense mode also flags the point's brick for the two-level search.
@@ -354,6 +376,16 @@ bool make_geometry(GridDesc& g, const double mn[3], const double mx[3], double h
     }
     g.nbricks = nb;
     return true;
+}
+
+#ifndef PCP_TSORT_IDX_DEFAULT
+#define PCP_TSORT_IDX_DEFAULT 0
+#endif
+// fp32 build: sort (cell id, index) pairs and gather the records (PCP_TSORT_IDX=1, A/B) or carry
+// the 16-byte records through the radix passes (0)
+bool tsort_idx() {
+    const char* e = getenv("PCP_TSORT_IDX");
+    return e ? atoi(e) != 0 : PCP_TSORT_IDX_DEFAULT != 0;
 }
 
 template <typename T>
@@ -540,6 +572,23 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
                 if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
                     PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u,
                                                            bits, st));
+            } else if (tsort_idx()) {
+                // (key, index) pairs through the radix passes, then one gather of the records
+                const float* src = direct ? (const float*)xyz : (const float*)cxyz;
+                const size_t sf = direct ? stride / sizeof(float) : (size_t)3;
+                uint32_t *i0 = nullptr, *i1 = nullptr;
+                if (!(rc = dmalloc(ctx, &i0, n)) && !(rc = dmalloc(ctx, &i1, n))) {
+                    hipLaunchKernelGGL(k_cell_keys_idx, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, src, sf, n, skey, i0);
+                    PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, i0, i1, (size_t)n, 0u, bits, st));
+                    if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
+                        PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, i0, i1, (size_t)n, 0u, bits, st));
+                    if (!rc)
+                        hipLaunchKernelGGL(k_gather_rec, dim3(grid_for(n, kB)), dim3(kB), 0, st, src, sf,
+                                           direct ? (const int32_t*)nullptr : (const int32_t*)ix->mapping,
+                                           (const uint32_t*)i1, n, (float4*)ix->pts);
+                }
+                dfree(ctx, i0);
+                dfree(ctx, i1);
             } else {
                 // no brick marks: the fp32 index serves ICP only, whose dense-grid searches never
                 // read brick occupancy (its brick table stays all-zero = "occupied")

@@ -2265,7 +2265,45 @@ __global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_
     }
 }
 
+// (PCP_QSORT_IDX variant) the sort key and the query's own index only; the sorted records are
+// then gathered once (k_gather_queries) instead of riding through every radix pass
+__global__ void k_query_keys_idx(GridDesc g, const float* q, size_t stride_f, int64_t n, uint32_t* key,
+                                 uint32_t* idx) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float* p = q + (size_t)i * stride_f;
+        const float x = p[0], y = p[1], z = p[2];
+        uint32_t k = query_key_end(g);
+        if (isfinite(x) && isfinite(y) && isfinite(z)) {
+            const int cx = clampi((int)floorf(cell_f<float>(g, x, 0) - 0.5f), 0, g.n[0] - 1);
+            const int cy = clampi((int)floorf(cell_f<float>(g, y, 1) - 0.5f), 0, g.n[1] - 1);
+            const int cz = clampi((int)floorf(cell_f<float>(g, z, 2) - 0.5f), 0, g.n[2] - 1);
+            if (PCP_QBRICK != 4) {
+                constexpr int B = PCP_QBRICK;
+                const int64_t b = ((int64_t)(cz / B) * qbricks(g, 1) + cy / B) * qbricks(g, 0) + cx / B;
+                k = (uint32_t)(b * B * B * B + ((cz % B) * B + cy % B) * B + cx % B);
+            } else {
+                k = PCP_QKEY_LOCAL ? (uint32_t)(brick_of(g, cx, cy, cz) * 64 + local_of(cx, cy, cz))
+                                   : (uint32_t)brick_of(g, cx, cy, cz);
+            }
+        }
+        key[i] = k;
+        idx[i] = (uint32_t)i;
+    }
+}
+__global__ void k_gather_queries(const float* q, size_t stride_f, const uint32_t* idx, int64_t n, QXyz* q3,
+                                 int32_t* qi) {
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = idx[s];
+        const float* p = q + (size_t)i * stride_f;
+        q3[s] = QXyz{p[0], p[1], p[2]};
+        qi[s] = (int32_t)i;
+    }
+}
+
 // the first query of each query brick (PCP_QBRICK^3 cells) in the sorted keys (finite keys only)
+#ifndef PCP_QSORT_IDX_DEFAULT  // query sort: (key, index) pairs + one gather (1) or 16-byte records as payload (0)
+#define PCP_QSORT_IDX_DEFAULT 0
+#endif
 #ifndef PCP_VER_DENSE  // verify: failures per 64-query chunk from which the whole chunk is searched (0: off)
 #define PCP_VER_DENSE 0
 #endif
@@ -2682,15 +2720,33 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
         if (!rc) rc = pcp::dmalloc(ctx, &d_cnt, 2);
         if (!rc && hipMemsetAsync(d_cnt, 0, 2 * sizeof(unsigned long long), st) != hipSuccess)
             rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
+        // PCP_QSORT_IDX=1 (A/B): sort (key, u32 index) pairs and gather the records once, instead
+        // of carrying the 16-byte records through every radix pass
+        const char* qsi = std::getenv("PCP_QSORT_IDX");
+        const bool sort_idx = qsi ? std::atoi(qsi) != 0 : PCP_QSORT_IDX_DEFAULT != 0;
+        uint32_t *i0 = nullptr, *i1 = nullptr;
         if (!rc && nq > 0) {
-            hipLaunchKernelGGL(pcp::k_query_keys, dim3(pcp::grid_for(nq, 256)), dim3(256), 0, st, target->g, q,
-                               q_stride / sizeof(float), nq, k0, r0);
             unsigned bits = 1;  // keys are in [0, query_key_end]
             while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)pcp::query_key_end(target->g)) bits++;
             size_t tb = 0;
-            hipError_t e = rocprim::radix_sort_pairs<pcp::RecSortConfig>(nullptr, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
-            if (e == hipSuccess && !(rc = pcp::dmalloc(ctx, (char**)&tmp, tb)))
-                e = rocprim::radix_sort_pairs<pcp::RecSortConfig>(tmp, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
+            hipError_t e = hipSuccess;
+            if (sort_idx) {
+                rc = pcp::dmalloc(ctx, &i0, nq);
+                if (!rc) rc = pcp::dmalloc(ctx, &i1, nq);
+                if (!rc) {
+                    hipLaunchKernelGGL(pcp::k_query_keys_idx, dim3(pcp::grid_for(nq, 256)), dim3(256), 0, st, target->g,
+                                       q, q_stride / sizeof(float), nq, k0, i0);
+                    e = rocprim::radix_sort_pairs(nullptr, tb, k0, k1, i0, i1, (size_t)nq, 0u, bits, st);
+                    if (e == hipSuccess && !(rc = pcp::dmalloc(ctx, (char**)&tmp, tb)))
+                        e = rocprim::radix_sort_pairs(tmp, tb, k0, k1, i0, i1, (size_t)nq, 0u, bits, st);
+                }
+            } else {
+                hipLaunchKernelGGL(pcp::k_query_keys, dim3(pcp::grid_for(nq, 256)), dim3(256), 0, st, target->g, q,
+                                   q_stride / sizeof(float), nq, k0, r0);
+                e = rocprim::radix_sort_pairs<pcp::RecSortConfig>(nullptr, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
+                if (e == hipSuccess && !(rc = pcp::dmalloc(ctx, (char**)&tmp, tb)))
+                    e = rocprim::radix_sort_pairs<pcp::RecSortConfig>(tmp, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
+            }
             if (!rc && e == hipSuccess)
                 hipLaunchKernelGGL(pcp::k_first_at_least, dim3(1), dim3(1), 0, st, k1, nq,
                                    pcp::query_key_end(target->g), d_cnt);
@@ -2729,10 +2785,16 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
         if (!rc) rc = pcp::dmalloc(ctx, &q3, nq + 1);
         if (!rc) rc = pcp::dmalloc(ctx, &qi, nq + 1);
         if (!rc && nfin > 0) {
-            hipLaunchKernelGGL(pcp::k_split_queries, dim3(pcp::grid_for(nfin, 256)), dim3(256), 0, st, (const float4*)qs,
-                               nfin, q3, qi);
+            if (sort_idx)
+                hipLaunchKernelGGL(pcp::k_gather_queries, dim3(pcp::grid_for(nfin, 256)), dim3(256), 0, st, q,
+                                   q_stride / sizeof(float), (const uint32_t*)i1, nfin, q3, qi);
+            else
+                hipLaunchKernelGGL(pcp::k_split_queries, dim3(pcp::grid_for(nfin, 256)), dim3(256), 0, st,
+                                   (const float4*)qs, nfin, q3, qi);
             if (hipGetLastError() != hipSuccess) rc = pcp::set_error(ctx, PCP_ERR_HIP, "query split");
         }
+        pcp::dfree(ctx, i0);
+        pcp::dfree(ctx, i1);
         pcp::dfree(ctx, k0);
         pcp::dfree(ctx, k1);
         pcp::dfree(ctx, r0);

@@ -18,6 +18,14 @@ for i in 1 2; do
   done
 done
 fi
+if [ -z "$NOSORT" ]; then
+PCP_QSORT_IDX=1 PCP_TSORT_IDX=1 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_icp.py tests/test_gpu_c4_scale.py -x -q --timeout 300 --timeout-method thread > $O/sortidx_tests.log 2>&1
+for i in 1 2 3; do
+  for v in 00 11 10 01; do
+    PCP_QSORT_IDX=${v:0:1} PCP_TSORT_IDX=${v:1:1} timeout -k 10 200 python3 -u bench.py --no-cpu --steps 5 >> $O/c4_sort_ab_$v.jsonl 2>> $O/c4_sort_ab.err
+  done
+done
+fi
 if [ -z "$NOPMC" ]; then
 sq1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_VALU"
 sq2="SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU_MFMA_F32 SQ_WAVES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
