@@ -12,6 +12,7 @@
 // score >= tau = min_c(L-th best of class c), so d2 >= |q|^2 + tau - E (E bounds the fp32
 // rounding).  A query whose k-th exact d2 is not below that bound is re-done by an exact
 // fp64 scan (k_bf_fallback) -- the result is exact either way.
+#include <algorithm>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -45,6 +46,9 @@ constexpr int kBlock = 64 * kWaves;
 #endif
 #ifndef PCP_BF_SIGN  // 1: thresholds in the MFMA's C operand, sign-bit hit test; 0: compares
 #define PCP_BF_SIGN 1
+#endif
+#ifndef PCP_BF_GLDS  // 1: target tiles staged by LDS-DMA into two LDS buffers; 0: through registers
+#define PCP_BF_GLDS 0
 #endif
 #ifndef PCP_BF_GROUP  // sub-tiles per hit test (1: every step)
 #define PCP_BF_GROUP 1
@@ -90,6 +94,11 @@ __global__ __launch_bounds__(256) void k_bf_targets(const double* t, size_t stri
     }
 }
 
+// the padding of the last target tile: never ranked (|p|^2 = +inf)
+__global__ void k_bf_pad(float4* t4, int64_t n) {
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) t4[i] = make_float4(0.f, 0.f, 0.f, INFINITY);
+}
+
 struct BfArgs {
     const float4* t4;
     const double* t;
@@ -131,7 +140,11 @@ __device__ __forceinline__ void group_min(double& d, int& j) {
 // QB blocks of 16 queries per wave; L = per-(row, class) list length.
 template <int L, int QB, int W>
 __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
+#if PCP_BF_GLDS
+    __shared__ float4 tiles[2][kTile];  // LDS-DMA double buffer (no staging registers)
+#else
     __shared__ float4 tile[kTile];
+#endif
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int cls = lane & 15, grp = lane >> 4;
@@ -214,6 +227,26 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
     const bool use_theta = a.kk <= 16;
 
     const int64_t ntiles = (a.nt + kTile - 1) / kTile;
+#if PCP_BF_GLDS
+    // global -> LDS directly (global_load_lds_dwordx4: wave-uniform LDS base + lane * 16 B), one
+    // tile ahead into the other buffer; the target array is padded to whole tiles with
+    // never-ranked records, so every lane's source address is valid
+    auto fetch = [&](int64_t tb, int buf) {
+#pragma unroll
+        for (int u = 0; u < kPerThread; u++) {
+            const float4* src = a.t4 + tb + u * kBlock + threadIdx.x;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(&tiles[buf][u * kBlock] +
+                                                                                       (threadIdx.x & ~63u)),
+                                             16, 0, 0);
+        }
+    };
+    fetch(0, 0);
+    for (int64_t tt = 0; tt < ntiles; tt++) {
+        __syncthreads();  // tile tt has landed (vmcnt(0)); every wave is done with tile tt - 1
+        if (tt + 1 < ntiles) fetch((tt + 1) * kTile, (int)((tt + 1) & 1));
+        float4* const tile = tiles[tt & 1];
+#else
     float4 pre[kPerThread];
     auto fetch = [&](int64_t tb) {
 #pragma unroll
@@ -229,6 +262,7 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
         for (int u = 0; u < kPerThread; u++) tile[u * kBlock + threadIdx.x] = pre[u];
         __syncthreads();
         if (tt + 1 < ntiles) fetch((tt + 1) * kTile);
+#endif
         const int tb = (int)(tt * kTile);
         const float* tf = (const float*)tile;
 #if !PCP_BF_SIGN
@@ -257,10 +291,14 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
         constexpr int SG = PCP_BF_GROUP;
         constexpr int NSUB = kTile / 16;
         static_assert(NSUB % SG == 0, "sub-tiles per group");
+        // B fragments two groups ahead: the LDS reads of group g + 2 are issued while group g is
+        // tested, so the MFMAs of group g + 1 never wait on a read issued just before them
         f32x4 gn[SG][QB];
+        float bq[SG];
 #pragma unroll
         for (int u = 0; u < SG; u++) {
             const float bfr = tf[(u * 16 + cls) * 4 + grp];
+            bq[u] = tf[((SG + u) * 16 + cls) * 4 + grp];
 #pragma unroll
             for (int b = 0; b < QB; b++) gn[u][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfr, nthr[b], 0, 0, 0);
         }
@@ -273,10 +311,14 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
             if (sub0 + SG < NSUB) {
 #pragma unroll
                 for (int u = 0; u < SG; u++) {
-                    const float bfr = tf[((sub0 + SG + u) * 16 + cls) * 4 + grp];
+                    const float bfr = bq[u];
 #pragma unroll
                     for (int b = 0; b < QB; b++)
                         gn[u][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfr, nthr[b], 0, 0, 0);
+                }
+                if (sub0 + 2 * SG < NSUB) {
+#pragma unroll
+                    for (int u = 0; u < SG; u++) bq[u] = tf[((sub0 + 2 * SG + u) * 16 + cls) * 4 + grp];
                 }
             }
             uint32_t sg = 0;
@@ -534,13 +576,16 @@ int pcp_knn_bruteforce(pcp_ctx* ctx, const double* t, size_t tstride, int64_t nt
     int32_t* fb = nullptr;
     uint32_t* fbc = nullptr;
     const unsigned npb = grid_for(nt > 0 ? nt : 1, 256, 1024);
-    int rc = dmalloc(ctx, &t4, nt > 0 ? nt : 1);
+    const int64_t ntpad = std::max<int64_t>((nt + kTile - 1) / kTile * kTile, 1);  // whole tiles (LDS-DMA)
+    int rc = dmalloc(ctx, &t4, ntpad);
     if (!rc) rc = dmalloc(ctx, &part, 2 * (size_t)npb);
     if (!rc) rc = dmalloc(ctx, &fb, nq);
     if (!rc) rc = dmalloc(ctx, &fbc, 1);
     double pmax2 = 0.0, nfin = 0.0;
     if (!rc && nt > 0) {
         hipLaunchKernelGGL(k_bf_targets, dim3(npb), dim3(256), 0, st, t, tstride, nt, t4, part);
+        if (ntpad > nt)
+            hipLaunchKernelGGL(k_bf_pad, dim3(1), dim3(256), 0, st, t4 + nt, ntpad - nt);
         std::vector<double> h(2 * npb);
         hipError_t e = hipMemcpyAsync(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);

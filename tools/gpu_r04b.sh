@@ -9,10 +9,13 @@ if [ -z "$NOREH" ]; then
 PCP_BENCH_DEVICE=0 PCP_BENCH_BACKEND=gloo timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --points 5000000 --no-cpu > $O/rehearsal_2rank.json 2> $O/rehearsal_2rank.err
 fi
-if [ -z "$NOC2" ] && [ -f variants/bfg4/libpcp.so ]; then
-PCP_LIB=$GRAFT_REPO_ROOT/variants/bfg4/libpcp.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_bruteforce.py -x -q --timeout 120 --timeout-method thread > $O/c2_bfg4_tests.log 2>&1
+if [ -z "$NOC2" ]; then
+for v in ${C2V:-bfglds bfglds2 bfglds4}; do
+  [ -f variants/$v/libpcp.so ] || continue
+  PCP_LIB=$GRAFT_REPO_ROOT/variants/$v/libpcp.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_bruteforce.py -x -q --timeout 120 --timeout-method thread > $O/c2_${v}_tests.log 2>&1
+done
 for i in 1 2; do
-  for v in default bfg4; do
+  for v in default ${C2V:-bfglds bfglds2 bfglds4}; do
     if [ $v = default ]; then L=""; else L=$GRAFT_REPO_ROOT/variants/$v/libpcp.so; fi
     PCP_LIB=$L timeout -k 10 200 python3 -u bench.py --config C2 --no-cpu --steps 5 >> $O/c2_ab_$v.jsonl 2>> $O/c2_ab.err
   done
