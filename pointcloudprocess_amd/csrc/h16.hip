@@ -33,7 +33,7 @@ constexpr int kB = 256;
 #define PCP_H16_BATCH 4
 #endif
 #ifndef PCP_H16_TILE_DEFAULT  // 1: the LDS-staged row kernels (k_h16_tile); 0: one lane per point, global loads
-#define PCP_H16_TILE_DEFAULT 1
+#define PCP_H16_TILE_DEFAULT 0
 #endif
 #ifndef PCP_H16_DIRECT_DEFAULT  // tile fill: rows straight to caller order through an LDS row buffer
 #define PCP_H16_DIRECT_DEFAULT 0

@@ -20,7 +20,7 @@ other = {}
 for r in rows:
     if start <= int(r["Start_Timestamp"]) <= end and not any(k in r["Kernel_Name"] for k in
                                                                ("k_icp_octant", "k_icp_verify", "k_icp_ring", "k_icp_tier1")):
-        k = r["Kernel_Name"].split("(")[0][:60]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:60]
         other[k] = other.get(k, 0.0) + d(r)
 for k, v in sorted(other.items(), key=lambda kv: -kv[1])[:12]:
     print(f"  other {v:9.0f} us  {k}")
@@ -28,7 +28,7 @@ for k, v in sorted(other.items(), key=lambda kv: -kv[1])[:12]:
 pre = {}
 for r in rows:
     if prev <= int(r["Start_Timestamp"]) < start:
-        k = r["Kernel_Name"].split("(")[0][:70]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:70]
         pre[k] = pre.get(k, 0.0) + d(r)
 for k, v in sorted(pre.items(), key=lambda kv: -kv[1])[:16]:
     print(f"  pre   {v:9.0f} us  {k}")
