@@ -47,6 +47,9 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_TILE_MORTON  // tiled normals: queries in Morton order inside each brick (1) or index order (0)
 #define PCP_TILE_MORTON 1
 #endif
+#ifndef PCP_TILE_ROWTAB  // tiled normals: per-point row bytes in LDS (1) or binary searches of the row table (0)
+#define PCP_TILE_ROWTAB 0
+#endif
 #ifndef PCP_TILE_LANE_DEFAULT  // tiled normals: each lane scans its own window (1) or the union box (0)
 #define PCP_TILE_LANE_DEFAULT 1
 #endif
@@ -1008,6 +1011,9 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
     constexpr uint32_t kMax = 0xffffffffu;
     __shared__ uint2 s_u[kTileCap];
     __shared__ uint32_t s_rs[kTileRows], s_rb[kTileRows + 1];
+#if PCP_TILE_ROWTAB
+    __shared__ uint8_t s_row[kTileCap];  // the (y, z) row of each staged point
+#endif
     const int lane = threadIdx.x;
     for (int64_t c = blockIdx.x; c * 64 < n; c += gridDim.x) {
         const bool valid = c * 64 + lane < n;
@@ -1074,9 +1080,21 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                     r = (r + stp < nrow && s_rb[r + stp] <= e) ? r + stp : r;
                 return r;
             };
+#if PCP_TILE_ROWTAB
+            // e advances by 64 per step, so each lane's row only moves forward: a short walk
+            // instead of a binary search, and the row of every staged point is kept (one byte)
+            // for the re-rank's list index -> position lookups
+            int rw = 0;
+            for (uint32_t e = lane; e < total; e += 64) {
+                while (s_rb[rw + 1] <= e) rw++;
+                const int r = rw;
+                s_row[e] = (uint8_t)r;
+                const double4 p = pts[s_rs[r] + (e - s_rb[r])];
+#else
             for (uint32_t e = lane; e < total; e += 64) {
                 const int r = row_of(e);
                 const double4 p = pts[s_rs[r] + (e - s_rb[r])];
+#endif
                 s_u[e] = make_uint2((uint32_t)quant14(p.x - ox, inv) | ((uint32_t)quant14(p.y - oy, inv) << 16),
                                     (uint32_t)quant14(p.z - oz, inv));
             }
@@ -1126,31 +1144,47 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                         e2 = a + (cb - ca);
                     }
                 };
-                int nr = 0;  // pass 1: this lane's non-empty rows
-#pragma unroll 5
-                for (int i = 0; i < kW; i++) {
-                    uint32_t a, e2;
-                    row_run(i, a, e2);
-                    nr += e2 > a ? 1 : 0;
-                }
-                int excl = nr;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int t2 = __shfl_up(excl, o, 64);
-                    if (lane >= o) excl += t2;
-                }
-                const int tot_rows = __shfl(excl, 63, 64);
-                excl -= nr;
-                lane_path = 2 * total + (uint32_t)tot_rows <= 2u * kTileCap;
-                if (lane_path) {
-                    uint32_t* s_w = reinterpret_cast<uint32_t*>(s_u) + 2 * total;
-                    int j = excl;  // pass 2 (the cell starts again, now from the caches): write them
+                uint32_t* s_w = reinterpret_cast<uint32_t*>(s_u);
+                int nr = 0, excl = 0;
+                if (2 * total + 64u * kW <= 2u * kTileCap) {
+                    // room for a fixed kW-word region per lane at the end of the list (odd stride:
+                    // the lanes' reads of one slot fall in distinct banks): one pass of cell starts
+                    lane_path = true;
+                    excl = 2 * kTileCap - 64 * kW + lane * kW;
 #pragma unroll 5
                     for (int i = 0; i < kW; i++) {
                         uint32_t a, e2;
                         row_run(i, a, e2);
-                        if (e2 > a) s_w[j++] = a | (e2 << 16);
+                        if (e2 > a) s_w[excl + nr++] = a | (e2 << 16);
                     }
+                } else {
+#pragma unroll 5
+                    for (int i = 0; i < kW; i++) {  // pass 1: this lane's non-empty rows
+                        uint32_t a, e2;
+                        row_run(i, a, e2);
+                        nr += e2 > a ? 1 : 0;
+                    }
+                    excl = nr;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int t2 = __shfl_up(excl, o, 64);
+                        if (lane >= o) excl += t2;
+                    }
+                    const int tot_rows = __shfl(excl, 63, 64);
+                    excl -= nr;
+                    lane_path = 2 * total + (uint32_t)tot_rows <= 2u * kTileCap;
+                    if (lane_path) {  // compacted after the staged points
+                        excl += 2 * (int)total;
+                        int j = excl;  // pass 2 (the cell starts again, now from the caches): write them
+#pragma unroll 5
+                        for (int i = 0; i < kW; i++) {
+                            uint32_t a, e2;
+                            row_run(i, a, e2);
+                            if (e2 > a) s_w[j++] = a | (e2 << 16);
+                        }
+                    }
+                }
+                if (lane_path) {
                     wave_lds_fence();
                     uint32_t rp = (uint32_t)excl, rend = (uint32_t)(excl + nr);
                     uint32_t e = 0, ee = 0;
@@ -1211,7 +1245,11 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
             for (int i = 0; i < M; i++) {
                 const bool has = t[i] != kMax;
                 const uint32_t ei = t[i] & (uint32_t)(kTileCap - 1);
+#if PCP_TILE_ROWTAB
+                const int r = s_row[has ? ei : 0u];
+#else
                 const int r = row_of(has ? ei : 0u);
+#endif
                 P[i] = has ? s_rs[r] + (ei - s_rb[r]) : 0u;
                 D[i] = has ? l2_simple(q.x, q.y, q.z, pts[P[i]]) : INFINITY;
             }

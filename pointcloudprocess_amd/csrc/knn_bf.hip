@@ -48,7 +48,7 @@ constexpr int kBlock = 64 * kWaves;
 #define PCP_BF_SIGN 1
 #endif
 #ifndef PCP_BF_GLDS  // 1: target tiles staged by LDS-DMA into two LDS buffers; 0: through registers
-#define PCP_BF_GLDS 0
+#define PCP_BF_GLDS 1
 #endif
 #ifndef PCP_BF_GROUP  // sub-tiles per hit test (1: every step)
 #define PCP_BF_GROUP 1
