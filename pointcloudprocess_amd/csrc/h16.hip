@@ -38,6 +38,9 @@ constexpr int kB = 256;
 #ifndef PCP_H16_DIRECT_DEFAULT  // tile fill: rows straight to caller order through an LDS row buffer
 #define PCP_H16_DIRECT_DEFAULT 0
 #endif
+#ifndef PCP_H16_FLUSH16  // fill: hits gathered 16 to a 64-byte store through a per-lane LDS slot buffer (1) or 4 to a 16-byte store from registers (0)
+#define PCP_H16_FLUSH16 1
+#endif
 #ifndef PCP_H16_NOSTORE  // profiling variant: the fill pass without its row stores
 #define PCP_H16_NOSTORE 0
 #endif
@@ -65,6 +68,9 @@ __global__ void k_h16_convert(GridDesc g, const float4* pts, int64_t n, uint2* r
         mapping[i] = __float_as_int(p.w);
     }
 }
+
+// staging rows are padded to whole stores: 16 ids (64 B) with the LDS slot buffer, else 4 (16 B)
+constexpr uint32_t kRowPad = PCP_H16_FLUSH16 ? 16u : 4u;
 
 struct H16Args {
     GridDesc g;
@@ -95,7 +101,7 @@ __global__ void k_h16_sorted_counts(const int32_t* mapping, int64_t n, int64_t n
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
         const int32_t c = mapping[s];
         const bool own = c < n_owned;
-        cnt_s[s] = own ? (int32_t)((offsets[c + 1] - offsets[c] + 3) & ~3ll) : 0;  // 16-byte aligned rows
+        cnt_s[s] = own ? (int32_t)((offsets[c + 1] - offsets[c] + (kRowPad - 1)) & ~(int64_t)(kRowPad - 1)) : 0;
         if (own) inv[c] = (int32_t)s;
     }
 }
@@ -152,6 +158,8 @@ template <bool FILL, bool DIRECT = false>
 struct H16Acc {
     int64_t o = 0;  // the row's start: in the staging rows, or (DIRECT) in the caller rows
     uint32_t cnt = 0;
+    int32_t* slot = nullptr;  // (PCP_H16_FLUSH16 staging fill) this lane's 16 LDS slots, `stride` words apart
+    int stride = 0;
     int32_t sink = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
     float S0 = 0.f, S1 = 0.f, S2 = 0.f, S00 = 0.f, S01 = 0.f, S02 = 0.f, S11 = 0.f, S12 = 0.f, S22 = 0.f;
     __device__ __forceinline__ void hit(float dx, float dy, float dz, int32_t id, int32_t* __restrict__ out_idx) {
@@ -163,19 +171,33 @@ struct H16Acc {
         } else if (FILL) {
 #if PCP_H16_NOSTORE
             sink ^= id;
+#elif PCP_H16_FLUSH16
+            // 16 hits per 64-byte store group: the row's lines are written whole by this lane in
+            // one burst (16-byte pieces spread over time were written to HBM part by part: the
+            // fill's WRITE_SIZE was 2.8x its row bytes)
+            slot[(cnt & 15u) * stride] = id;
+            if ((cnt & 15u) == 15u) flush(out_idx, cnt & ~15u, 16u);
 #else
-            const uint32_t slot = cnt & 3u;
-            w0 = slot == 0 ? id : w0;
-            w1 = slot == 1 ? id : w1;
-            w2 = slot == 2 ? id : w2;
-            w3 = slot == 3 ? id : w3;
-            if (slot == 3) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
+            const uint32_t sl = cnt & 3u;
+            w0 = sl == 0 ? id : w0;
+            w1 = sl == 1 ? id : w1;
+            w2 = sl == 2 ? id : w2;
+            w3 = sl == 3 ? id : w3;
+            if (sl == 3) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
 #endif
             S0 += dx; S1 += dy; S2 += dz;
             S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy, S01); S02 = __fmaf_rn(dx, dz, S02);
             S11 = __fmaf_rn(dy, dy, S11); S12 = __fmaf_rn(dy, dz, S12); S22 = __fmaf_rn(dz, dz, S22);
         }
         cnt++;
+    }
+    // the first m (a multiple of 4 up to 16) slots to row entries [at, at + m)
+    __device__ __forceinline__ void flush(int32_t* __restrict__ out_idx, uint32_t at, uint32_t m) {
+#pragma unroll
+        for (uint32_t q = 0; q < 16u; q += 4u)
+            if (q < m)
+                *(int4*)(out_idx + o + at + q) = make_int4(slot[q * stride], slot[(q + 1) * stride],
+                                                           slot[(q + 2) * stride], slot[(q + 3) * stride]);
     }
     // the fill's sums and count of a hit whose id is stored elsewhere (the tile kernel's LDS rows)
     __device__ __forceinline__ void hit_sums_only(float dx, float dy, float dz) {
@@ -192,12 +214,14 @@ struct H16Acc {
                                            int32_t* __restrict__ inv) {
         const GridDesc& g = a.g;
         if (PCP_H16_NOSTORE && FILL && !DIRECT && sink == 0x7fffffff) out_idx[o] = sink;
-        if (!PCP_H16_NOSTORE && FILL && !DIRECT && (cnt & 3u))
+        if (!PCP_H16_NOSTORE && PCP_H16_FLUSH16 && FILL && !DIRECT && (cnt & 15u))
+            flush(out_idx, cnt & ~15u, ((cnt & 15u) + 3u) & ~3u);  // the padded tail
+        if (!PCP_H16_NOSTORE && !PCP_H16_FLUSH16 && FILL && !DIRECT && (cnt & 3u))
             *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
         if (!FILL) {
             count[caller] = (int32_t)cnt;
             if (cnt_s) {
-                cnt_s[s] = (int32_t)((cnt + 3u) & ~3u);  // 16-byte aligned staging rows
+                cnt_s[s] = (int32_t)((cnt + (kRowPad - 1)) & ~(kRowPad - 1));  // whole-store staging rows
                 inv[caller] = (int32_t)s;
             }
         } else if (out_nrm) {
@@ -228,7 +252,8 @@ template <bool FILL, bool DIRECT = false>
 __device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t caller, int32_t* count,
                                           const int64_t* __restrict__ offsets, const int32_t* __restrict__ ids,
                                           int32_t* __restrict__ out_idx, pcp_plane* __restrict__ out_nrm,
-                                          int32_t* __restrict__ cnt_s, int32_t* __restrict__ inv) {
+                                          int32_t* __restrict__ cnt_s, int32_t* __restrict__ inv, int32_t* slot,
+                                          int stride) {
     const GridDesc& g = a.g;
     const uint2* __restrict__ rec = a.rec;
     const uint2 qr = a.rec[s];
@@ -243,6 +268,8 @@ __device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t c
     const float gzl = fmaxf(qz, 0.f), gzr = fmaxf(a.hf - qz, 0.f);
     H16Acc<FILL, DIRECT> acc;
     if (FILL) acc.o = DIRECT ? offsets[caller] : offsets[s];  // the caller rows, or the sorted-order staging rows
+    acc.slot = slot;
+    acc.stride = stride;
     for (int dz = -1; dz <= 1; dz++) {
         const int z = cz + dz;
         if (z < 0 || z >= g.n[2]) continue;
@@ -293,13 +320,14 @@ __global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, co
                                                    const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
                                                    pcp_plane* __restrict__ out_nrm, int32_t* __restrict__ cnt_s = nullptr,
                                                    int32_t* __restrict__ inv = nullptr) {
+    __shared__ int32_t s_slot[(FILL && PCP_H16_FLUSH16) ? 16 * kB : 1];  // slot-major: conflict-free
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < a.n; s += (int64_t)gridDim.x * blockDim.x) {
         const int32_t caller = a.mapping[s];
         if (caller >= a.n_owned) {
             if (!FILL && cnt_s) cnt_s[s] = 0;
             continue;
         }
-        h16_point<FILL>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
+        h16_point<FILL>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv, s_slot + threadIdx.x, kB);
     }
 }
 
@@ -383,6 +411,7 @@ __global__ __launch_bounds__(64) void k_h16_tile(H16Args a, int32_t* count, cons
     __shared__ float4 s_p[kCap];
     __shared__ __attribute__((aligned(16))) uint32_t s_rs[kH16Rows];  // (DIRECT: 64 int64 caller starts)
     __shared__ uint32_t s_rb[kH16Rows + 1];
+    __shared__ int32_t s_slot[(FILL && PCP_H16_FLUSH16) ? 16 * 64 : 1];
     const GridDesc& g = a.g;
     const int lane = threadIdx.x;
     for (int64_t c = blockIdx.x; c * 64 < a.n; c += gridDim.x) {
@@ -481,7 +510,9 @@ __global__ __launch_bounds__(64) void k_h16_tile(H16Args a, int32_t* count, cons
             const int tot = __shfl(excl, 63, 64);
             excl -= nc;
             if (4 * total + (uint32_t)tot > 4u * kCap) {  // no room for the cell lists
-                if (mine) h16_point<FILL, DIRECT>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
+                if (mine)
+                    h16_point<FILL, DIRECT>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv,
+                                            s_slot + lane, 64);
                 if (stats && lane == 0) atomicAdd(stats + 2, 1ull);
                 continue;
             }
@@ -515,6 +546,8 @@ __global__ __launch_bounds__(64) void k_h16_tile(H16Args a, int32_t* count, cons
             h16_wave_fence();
             H16Acc<FILL, DIRECT> acc;
             if (FILL && mine) acc.o = DIRECT ? dst : offsets[s];
+            acc.slot = s_slot + lane;
+            acc.stride = 64;
             uint32_t rp = (uint32_t)excl, rend = (uint32_t)(excl + nc);
             uint32_t e = 0, ee = 0;
             float dxc = 0.f, ey = 0.f, ez = 0.f;
@@ -561,7 +594,8 @@ __global__ __launch_bounds__(64) void k_h16_tile(H16Args a, int32_t* count, cons
             }
             if (mine) acc.finish(a, s, caller, cx, cy, cz, qx, qy, qz, count, out_idx, out_nrm, cnt_s, inv);
         }
-        if (over && act) h16_point<FILL, DIRECT>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv);
+        if (over && act)
+            h16_point<FILL, DIRECT>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv, s_slot + lane, 64);
     }
 }
 
@@ -710,7 +744,7 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
         return PCP_OK;
     }
     PCP_TRY(dmalloc(ctx, &soff, (size_t)ix->n + 1));
-    PCP_TRY(dmalloc(ctx, &tmp, (size_t)total + 3 * (size_t)n_owned + 4));  // rows padded to 4
+    PCP_TRY(dmalloc(ctx, &tmp, (size_t)total + (kRowPad - 1) * (size_t)n_owned + kRowPad));  // padded rows
     // the sorted-order row lengths and the inverse map: kept by the count pass of this radius and
     // query set, else gathered back from the caller offsets
     const int32_t *cnt_use = ix->h16_cnt_s, *inv_use = ix->h16_inv;

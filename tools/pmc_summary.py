@@ -3,7 +3,9 @@
 
 FETCH_SIZE and WRITE_SIZE are in KB.  gfx950 correction (MI355X_MICROARCH.md, HBM section):
 FETCH_SIZE reports half the bytes of wide (16 B/lane) reads -> x2; WRITE_SIZE is exact.
-  python tools/pmc_summary.py <fetch_dir> <write_dir> [kernel-substring ...]
+  python tools/pmc_summary.py [--src=h16.hip] <fetch_dir> <write_dir> [kernel-name ...]
+(the sha1 of the named csrc source is recorded, so a bench line only quotes counters measured on
+the kernels it runs)
 """
 import collections
 import csv
@@ -25,8 +27,12 @@ def per_kernel(path, counter):
 
 
 def main():
-    fdir, wdir = sys.argv[1], sys.argv[2]
-    keys = sys.argv[3:] or ["k_icp_verify", "k_icp_octant", "k_icp_ring"]
+    args = sys.argv[1:]
+    src_rel = "icp.hip"
+    if args and args[0].startswith("--src="):  # the source whose kernels are summarised (sha1 recorded)
+        src_rel = args.pop(0)[len("--src="):]
+    fdir, wdir = args[0], args[1]
+    keys = args[2:] or ["k_icp_verify", "k_icp_octant", "k_icp_ring"]
     f, w = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
     out = {"source": f"{fdir}, {wdir}", "fetch_correction": 2.0, "kernels": {}}
     for k in keys:
@@ -36,8 +42,12 @@ def main():
             out["kernels"][k] = {"launches": len(fb), "fetch_bytes_avg": sum(fb) / len(fb),
                                  "write_bytes_avg": sum(wb) / len(wb) if wb else None}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    src = os.path.join(root, "pointcloudprocess_amd", "csrc", "icp.hip")
-    out["icp_hip_sha1"] = hashlib.sha1(open(src, "rb").read()).hexdigest()
+    src = os.path.join(root, "pointcloudprocess_amd", "csrc", src_rel)
+    sha = hashlib.sha1(open(src, "rb").read()).hexdigest()
+    if src_rel == "icp.hip":
+        out["icp_hip_sha1"] = sha
+    out["src"] = src_rel
+    out["src_sha1"] = sha
     print(json.dumps(out, indent=1))
 
 
