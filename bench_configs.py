@@ -50,6 +50,50 @@ class Timer:
 
 _ORA = {}
 
+# the kernels each config's timed call runs (their PMC traffic is the line's roofline.traffic)
+PMC_KERNELS = {
+    "C2": ("knn_bf.hip", ("k_bf_mfma", "k_bf_fallback", "k_bf_targets", "k_bf_pad")),
+    "C3": ("knn.hip", ("k_normals_tile", "k_normals", "k_normals_coop", "k_brick_keys", "k_plane_default")),
+    "C5": ("h16.hip", ("k_h16_radius", "k_h16_tile", "k_h16_rows_to_caller", "tile_scan", "k_h16_ids",
+                       "k_h16_plane_default", "k_h16_sorted_counts")),
+}
+
+
+def pmc_traffic(cfg, calls=1):
+    """HBM bytes per timed call (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction)
+    of the config's kernels, from the newest profiles/*/pmc_traffic_<cfg>.json measured on the
+    current source of those kernels (sha1 match), else None.  Made by tools/pmc_summary.py
+    --src=<file> from separate FETCH_SIZE / WRITE_SIZE passes of `bench.py --config <cfg> --steps 1
+    --warmup 0 --no-cpu` (one timed call)."""
+    import glob
+    import hashlib
+    src, kernels = PMC_KERNELS[cfg]
+    sha = hashlib.sha1(open(os.path.join(ROOT, "pointcloudprocess_amd", "csrc", src), "rb").read()).hexdigest()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_traffic_{cfg}.json")), key=os.path.getmtime,
+                    reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("src_sha1") != sha:
+            continue
+        tot = 0.0
+        for k in kernels:
+            e = d["kernels"].get(k)
+            if e is not None:
+                tot += e["launches"] * (e["fetch_bytes_avg"] + (e["write_bytes_avg"] or 0.0))
+        return tot / calls, os.path.relpath(f, ROOT)
+    return None
+
+
+def _with_traffic(roof, cfg):
+    t = pmc_traffic(cfg)
+    if roof is not None and t is not None:
+        roof["traffic"] = round(t[0] / (roof["kernel_avg_ms"] * 1e-3) / 1e9, 2)
+        roof["traffic_bytes_per_launch"] = round(t[0])
+        roof["traffic_source"] = t[1]
+    return roof
+
 
 def _oracle():
     """The oracle built -O3 -march=native on this host (bench.native_oracle); cpu legs only."""
@@ -339,7 +383,7 @@ def main(args):
         "data": "synthetic (seeded); every rank its own batch",
         "config": {"workload": info["workload"], "parallelism": f"x{world} independent batches, no collective"},
         "device_ms_per_step": round(timer.avg, 3),
-        "roofline": roof(timer.avg) if roof else None,
+        "roofline": _with_traffic(roof(timer.avg), args.config) if roof else None,
         "build_id": ctx.lib.pcp_build_id().decode(),  # SHA-1 of the libpcp sources (provenance)
         "cpu_baseline": None,
     }

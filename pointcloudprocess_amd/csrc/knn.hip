@@ -48,7 +48,7 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #define PCP_TILE_MORTON 1
 #endif
 #ifndef PCP_TILE_ROWTAB  // tiled normals: per-point row bytes in LDS (1) or binary searches of the row table (0)
-#define PCP_TILE_ROWTAB 0
+#define PCP_TILE_ROWTAB 1
 #endif
 #ifndef PCP_TILE_LANE_DEFAULT  // tiled normals: each lane scans its own window (1) or the union box (0)
 #define PCP_TILE_LANE_DEFAULT 1

@@ -3,7 +3,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-r04e}; mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_h16.py tests/test_gpu_fullsize.py -x -v -s --timeout 500 --timeout-method thread -k "h16 or c5" > $O/h16_tests.log 2>&1
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_h16.py tests/test_gpu_fullsize.py tests/test_gpu_knn.py -x -v -s --timeout 500 --timeout-method thread -k "h16 or c5 or c3 or normals" > $O/h16_tests.log 2>&1
 for i in 1 2; do
   for v in default flush4; do
     L=""; [ $v = flush4 ] && L=$GRAFT_REPO_ROOT/variants/flush4/libpcp.so
