@@ -41,6 +41,9 @@ constexpr int kB = 256;
 #ifndef PCP_H16_FLUSH16  // fill: hits gathered 16 to a 64-byte store through a per-lane LDS slot buffer (1) or 4 to a 16-byte store from registers (0)
 #define PCP_H16_FLUSH16 1
 #endif
+#ifndef PCP_H16_LATEID  // fill (per-lane kernel): ids gathered per 16-hit flush (1) or loaded with every candidate (0)
+#define PCP_H16_LATEID 0
+#endif
 #ifndef PCP_H16_NOSTORE  // profiling variant: the fill pass without its row stores
 #define PCP_H16_NOSTORE 0
 #endif
@@ -160,6 +163,7 @@ struct H16Acc {
     uint32_t cnt = 0;
     int32_t* slot = nullptr;  // (PCP_H16_FLUSH16 staging fill) this lane's 16 LDS slots, `stride` words apart
     int stride = 0;
+    const int32_t* late_ids = nullptr;  // set: the slots hold sorted positions, their ids gathered per flush
     int32_t sink = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
     float S0 = 0.f, S1 = 0.f, S2 = 0.f, S00 = 0.f, S01 = 0.f, S02 = 0.f, S11 = 0.f, S12 = 0.f, S22 = 0.f;
     __device__ __forceinline__ void hit(float dx, float dy, float dz, int32_t id, int32_t* __restrict__ out_idx) {
@@ -193,6 +197,15 @@ struct H16Acc {
     }
     // the first m (a multiple of 4 up to 16) slots to row entries [at, at + m)
     __device__ __forceinline__ void flush(int32_t* __restrict__ out_idx, uint32_t at, uint32_t m) {
+        if (late_ids) {  // 16 independent id loads, then the stores
+            int32_t v[16];
+#pragma unroll
+            for (uint32_t q = 0; q < 16u; q++) v[q] = q < m ? late_ids[slot[q * stride]] : 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 16u; q += 4u)
+                if (q < m) *(int4*)(out_idx + o + at + q) = make_int4(v[q], v[q + 1], v[q + 2], v[q + 3]);
+            return;
+        }
 #pragma unroll
         for (uint32_t q = 0; q < 16u; q += 4u)
             if (q < m)
@@ -270,6 +283,10 @@ __device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t c
     if (FILL) acc.o = DIRECT ? offsets[caller] : offsets[s];  // the caller rows, or the sorted-order staging rows
     acc.slot = slot;
     acc.stride = stride;
+    // PCP_H16_LATEID: the candidates' ids are not loaded with their records; a hit keeps its
+    // sorted position and each 16-hit flush gathers the 16 ids at once
+    constexpr bool kLateId = PCP_H16_LATEID && PCP_H16_FLUSH16 && FILL && !DIRECT;
+    if (kLateId) acc.late_ids = ids;
     for (int dz = -1; dz <= 1; dz++) {
         const int z = cz + dz;
         if (z < 0 || z >= g.n[2]) continue;
@@ -296,7 +313,7 @@ __device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t c
                 for (int u = 0; u < NB; u++) {
                     const uint32_t kk = min(k + (uint32_t)u, k1 - 1u);
                     pr[u] = rec[kk];
-                    if (FILL) idv[u] = ids[kk];
+                    if (FILL && !kLateId) idv[u] = ids[kk];
                 }
 #pragma unroll
                 for (int u = 0; u < NB; u++) {
@@ -306,7 +323,7 @@ __device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t c
                     const float dy_ = ey + h_hi(pr[u].x);
                     const float dz_ = ez + h_lo(pr[u].y);
                     const float d2 = __fmaf_rn(dz_, dz_, __fmaf_rn(dy_, dy_, dx * dx));
-                    if (kk < k1 && d2 < a.r2) acc.hit(dx, dy_, dz_, FILL ? idv[u] : 0, out_idx);
+                    if (kk < k1 && d2 < a.r2) acc.hit(dx, dy_, dz_, FILL ? (kLateId ? (int32_t)kk : idv[u]) : 0, out_idx);
                 }
             }
 
