@@ -72,25 +72,35 @@ for block, K in variants:
     qs = np.zeros((n, 3))          # query position at its last search
     D = np.zeros(n)                # certified bound of that search
     cache = np.zeros((n, K), np.int64)
+    d3s = np.zeros(n)
+    t1 = []
     searched = []
     for it, T in enumerate(poses):
         qt = xf(T)
         if it == 0:
             need = np.ones(n, bool)
         else:
-            dc = np.linalg.norm(tgt[cache].astype(np.float64) - qt[:, None, :], axis=2).min(1)
+            dall = np.linalg.norm(tgt[cache].astype(np.float64) - qt[:, None, :], axis=2)
+            dc = dall.min(1)
             delta = np.linalg.norm(qt - qs, axis=1)
             need = ~(dc < D - delta)
+            # a two-tier verify: settled from the first 3 cached points alone when their winner
+            # is below min(d_3 at the search pose, D) - delta
+            tier1 = dall[:, :3].min(1) < np.minimum(d3s, D) - delta
+            t1.append((tier1 & ~need).sum() / max(int((~need).sum()), 1))
         idx = np.nonzero(need)[0]
         dd, ii = tree.query(qt[idx], k=K + 1, workers=8)
         c = cert(qt[idx], block)
         ok = dd[:, 0] <= c
         cache[idx] = ii[:, :K]
+        d3s[idx] = dd[:, min(3, K)]
         D[idx] = np.where(ok, np.minimum(dd[:, K], c), 0.0)
         qs[idx] = qt[idx]
         searched.append(len(idx) / n)
     cells = 8 if block == "oct" else 27
     tot = sum(searched)
     print(f"{block} K={K}: searched fraction per iteration " + " ".join(f"{s:.3f}" for s in searched))
+    if K > 3:
+        print("   share of settled verifies settled by the first 3 cached points " + " ".join(f"{x:.2f}" for x in t1))
     print(f"   sum {tot:.3f} x n searches; iteration 0 {searched[0]:.2f}, later {tot - searched[0]:.3f}; "
           f"cells scanned per query summed {tot * cells:.1f}; cache gathers per verify {K}")
