@@ -180,7 +180,7 @@ struct H16Acc {
             // one burst (16-byte pieces spread over time were written to HBM part by part: the
             // fill's WRITE_SIZE was 2.8x its row bytes)
             slot[(cnt & 15u) * stride] = id;
-            if ((cnt & 15u) == 15u) flush(out_idx, cnt & ~15u, 16u);
+            if ((cnt & 15u) == 15u) flush(out_idx, cnt & ~15u, 16u, 16u);
 #else
             const uint32_t sl = cnt & 3u;
             w0 = sl == 0 ? id : w0;
@@ -195,12 +195,13 @@ struct H16Acc {
         }
         cnt++;
     }
-    // the first m (a multiple of 4 up to 16) slots to row entries [at, at + m)
-    __device__ __forceinline__ void flush(int32_t* __restrict__ out_idx, uint32_t at, uint32_t m) {
+    // the first m (a multiple of 4 up to 16) slots to row entries [at, at + m); slots from `valid`
+    // on are the row's padding (stale LDS: never dereferenced)
+    __device__ __forceinline__ void flush(int32_t* __restrict__ out_idx, uint32_t at, uint32_t m, uint32_t valid) {
         if (late_ids) {  // 16 independent id loads, then the stores
             int32_t v[16];
 #pragma unroll
-            for (uint32_t q = 0; q < 16u; q++) v[q] = q < m ? late_ids[slot[q * stride]] : 0;
+            for (uint32_t q = 0; q < 16u; q++) v[q] = q < valid ? late_ids[slot[q * stride]] : 0;
 #pragma unroll
             for (uint32_t q = 0; q < 16u; q += 4u)
                 if (q < m) *(int4*)(out_idx + o + at + q) = make_int4(v[q], v[q + 1], v[q + 2], v[q + 3]);
@@ -228,7 +229,7 @@ struct H16Acc {
         const GridDesc& g = a.g;
         if (PCP_H16_NOSTORE && FILL && !DIRECT && sink == 0x7fffffff) out_idx[o] = sink;
         if (!PCP_H16_NOSTORE && PCP_H16_FLUSH16 && FILL && !DIRECT && (cnt & 15u))
-            flush(out_idx, cnt & ~15u, ((cnt & 15u) + 3u) & ~3u);  // the padded tail
+            flush(out_idx, cnt & ~15u, ((cnt & 15u) + 3u) & ~3u, cnt & 15u);  // the padded tail
         if (!PCP_H16_NOSTORE && !PCP_H16_FLUSH16 && FILL && !DIRECT && (cnt & 3u))
             *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
         if (!FILL) {
