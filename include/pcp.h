@@ -126,6 +126,10 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_
  * row (calculate_plan_parameter(cloud, radius), calculate_feature.h:15) from fp32 sums.
  * Distances are fp32 of fp16 offsets: pairs within 3e-4 m of the radius may differ from an
  * exact search.
+ * Memory: the count also stages every row and plane in the index (rows at a fixed stride of 96
+ * entries + a spill pool: ~400 B per indexed point, held until the next count or
+ * pcp_index_destroy) so that the fill only moves them; when that memory is not available the
+ * count keeps only the row lengths and the fill searches again (same results).
  * Threading: the count keeps its sorted-order row lengths in the index for the fill of the
  * same (radius, n_owned) that follows it, so count -> fill pairs on ONE index must not
  * interleave across threads or streams (serialize them, or give each caller its own index);

@@ -155,5 +155,17 @@ struct pcp_index {
     int64_t h16_inv_cap = 0;
     float h16_last_r = -1.f;
     int64_t h16_last_owned = -1;
+    // the fused count (h16.hip, PCP_H16_FUSED): the count pass also writes every row (fixed
+    // stride, sorted order, caller indices), the planes (caller order) and the list of rows longer
+    // than the stride; the fill of the same radius and query set then only moves them
+    int32_t* h16_rows = nullptr;
+    int64_t h16_rows_cap = 0;    // entries
+    pcp_plane* h16_planes = nullptr;
+    int32_t* h16_ovf = nullptr;  // sorted positions of the overflowed rows (+ their count, the spill count)
+    int32_t* h16_spill_of = nullptr;  // caller -> spill row (rows longer than the stride)
+    int64_t h16_ovf_cap = 0;
+    float h16_fused_r = -1.f;
+    int64_t h16_fused_owned = -1;
+    uint32_t h16_fused_stride = 0;
     pcp_ctx* owner = nullptr;
 };

@@ -702,6 +702,10 @@ int pcp_index_destroy(pcp_index* ix) {
     pcp::dfree(ix->owner, ix->cell);
     pcp::dfree(ix->owner, ix->h16_cnt_s);
     pcp::dfree(ix->owner, ix->h16_inv);
+    pcp::dfree(ix->owner, ix->h16_rows);
+    pcp::dfree(ix->owner, ix->h16_planes);
+    pcp::dfree(ix->owner, ix->h16_ovf);
+    pcp::dfree(ix->owner, ix->h16_spill_of);
     pcp_ctx* owner = ix->owner;
     delete ix;
     pcp::ctx_release(owner);

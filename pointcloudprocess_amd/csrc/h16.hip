@@ -44,6 +44,12 @@ constexpr int kB = 256;
 #ifndef PCP_H16_LATEID  // fill (per-lane kernel): ids gathered per 16-hit flush (1) or loaded with every candidate (0)
 #define PCP_H16_LATEID 0
 #endif
+#ifndef PCP_H16_FUSED_DEFAULT  // 1: the count pass also writes the rows and planes (fixed-stride staging); the fill moves them
+#define PCP_H16_FUSED_DEFAULT 1
+#endif
+#ifndef PCP_H16_FUSED_STRIDE  // fused staging row capacity (a multiple of 16); longer rows spill into a pool
+#define PCP_H16_FUSED_STRIDE 96
+#endif
 #ifndef PCP_H16_NOSTORE  // profiling variant: the fill pass without its row stores
 #define PCP_H16_NOSTORE 0
 #endif
@@ -82,6 +88,16 @@ struct H16Args {
     const int32_t* mapping;
     int64_t n, n_owned;
     float hf, r2, rcut2;  // cell size, r^2 (the test), (r + margin)^2 (cell pruning)
+    // fused count: staging rows `cap` entries apart (0: rows at offsets[s]); a row that reaches cap
+    // continues in a spill row of the pool at spill_base (taken from *nspill, recorded in
+    // spill_of[caller]); the sorted positions of rows longer than that go to ovf, counted in *novf
+    uint32_t cap;
+    int32_t* ovf;
+    uint32_t* novf;
+    int32_t* spill_of;
+    uint32_t* nspill;
+    uint32_t spill_rows;
+    int64_t spill_base;
 };
 
 // one lane per sorted point; halo points (caller index >= n_owned) are not queries
@@ -114,22 +130,38 @@ __global__ void k_h16_sorted_counts(const int32_t* mapping, int64_t n, int64_t n
 // are ~n-bar long, so a lane advances about one row per step).  The per-row form (the wave
 // copying one row after another) left a dependent load->store per row and lanes idle past
 // each row's end.
+// Fused form (fstride > 0): the staged rows are fstride entries apart and hold caller indices,
+// translated through gid when the fill reports global ids; a row longer than fstride continues
+// in its spill row (spill_of), and one longer than two strides, or without a spill row, is
+// rewritten whole by k_h16_overflow after this pass; the staged planes (caller order) ride along,
+// one per row.
 __global__ __launch_bounds__(kB) void k_h16_rows_to_caller(const int32_t* inv, int64_t n_owned, const int64_t* soff,
                                                            const int64_t* offsets, const int32_t* __restrict__ tmp,
-                                                           int32_t* __restrict__ out) {
+                                                           int32_t* __restrict__ out, int64_t fstride = 0,
+                                                           const int32_t* __restrict__ gid = nullptr,
+                                                           const pcp_plane* __restrict__ pl_src = nullptr,
+                                                           pcp_plane* __restrict__ pl_dst = nullptr,
+                                                           const int32_t* __restrict__ spill_of = nullptr,
+                                                           int64_t spill_base = 0) {
     constexpr int kW = kB / 64;
     __shared__ int64_t s_dst[kW][65];
     __shared__ int64_t s_src[kW][64];
+    __shared__ int64_t s_spl[kW][64];  // fused: the spill row's start - fstride, or -1
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * kW;
     for (int64_t w = blockIdx.x * (int64_t)kW + wid; w * 64 < n_owned; w += nw) {
         const int rows = (int)min((int64_t)64, n_owned - w * 64);
         const int64_t c = w * 64 + lane;
         if (lane < rows) {
+            if (pl_dst) pl_dst[c] = pl_src[c];
             s_dst[wid][lane] = offsets[c];
             // an empty row (e.g. a caller point the build dropped as non-finite) has no staged
             // row and no inverse entry: never read inv for it
-            s_src[wid][lane] = offsets[c + 1] > offsets[c] ? soff[inv[c]] : 0;
+            const int64_t len = offsets[c + 1] - offsets[c];
+            s_src[wid][lane] = len > 0 ? (fstride ? (int64_t)inv[c] * fstride : soff[inv[c]]) : 0;
+            // (spill_of is written for every row longer than the stride)
+            const int32_t sp = fstride && len > fstride ? spill_of[c] : -1;
+            s_spl[wid][lane] = sp >= 0 ? spill_base + (int64_t)sp * fstride - fstride : -1;
         }
         if (lane == 0) s_dst[wid][rows] = offsets[w * 64 + rows];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -137,15 +169,24 @@ __global__ __launch_bounds__(kB) void k_h16_rows_to_caller(const int32_t* inv, i
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int64_t d0 = s_dst[wid][0], d1 = s_dst[wid][rows];
         int r = 0;
-        int64_t rd = d0, rn = s_dst[wid][1], rs = s_src[wid][0];
+        int64_t rd = d0, rn = s_dst[wid][1], rs = s_src[wid][0], rp = s_spl[wid][0];
         for (int64_t p = d0 + lane; p < d1; p += 64) {
             while (p >= rn) {  // empty rows are skipped too
                 r++;
                 rd = rn;
                 rn = s_dst[wid][r + 1];
                 rs = s_src[wid][r];
+                rp = s_spl[wid][r];
             }
-            out[p] = tmp[rs + (p - rd)];
+            if (fstride == 0) {
+                out[p] = tmp[rs + (p - rd)];
+            } else {
+                const int64_t e = p - rd;
+                if (e < fstride || (rp >= 0 && e < 2 * fstride)) {
+                    const int32_t v = tmp[(e < fstride ? rs : rp) + e];
+                    out[p] = gid ? gid[v] : v;
+                }
+            }
         }
         // the LDS rows are rewritten by the wave's next group
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -163,6 +204,20 @@ struct H16Acc {
     uint32_t cnt = 0;
     int32_t* slot = nullptr;  // (PCP_H16_FLUSH16 staging fill) this lane's 16 LDS slots, `stride` words apart
     int stride = 0;
+    uint32_t cap = 0xffffffffu;  // fused staging: entries from cap on are not stored (the row is redone)
+    uint32_t* spill_ctr = nullptr;  // fused staging: the spill pool (rows of the same stride)
+    uint32_t spill_rows = 0;
+    int64_t spill_base = 0;
+    int32_t spill = -1;
+    // the row is full: continue in a spill row (the staging offsets then address it directly)
+    __device__ __forceinline__ void grow() {
+        const uint32_t sp = atomicAdd(spill_ctr, 1u);
+        if (sp < spill_rows) {
+            spill = (int32_t)sp;
+            o = spill_base + (int64_t)sp * cap - cap;
+            cap *= 2u;
+        }
+    }
     const int32_t* late_ids = nullptr;  // set: the slots hold sorted positions, their ids gathered per flush
     int32_t sink = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
     float S0 = 0.f, S1 = 0.f, S2 = 0.f, S00 = 0.f, S01 = 0.f, S02 = 0.f, S11 = 0.f, S12 = 0.f, S22 = 0.f;
@@ -179,15 +234,17 @@ struct H16Acc {
             // 16 hits per 64-byte store group: the row's lines are written whole by this lane in
             // one burst (16-byte pieces spread over time were written to HBM part by part: the
             // fill's WRITE_SIZE was 2.8x its row bytes)
+            if (cnt == cap && spill_ctr && spill < 0) grow();
             slot[(cnt & 15u) * stride] = id;
-            if ((cnt & 15u) == 15u) flush(out_idx, cnt & ~15u, 16u, 16u);
+            if ((cnt & 15u) == 15u && cnt < cap) flush(out_idx, cnt & ~15u, 16u, 16u);
 #else
+            if (cnt == cap && spill_ctr && spill < 0) grow();
             const uint32_t sl = cnt & 3u;
             w0 = sl == 0 ? id : w0;
             w1 = sl == 1 ? id : w1;
             w2 = sl == 2 ? id : w2;
             w3 = sl == 3 ? id : w3;
-            if (sl == 3) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
+            if (sl == 3 && cnt < cap) *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
 #endif
             S0 += dx; S1 += dy; S2 += dz;
             S00 = __fmaf_rn(dx, dx, S00); S01 = __fmaf_rn(dx, dy, S01); S02 = __fmaf_rn(dx, dz, S02);
@@ -228,9 +285,9 @@ struct H16Acc {
                                            int32_t* __restrict__ inv) {
         const GridDesc& g = a.g;
         if (PCP_H16_NOSTORE && FILL && !DIRECT && sink == 0x7fffffff) out_idx[o] = sink;
-        if (!PCP_H16_NOSTORE && PCP_H16_FLUSH16 && FILL && !DIRECT && (cnt & 15u))
+        if (!PCP_H16_NOSTORE && PCP_H16_FLUSH16 && FILL && !DIRECT && (cnt & 15u) && cnt < cap)
             flush(out_idx, cnt & ~15u, ((cnt & 15u) + 3u) & ~3u, cnt & 15u);  // the padded tail
-        if (!PCP_H16_NOSTORE && !PCP_H16_FLUSH16 && FILL && !DIRECT && (cnt & 3u))
+        if (!PCP_H16_NOSTORE && !PCP_H16_FLUSH16 && FILL && !DIRECT && (cnt & 3u) && cnt < cap)
             *(int4*)(out_idx + o + (cnt & ~3u)) = make_int4(w0, w1, w2, w3);
         if (!FILL) {
             count[caller] = (int32_t)cnt;
@@ -238,7 +295,15 @@ struct H16Acc {
                 cnt_s[s] = (int32_t)((cnt + (kRowPad - 1)) & ~(kRowPad - 1));  // whole-store staging rows
                 inv[caller] = (int32_t)s;
             }
-        } else if (out_nrm) {
+        } else if (!DIRECT && a.cap) {  // fused count: the count, the inverse map, the overflow list
+            count[caller] = (int32_t)cnt;
+            inv[caller] = (int32_t)s;
+            if (cnt > a.cap) {
+                a.spill_of[caller] = spill;
+                if (cnt > cap) a.ovf[atomicAdd(a.novf, 1u)] = (int32_t)s;
+            }
+        }
+        if (FILL && out_nrm) {
             pcp_plane pl{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
             if (cnt > 0) {
                 const double nn = (double)cnt;
@@ -281,7 +346,14 @@ __device__ __forceinline__ void h16_point(const H16Args& a, int64_t s, int32_t c
     const float gyl = fmaxf(qy, 0.f), gyr = fmaxf(a.hf - qy, 0.f);
     const float gzl = fmaxf(qz, 0.f), gzr = fmaxf(a.hf - qz, 0.f);
     H16Acc<FILL, DIRECT> acc;
-    if (FILL) acc.o = DIRECT ? offsets[caller] : offsets[s];  // the caller rows, or the sorted-order staging rows
+    // the caller rows, the sorted-order staging rows, or (fused count) the fixed-stride ones
+    if (FILL) acc.o = DIRECT ? offsets[caller] : (a.cap ? s * (int64_t)a.cap : offsets[s]);
+    if (FILL && !DIRECT && a.cap) {
+        acc.cap = a.cap;
+        acc.spill_ctr = a.nspill;
+        acc.spill_rows = a.spill_rows;
+        acc.spill_base = a.spill_base;
+    }
     acc.slot = slot;
     acc.stride = stride;
     // PCP_H16_LATEID: the candidates' ids are not loaded with their records; a hit keeps its
@@ -346,6 +418,19 @@ __global__ __launch_bounds__(kB) void k_h16_radius(H16Args a, int32_t* count, co
             continue;
         }
         h16_point<FILL>(a, s, caller, count, offsets, ids, out_idx, out_nrm, cnt_s, inv, s_slot + threadIdx.x, kB);
+    }
+}
+
+// the fused fill's rows longer than two staging strides or without a spill row: each redone in
+// full, straight into its caller row (a few in a million at the default stride)
+__global__ __launch_bounds__(kB) void k_h16_overflow(H16Args a, const uint32_t* novf, const int32_t* __restrict__ list,
+                                                     const int64_t* __restrict__ offsets, const int32_t* __restrict__ ids,
+                                                     int32_t* __restrict__ out_idx) {
+    const uint32_t m = *novf;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const int64_t s = list[i];
+        h16_point<true, true>(a, s, a.mapping[s], (int32_t*)nullptr, offsets, ids, out_idx, (pcp_plane*)nullptr,
+                              (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, 0);
     }
 }
 
@@ -648,6 +733,17 @@ bool h16_direct_mode() {
     const char* e = getenv("PCP_H16_DIRECT");
     return e ? atoi(e) != 0 : PCP_H16_DIRECT_DEFAULT != 0;
 }
+// the fused count (1, default) or count-only + full fill (PCP_H16_FUSED=0); PCP_H16_FUSED_STRIDE
+// overrides the staging stride (tests force overflowing rows with a small one)
+bool h16_fused_mode() {
+    const char* e = getenv("PCP_H16_FUSED");
+    return e ? atoi(e) != 0 : PCP_H16_FUSED_DEFAULT != 0;
+}
+uint32_t h16_fused_stride() {
+    const char* e = getenv("PCP_H16_FUSED_STRIDE");
+    const long v = e ? atol(e) : PCP_H16_FUSED_STRIDE;
+    return (uint32_t)std::min<long>(std::max<long>((v + 15) / 16 * 16, 16), 4096);
+}
 unsigned tile_blocks(int64_t n) { return (unsigned)std::min<int64_t>(std::max<int64_t>((n + 63) / 64, 1), 1 << 20); }
 
 int check_query(pcp_ctx* ctx, const pcp_index* ix, float r, int64_t n_owned) {
@@ -716,6 +812,60 @@ int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_
         PCP_TRY(dmalloc(ix->owner, &ixm->h16_inv, (size_t)n_owned));
         ixm->h16_inv_cap = n_owned;
     }
+    ixm->h16_fused_r = -1.f;
+    if (!h16_tile_mode() && h16_fused_mode()) {
+        // the fused count: rows, planes and the overflow list for the fill; needs ~4 x stride
+        // bytes per point of staging, so it gives way to the two-pass form when that is not there
+        const uint32_t stride = h16_fused_stride();
+        const int64_t spill_rows = std::max<int64_t>(1024, ix->n / 32);  // ~1.4 % of the rows spill at 96
+        const size_t need = ((size_t)ix->n + (size_t)spill_rows) * stride;
+        bool ok = true;
+        if (ixm->h16_rows_cap < (int64_t)need) {
+            dfree(ix->owner, ixm->h16_rows);
+            ixm->h16_rows = nullptr;
+            ixm->h16_rows_cap = 0;
+            ok = dmalloc(ix->owner, &ixm->h16_rows, need) == PCP_OK;
+            if (ok) ixm->h16_rows_cap = (int64_t)need;
+        }
+        if (ok && ixm->h16_ovf_cap < n_owned) {
+            dfree(ix->owner, ixm->h16_planes);
+            dfree(ix->owner, ixm->h16_ovf);
+            dfree(ix->owner, ixm->h16_spill_of);
+            ixm->h16_planes = nullptr;
+            ixm->h16_ovf = nullptr;
+            ixm->h16_spill_of = nullptr;
+            ixm->h16_ovf_cap = 0;
+            ok = dmalloc(ix->owner, &ixm->h16_planes, (size_t)n_owned) == PCP_OK &&
+                 dmalloc(ix->owner, &ixm->h16_ovf, (size_t)n_owned + 2) == PCP_OK &&
+                 dmalloc(ix->owner, &ixm->h16_spill_of, (size_t)n_owned) == PCP_OK;
+            if (ok) ixm->h16_ovf_cap = n_owned;
+        }
+        if (ok) {
+            H16Args af = a;
+            af.cap = stride;
+            af.ovf = ixm->h16_ovf;
+            af.novf = (uint32_t*)(ixm->h16_ovf + ixm->h16_ovf_cap);
+            af.nspill = af.novf + 1;
+            af.spill_of = ixm->h16_spill_of;
+            af.spill_rows = (uint32_t)spill_rows;
+            af.spill_base = (int64_t)ix->n * stride;
+            PCP_HIP(ctx, hipMemsetAsync(af.novf, 0, 2 * sizeof(uint32_t), ctx->stream));
+            hipLaunchKernelGGL(k_h16_plane_default, dim3(grid_for(n_owned, kB)), dim3(kB), 0, ctx->stream,
+                               ixm->h16_planes, n_owned);
+            hipLaunchKernelGGL(k_h16_radius<true>, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, af, count_dev,
+                               (const int64_t*)nullptr, (const int32_t*)ix->mapping, ixm->h16_rows, ixm->h16_planes,
+                               (int32_t*)nullptr, ixm->h16_inv);
+            PCP_LAUNCH_CHECK(ctx);
+            ixm->h16_fused_r = radius;
+            ixm->h16_fused_owned = n_owned;
+            ixm->h16_fused_stride = stride;
+            return PCP_OK;
+        }
+        // not enough device memory for the staging: release what was taken, count only
+        dfree(ix->owner, ixm->h16_rows);
+        ixm->h16_rows = nullptr;
+        ixm->h16_rows_cap = 0;
+    }
     if (h16_tile_mode())
         hipLaunchKernelGGL(k_h16_tile<false>, dim3(tile_blocks(ix->n)), dim3(64), 0, ctx->stream, a, count_dev,
                            (const int64_t*)nullptr, (const int32_t*)nullptr, (int32_t*)nullptr, (pcp_plane*)nullptr,
@@ -737,6 +887,37 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
     PCP_TRY(check_query(ctx, ix, radius, n_owned));
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     if (n_owned == 0) return PCP_OK;
+    if (ix->n > 0 && ix->h16_rows && ix->h16_fused_r == radius && ix->h16_fused_owned == n_owned) {
+        // the fused count of this radius and query set staged the rows and planes: move them
+        const H16Args a = make_args(ix, radius, n_owned);
+        const uint32_t* novf_dev = (const uint32_t*)(ix->h16_ovf + ix->h16_ovf_cap);
+        uint32_t novf = 0;
+        PCP_HIP(ctx, hipMemcpyAsync(&novf, novf_dev, sizeof(novf), hipMemcpyDeviceToHost, ctx->stream));
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        hipLaunchKernelGGL(k_h16_rows_to_caller, dim3(grid_for(n_owned, kB, 1 << 16)), dim3(kB), 0, ctx->stream,
+                           (const int32_t*)ix->h16_inv, n_owned, (const int64_t*)nullptr, offsets_dev,
+                           (const int32_t*)ix->h16_rows, idx_dev, (int64_t)ix->h16_fused_stride, global_id_dev,
+                           (const pcp_plane*)ix->h16_planes, normals_dev, (const int32_t*)ix->h16_spill_of,
+                           (int64_t)ix->n * ix->h16_fused_stride);
+        PCP_LAUNCH_CHECK(ctx);
+        if (novf == 0) return PCP_OK;
+        int32_t* ids = nullptr;
+        struct Free {
+            pcp_ctx* c; int32_t** a;
+            ~Free() { dfree(c, *a); }
+        } fr{ctx, &ids};
+        const int32_t* rep_ids = ix->mapping;  // the reported ids: the caller indices, or their global ids
+        if (global_id_dev) {
+            PCP_TRY(dmalloc(ctx, &ids, (size_t)ix->n));
+            hipLaunchKernelGGL(k_h16_ids, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, (const int32_t*)ix->mapping,
+                               global_id_dev, ix->n, ids);
+            rep_ids = ids;
+        }
+        hipLaunchKernelGGL(k_h16_overflow, dim3(grid_for(novf, kB)), dim3(kB), 0, ctx->stream, a, novf_dev,
+                           (const int32_t*)ix->h16_ovf, offsets_dev, rep_ids, idx_dev);
+        PCP_LAUNCH_CHECK(ctx);
+        return PCP_OK;
+    }
     if (normals_dev)
         hipLaunchKernelGGL(k_h16_plane_default, dim3(grid_for(n_owned, kB)), dim3(kB), 0, ctx->stream, normals_dev,
                            n_owned);

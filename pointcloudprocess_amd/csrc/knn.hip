@@ -1072,6 +1072,7 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                          oz = g.o[2] + (double)b.z0 * g.h;
             const int ext = max(max(b.x1 - b.x0, b.y1 - b.y0), b.z1 - b.z0) + 1;
             const double step = (double)ext * g.h / (double)kTileQ, inv = 1.0 / step;
+#if !PCP_TILE_ROWTAB
             const int nrow = b.nrow;
             auto row_of = [&](uint32_t e) {
                 int r = 0;
@@ -1080,6 +1081,7 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                     r = (r + stp < nrow && s_rb[r + stp] <= e) ? r + stp : r;
                 return r;
             };
+#endif
 #if PCP_TILE_ROWTAB
             // e advances by 64 per step, so each lane's row only moves forward: a short walk
             // instead of a binary search, and the row of every staged point is kept (one byte)

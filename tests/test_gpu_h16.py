@@ -159,6 +159,7 @@ def test_h16_direct_fill_matches_staged(ctx, scene, monkeypatch):
     (PCP_H16_DIRECT=1) against the staged rows + copy pass (0): byte-identical CSR and normals."""
     from pointcloudprocess_amd import ops
     out = {}
+    monkeypatch.setenv("PCP_H16_TILE", "1")  # the direct fill is a form of the tile kernel
     for mode in ("1", "0"):
         monkeypatch.setenv("PCP_H16_DIRECT", mode)
         ix = ops.H16Index(ctx, torch.from_numpy(scene).to(ctx.device), cell_size=R)
@@ -167,3 +168,45 @@ def test_h16_direct_fill_matches_staged(ctx, scene, monkeypatch):
         ix.close()
     for a, b in zip(out["1"], out["0"]):
         assert torch.equal(a, b)
+
+
+def test_h16_fused_count_matches_two_pass(ctx, scene, monkeypatch):
+    """The fused count (default: the count pass stages every row at a fixed stride and the planes;
+    the fill moves them to caller order and redoes the rows longer than the stride) against the
+    count-only pass + full fill (PCP_H16_FUSED=0): byte-identical CSR and normals, with caller
+    indices and with global ids, at the default stride and at 32- and 16-entry strides (rows
+    continue in spill rows until the pool runs out, the rest -- and rows longer than two strides
+    -- take the redo path)."""
+    import ctypes as C
+    from pointcloudprocess_amd import ops
+    xyz = scene[:600_000]
+    n = xyz.shape[0]
+    gid = torch.from_numpy(np.random.default_rng(11).permutation(n).astype(np.int32) * 3 + 5).to(ctx.device)
+    lib = ctx.lib
+    out = {}
+    for mode, stride in (("0", None), ("1", None), ("1", "32"), ("1", "16")):
+        monkeypatch.setenv("PCP_H16_FUSED", mode)
+        if stride:
+            monkeypatch.setenv("PCP_H16_FUSED_STRIDE", stride)
+        else:
+            monkeypatch.delenv("PCP_H16_FUSED_STRIDE", raising=False)
+        ix = ops.H16Index(ctx, torch.from_numpy(xyz).to(ctx.device), cell_size=R)
+        offs, idx, nrm = ix.radius_normals(R)
+        idx_g = torch.empty_like(idx)
+        nrm_g = torch.empty_like(nrm)
+        ctx.check(lib.pcp_h16_radius_fill(ctx.h, ix.h, float(R), n, C.c_void_p(offs.data_ptr()),
+                                          C.c_void_p(gid.data_ptr()), C.c_void_p(idx_g.data_ptr()),
+                                          C.c_void_p(nrm_g.data_ptr())))
+        torch.cuda.synchronize()
+        out[(mode, stride)] = (offs.cpu(), idx.cpu(), nrm.cpu().view(torch.int32), idx_g.cpu(),
+                               nrm_g.cpu().view(torch.int32))
+        ix.close()
+    ref = out[("0", None)]
+    assert torch.equal(ref[3], gid.cpu()[ref[1].long()])
+    assert torch.equal(ref[4], ref[2])
+    lens = (ref[0][1:] - ref[0][:-1]).numpy()
+    print(f"rows over 96: {(lens > 96).mean():.4f}, over 32 / 64: {(lens > 32).mean():.4f} / "
+          f"{(lens > 64).mean():.4f}, over 16 / 32: {(lens > 16).mean():.4f} / {(lens > 32).mean():.4f}")
+    for key in (("1", None), ("1", "32"), ("1", "16")):
+        for a, b in zip(out[key], ref):
+            assert torch.equal(a, b), key
