@@ -55,7 +55,7 @@ PMC_KERNELS = {
     "C2": ("knn_bf.hip", ("k_bf_mfma", "k_bf_fallback", "k_bf_targets", "k_bf_pad")),
     "C3": ("knn.hip", ("k_normals_tile", "k_normals", "k_normals_coop", "k_brick_keys", "k_plane_default")),
     "C5": ("h16.hip", ("k_h16_radius", "k_h16_tile", "k_h16_rows_to_caller", "tile_scan", "k_h16_ids",
-                       "k_h16_plane_default", "k_h16_sorted_counts", "k_h16_overflow")),
+                       "k_h16_plane_default", "k_h16_sorted_counts", "k_h16_overflow", "k_h16_cw", "k_h16_cw_planes")),
 }
 
 

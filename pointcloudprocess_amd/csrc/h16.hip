@@ -707,6 +707,416 @@ __global__ void k_h16_plane_default(pcp_plane* out, int64_t n) {
         out[i] = pcp_plane{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};  // points dropped as non-finite
 }
 
+// ---- cell-wave form (PCP_H16_CW, the default): one wave per query cell, lanes = candidates.
+// The wave loads its cell's 3x3x3 neighbourhood once -- the 9 (dy, dz) rows of cells [cx - 1,
+// cx + 1], concatenated in the per-lane kernel's visiting order (dz, dy, then ascending sorted
+// position) -- one candidate per lane and step, into registers (fp16 offsets widened to fp32, the
+// x-cell offset dxc and the row's dy h, dz h).  Each query of the cell is then a wave-uniform
+// value: its test d2 < r^2 runs on every lane against that lane's candidates (the per-lane
+// kernel's formula, op for op, so the hit set is identical; the per-lane kernel's row/cell
+// pruning only skips cells that cannot hold a hit), the hits are compacted by ballot + mbcnt
+// in candidate order, which IS the row's order, and stored as one contiguous run per step
+// straight into the caller's CSR row.  No per-lane load chains, no divergent stores, no
+// staging rows and no caller-order copy.  The F1 sums (n, S, S S^T of the offsets from the
+// query) are accumulated per lane for 4 queries at once and reduce-scattered across the wave
+// (36 values, ~25 VALU ops per query); they go out in sorted order and k_h16_cw_planes forms
+// the planes (the fp64 eigen core stays out of this kernel's registers).
+#ifndef PCP_H16_CW_DEFAULT
+#define PCP_H16_CW_DEFAULT 1
+#endif
+#ifndef PCP_H16_CW_MINB  // blocks per CU the cell-wave kernels are register-budgeted for
+#define PCP_H16_CW_MINB 4
+#endif
+constexpr int kCwWaves = kB / 64;
+constexpr int kCwSteps = 6;  // candidate steps held in registers (6 x 64); larger neighbourhoods loop
+constexpr int kCwQ = 4;      // queries per accumulator batch (4 x 9 sums reduce-scattered together)
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+struct alignas(16) CwSums {  // one query's F1 sums (sorted order) for k_h16_cw_planes (3 x 16-byte words)
+    float S0, S1, S2, S00, S01, S02, S11, S12, S22;
+    int32_t n, pad0, pad1;
+};
+
+template <int CTRL>
+__device__ __forceinline__ float cw_dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ float cw_bfly(float a, float b, bool s) {
+    const float t = s ? b : a, u = s ? a : b;
+    return t + cw_dpp<CTRL>(u);
+}
+__device__ __forceinline__ float cw_swap_add32(float a, float b) {  // lanes < 32: a_lo + a_hi; >= 32: b_lo + b_hi
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float cw_swap_add16(float a, float b) {  // even rows: a's row pair; odd rows: b's
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// Reduce-scatter of v[36] (value qi * 9 + k) over the wave: afterwards lane l holds the wave total
+// of value 18 b5 + 9 b4 + (b0 + 2 b1 + 3 b2 + 5 b3) when cw_owner(l) (each value exactly once).
+__device__ __forceinline__ float cw_reduce36(const float (&v)[36], int lane) {
+    float w18[18];
+#pragma unroll
+    for (int i = 0; i < 18; i++) w18[i] = cw_swap_add32(v[i], v[i + 18]);
+    float w9[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) w9[i] = cw_swap_add16(w18[i], w18[i + 9]);
+    const bool s3 = lane & 8, s2 = lane & 4, s1 = lane & 2, s0 = lane & 1;
+    float x5[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) x5[i] = cw_bfly<0x140>(w9[i], i + 5 < 9 ? w9[i + 5] : 0.f, s3);  // row mirror
+    float x3[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) x3[i] = cw_bfly<0x141>(x5[i], i + 3 < 5 ? x5[i + 3] : 0.f, s2);  // half-row mirror
+    const float y0 = cw_bfly<0x4E>(x3[0], x3[2], s1), y1 = cw_bfly<0x4E>(x3[1], 0.f, s1);  // quad [2,3,0,1]
+    return cw_bfly<0xB1>(y0, y1, s0);                                                     // quad [1,0,3,2]
+}
+__device__ __forceinline__ int cw_slot9(int lane) {
+    return (lane & 1) + 2 * ((lane >> 1) & 1) + 3 * ((lane >> 2) & 1) + 5 * ((lane >> 3) & 1);
+}
+__device__ __forceinline__ bool cw_owner(int lane) {
+    const int i1 = (lane & 1) + 2 * ((lane >> 1) & 1), i2 = i1 + 3 * ((lane >> 2) & 1);
+    return i1 < 3 && i2 < 5 && i2 + 5 * ((lane >> 3) & 1) < 9;
+}
+
+// FILL = false: count[caller] = the row length.  FILL = true: the row's ids (ids[sorted position])
+// at out_idx[offsets[caller] ...] and the query's sums at sums[sorted position].
+template <bool FILL>
+__global__ __launch_bounds__(kB, PCP_H16_CW_MINB) void k_h16_cw(H16Args a, int32_t* __restrict__ count, const int64_t* __restrict__ offsets,
+                                               const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
+                                               CwSums* __restrict__ sums) {
+    __shared__ uint4 s_row[kCwWaves][9];  // per neighbour row: kk = j + off, the query column [b1, b2)
+    __shared__ float s_sum[kCwWaves][64 * 9];
+    const GridDesc& g = a.g;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t nwaves = (int64_t)gridDim.x * kCwWaves;
+    const float hf = a.hf, r2 = a.r2;
+    for (int64_t w = blockIdx.x * (int64_t)kCwWaves + wid; w * 64 < a.n; w += nwaves) {
+        // the cells whose first point lies in this wave's 64 sorted positions
+        const int64_t p = w * 64 + lane;
+        const uint32_t cp = p < a.n ? a.cell[p] : 0xffffffffu;
+        const uint32_t cq = (p < a.n && p > 0) ? a.cell[p - 1] : 0xfffffffeu;
+        uint64_t heads = __ballot(p < a.n && (p == 0 || cp != cq));
+        while (heads) {
+            const int hl = __builtin_ctzll(heads);
+            heads &= heads - 1;
+            const uint32_t cid = (uint32_t)__builtin_amdgcn_readlane((int)cp, hl);
+            const int64_t cs = w * 64 + hl;
+            const int64_t ce = (int64_t)g.cstart[(int64_t)cid + 1];
+            const int cx = (int)(cid % (uint32_t)g.n[0]);
+            const int cy = (int)((cid / (uint32_t)g.n[0]) % (uint32_t)g.n[1]);
+            const int cz = (int)(cid / ((uint32_t)g.n[0] * (uint32_t)g.n[1]));
+            // the 9 rows (lane r: dz = r / 3 - 1, dy = r % 3 - 1), cells [cx - 1, cx + 1] clipped
+            uint32_t len = 0;
+            if (lane < 9) {
+                const int y = cy + lane % 3 - 1, z = cz + lane / 3 - 1;
+                uint32_t k0 = 0, b1 = 0, b2 = 0;
+                if (y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2]) {
+                    const int xa = max(cx - 1, 0), xb = min(cx + 1, g.n[0] - 1);
+                    const int64_t c0 = dense_id(g, xa, y, z), cc = dense_id(g, cx, y, z);
+                    k0 = g.cstart[c0];
+                    len = g.cstart[c0 + (xb - xa + 1)] - k0;
+                    b1 = g.cstart[cc];
+                    b2 = g.cstart[cc + 1];
+                }
+                uint32_t pre = 0;  // exclusive prefix of the row lengths
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t lk = (uint32_t)__shfl((int)len, k, 64);
+                    pre += k < lane ? lk : 0u;
+                }
+                s_row[wid][lane] = make_uint4(k0 - pre, b1, b2, pre);
+            }
+            uint32_t P[9];  // wave-uniform row starts in the concatenated list, and M
+            {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    P[k] = acc;
+                    acc += (uint32_t)__builtin_amdgcn_readlane((int)len, k);
+                }
+                len = acc;  // M
+            }
+            const uint32_t M = len;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // candidates of block `blk` (kCwSteps x 64 from list entry blk) into registers
+            float cox[kCwSteps], coy[kCwSteps], coz[kCwSteps], cdx[kCwSteps], cdy[kCwSteps], cdz[kCwSteps];
+            int32_t cid_[kCwSteps];
+            auto load_block = [&](uint32_t blk) {
+#pragma unroll
+                for (int s = 0; s < kCwSteps; s++) {
+                    if (blk + 64u * s >= M) break;  // (uniform) the block's steps past the list are never read
+                    const uint32_t j = blk + 64u * s + (uint32_t)lane;
+                    const bool ok = j < M;
+                    int r = 0;
+#pragma unroll
+                    for (int k = 1; k < 9; k++) r += j >= P[k] ? 1 : 0;
+                    const uint4 row = s_row[wid][r];
+                    const uint32_t kk = ok ? j + row.x : 0u;
+                    const uint2 pr = a.rec[kk];
+                    cid_[s] = FILL && ok ? ids[kk] : 0;
+                    cox[s] = h_lo(pr.x);
+                    coy[s] = h_hi(pr.x);
+                    coz[s] = h_lo(pr.y);
+                    // past the list: a finite far offset (d2 ~ 1e38 >= r^2, never a hit)
+                    cdx[s] = ok ? (kk < row.y ? -hf : (kk < row.z ? 0.f : hf)) : 1e19f;
+                    cdy[s] = (float)(r % 3 - 1) * hf;
+                    cdz[s] = (float)(r / 3 - 1) * hf;
+                }
+            };
+            // the per-lane kernel's expression (h16_point), op for op: same d2, same hit set
+            auto test = [&](int s, float x, float y, float z, float& dx, float& dy, float& dz) {
+                dx = cdx[s] + (cox[s] - x);
+                dy = (cdy[s] - y) + coy[s];
+                dz = (cdz[s] - z) + coz[s];
+                return __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx)) < r2;
+            };
+            const uint32_t nblk = (M + kCwSteps * 64 - 1) / (kCwSteps * 64);
+            if (nblk == 1) load_block(0u);
+            // the cell's queries, 64 at a time
+            for (int64_t qs = cs; qs < ce; qs += 64) {
+                const int nseg = (int)min((int64_t)64, ce - qs);
+                float qx = 0.f, qy = 0.f, qz = 0.f;
+                int32_t caller = 0x7fffffff;
+                int64_t base = 0;
+                if (lane < nseg) {
+                    const uint2 qr = a.rec[qs + lane];
+                    qx = h_lo(qr.x), qy = h_hi(qr.x), qz = h_lo(qr.y);
+                    caller = a.mapping[qs + lane];
+                    if (FILL && caller < a.n_owned) base = offsets[caller];
+                }
+                int32_t cntv = 0;  // lane i: the row length of query i of the segment
+                if constexpr (!FILL) {
+                    // count: two queries at a time (the tests as packed fp32: v_pk_add/mul/fma_f32
+                    // round each half exactly as the scalar ops), one ballot per query and step
+                    for (int qi = 0; qi < nseg; qi += 2) {
+                        const int q1 = min(qi + 1, 63);
+                        const bool a0 = __builtin_amdgcn_readlane(caller, qi) < a.n_owned;
+                        const bool a1 = qi + 1 < nseg && __builtin_amdgcn_readlane(caller, q1) < a.n_owned;
+                        if (!a0 && !a1) continue;
+                        const f2 sx = {__int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), qi)),
+                                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), q1))};
+                        const f2 sy = {__int_as_float(__builtin_amdgcn_readlane(__float_as_int(qy), qi)),
+                                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qy), q1))};
+                        const f2 sz = {__int_as_float(__builtin_amdgcn_readlane(__float_as_int(qz), qi)),
+                                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qz), q1))};
+                        uint32_t c0 = 0, c1 = 0;
+                        for (uint32_t b = 0; b < nblk; b++) {
+                            if (nblk > 1) load_block(b * (uint32_t)(kCwSteps * 64));
+                            const uint32_t mb = min(M - b * (uint32_t)(kCwSteps * 64), (uint32_t)(kCwSteps * 64));
+#pragma unroll
+                            for (int s = 0; s < kCwSteps; s++) {
+                                if (64u * s >= mb) break;
+                                const f2 dx = (f2)cdx[s] + ((f2)cox[s] - sx);
+                                const f2 dy = ((f2)cdy[s] - sy) + (f2)coy[s];
+                                const f2 dz = ((f2)cdz[s] - sz) + (f2)coz[s];
+                                const f2 d2 = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+                                c0 += (uint32_t)__popcll(__ballot(d2[0] < r2));
+                                c1 += (uint32_t)__popcll(__ballot(d2[1] < r2));
+                            }
+                        }
+                        cntv = lane == qi ? (int32_t)c0 : cntv;
+                        cntv = lane == qi + 1 ? (int32_t)c1 : cntv;
+                    }
+                } else {
+                    for (int qb = 0; qb < nseg; qb += kCwQ) {
+                        float acc[kCwQ * 9];
+#pragma unroll
+                        for (int v = 0; v < kCwQ * 9; v++) acc[v] = 0.f;
+                        float sqx[kCwQ], sqy[kCwQ], sqz[kCwQ];
+                        int64_t sbase[kCwQ];
+                        bool act[kCwQ];
+                        uint32_t qcnt[kCwQ];
+#pragma unroll
+                        for (int qi = 0; qi < kCwQ; qi++) {
+                            const int q = min(qb + qi, 63);
+                            sqx[qi] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), q));
+                            sqy[qi] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qy), q));
+                            sqz[qi] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qz), q));
+                            act[qi] = qb + qi < nseg && __builtin_amdgcn_readlane(caller, q) < a.n_owned;
+                            const uint64_t bq = (uint64_t)base;
+                            sbase[qi] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bq, q)) |
+                                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bq >> 32), q) << 32));
+                            qcnt[qi] = 0u;
+                        }
+                        for (uint32_t b = 0; b < nblk; b++) {
+                            if (nblk > 1) load_block(b * (uint32_t)(kCwSteps * 64));
+                            const uint32_t mb = min(M - b * (uint32_t)(kCwSteps * 64), (uint32_t)(kCwSteps * 64));
+#pragma unroll
+                            for (int s = 0; s < kCwSteps; s++) {
+                                if (64u * s >= mb) break;
+#pragma unroll
+                                for (int qi = 0; qi < kCwQ; qi++) {
+                                    if (!act[qi]) continue;
+                                    float dx, dy, dz;
+                                    const bool hit = test(s, sqx[qi], sqy[qi], sqz[qi], dx, dy, dz);
+                                    const uint64_t m = __ballot(hit);
+                                    if (hit) {  // the row entry (ballot order = candidate order) and the sums
+                                        const uint32_t pos = qcnt[qi] + __builtin_amdgcn_mbcnt_hi(
+                                                                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                                        out_idx[sbase[qi] + pos] = cid_[s];
+                                        float* A = acc + qi * 9;
+                                        A[0] += dx;
+                                        A[1] += dy;
+                                        A[2] += dz;
+                                        A[3] = __fmaf_rn(dx, dx, A[3]);
+                                        A[4] = __fmaf_rn(dx, dy, A[4]);
+                                        A[5] = __fmaf_rn(dx, dz, A[5]);
+                                        A[6] = __fmaf_rn(dy, dy, A[6]);
+                                        A[7] = __fmaf_rn(dy, dz, A[7]);
+                                        A[8] = __fmaf_rn(dz, dz, A[8]);
+                                    }
+                                    qcnt[qi] += (uint32_t)__popcll(m);
+                                }
+                            }
+                        }
+#pragma unroll
+                        for (int qi = 0; qi < kCwQ; qi++) cntv = lane == qb + qi ? (int32_t)qcnt[qi] : cntv;
+                        const float tot = cw_reduce36(acc, lane);
+                        const int qi = 2 * ((lane >> 5) & 1) + ((lane >> 4) & 1);
+                        if (cw_owner(lane) && qb + qi < 64) s_sum[wid][(qb + qi) * 9 + cw_slot9(lane)] = tot;
+                    }
+                }
+                if (!FILL) {
+                    if (lane < nseg && caller < a.n_owned) count[caller] = cntv;
+                } else {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (sums && lane < nseg && caller < a.n_owned) {
+                        const float* S = &s_sum[wid][lane * 9];
+                        sums[qs + lane] = CwSums{S[0], S[1], S[2], S[3], S[4], S[5], S[6], S[7], S[8], cntv, 0, 0};
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+            }
+            // s_row is rewritten by the next cell
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+}
+
+// F1's plane from the fp64 covariance by the closed-form symmetric 3x3 eigen decomposition
+// (trigonometric eigenvalues, the smallest one's eigenvector as the largest cross product of two
+// rows of C - l3 I): a fixed ~250 fp64 ops against the cyclic Jacobi's 4-6 data-dependent sweeps
+// (the planes pass was 12.8 ms of the 200M-point step with it).  Rows whose two smallest
+// eigenvalues nearly coincide (the normal is ill-conditioned in any method; fewer than 3
+// neighbours, lines) keep the Jacobi core, as does everything outside C5, whose results are
+// checked to tolerance (fp32 sums of fp16 offsets) rather than bit for bit.
+// Returns false (out untouched) for the rows that keep the Jacobi core (k_h16_cw_planes_fb: the
+// rare rows must not set the register budget of the streaming pass).
+__device__ inline bool h16_plane(const double C[9], double xa, double ya, double za, pcp_plane& out) {
+    const double a00 = C[0], a01 = C[1], a02 = C[2], a11 = C[4], a12 = C[5], a22 = C[8];
+    const double m = (a00 + a11 + a22) / 3.0;
+    const double b00 = a00 - m, b11 = a11 - m, b22 = a22 - m;
+    const double p1 = a01 * a01 + a02 * a02 + a12 * a12;
+    const double q = (b00 * b00 + b11 * b11 + b22 * b22 + 2.0 * p1) / 6.0;
+    bool ok = q > 0.0;
+    double l1 = m, l2 = m, l3 = m, n0 = 1.0, n1 = 0.0, n2 = 0.0;
+    if (ok) {
+        const double p = sqrt(q);
+        const double det = b00 * (b11 * b22 - a12 * a12) - a01 * (a01 * b22 - a12 * a02) + a02 * (a01 * a12 - b11 * a02);
+        const double r = fmin(fmax(det / (2.0 * p * p * p), -1.0), 1.0);
+        const double phi = acos(r) / 3.0;
+        l1 = m + 2.0 * p * cos(phi);
+        l3 = m + 2.0 * p * cos(phi + 2.0943951023931954923);  // + 2 pi / 3
+        l2 = 3.0 * m - l1 - l3;
+        ok = (l2 - l3) > 1e-4 * (l1 - l3);
+        if (ok) {
+            const double r00 = a00 - l3, r11 = a11 - l3, r22 = a22 - l3;
+            // cross products of the rows (r00, a01, a02), (a01, r11, a12), (a02, a12, r22)
+            const double x0 = a01 * a12 - a02 * r11, y0 = a02 * a01 - r00 * a12, z0 = r00 * r11 - a01 * a01;
+            const double x1 = a01 * r22 - a02 * a12, y1 = a02 * a02 - r00 * r22, z1 = r00 * a12 - a01 * a02;
+            const double x2 = r11 * r22 - a12 * a12, y2 = a12 * a02 - a01 * r22, z2 = a01 * a12 - r11 * a02;
+            const double s0 = x0 * x0 + y0 * y0 + z0 * z0, s1 = x1 * x1 + y1 * y1 + z1 * z1,
+                         s2 = x2 * x2 + y2 * y2 + z2 * z2;
+            double cx = x0, cy = y0, cz = z0, sb = s0;
+            if (s1 > sb) cx = x1, cy = y1, cz = z1, sb = s1;
+            if (s2 > sb) cx = x2, cy = y2, cz = z2, sb = s2;
+            ok = sb > 0.0;
+            const double inv = ok ? 1.0 / sqrt(sb) : 0.0;
+            n0 = cx * inv, n1 = cy * inv, n2 = cz * inv;
+        }
+    }
+    if (!ok) return false;
+    // the F1 core's sign, distance and ratios (pca.hpp plane_from_cov)
+    double n[3] = {n0, n1, n2};
+    int big = 0;
+    for (int k = 1; k < 3; k++)
+        if (fabs(n[k]) > fabs(n[big])) big = k;
+    if (n[big] < 0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+    out.normal_x = (float)n[0];
+    out.normal_y = (float)n[1];
+    out.normal_z = (float)n[2];
+    const double dist = -((double)out.normal_x * xa + (double)out.normal_y * ya + (double)out.normal_z * za);
+    out.distance = (float)dist;
+    out.min_value = (float)l3;
+    out.curvature = (float)(l3 / (l1 + l2 + l3));
+    return true;
+}
+
+// the fp64 covariance and absolute mean of sorted point s from its F1 sums (H16Acc::finish)
+__device__ inline void cw_cov(const H16Args& a, int64_t s, const CwSums& q, double C[9], double& xa, double& ya,
+                              double& za) {
+    const GridDesc& g = a.g;
+    const uint2 qr = a.rec[s];
+    const float qx = h_lo(qr.x), qy = h_hi(qr.x), qz = h_lo(qr.y);
+    const uint32_t cid = a.cell[s];
+    const int cx = (int)(cid % (uint32_t)g.n[0]);
+    const int cy = (int)((cid / (uint32_t)g.n[0]) % (uint32_t)g.n[1]);
+    const int cz = (int)(cid / ((uint32_t)g.n[0] * (uint32_t)g.n[1]));
+    const double nn = (double)q.n;
+    const double m0 = q.S0 / nn, m1 = q.S1 / nn, m2 = q.S2 / nn;
+    C[0] = q.S00 - nn * m0 * m0; C[1] = q.S01 - nn * m0 * m1; C[2] = q.S02 - nn * m0 * m2;
+    C[3] = C[1];                 C[4] = q.S11 - nn * m1 * m1; C[5] = q.S12 - nn * m1 * m2;
+    C[6] = C[2];                 C[7] = C[5];                 C[8] = q.S22 - nn * m2 * m2;
+    xa = g.o[0] + (double)cx * g.h + (double)qx + m0;
+    ya = g.o[1] + (double)cy * g.h + (double)qy + m1;
+    za = g.o[2] + (double)cz * g.h + (double)qz + m2;
+}
+
+// the rows h16_plane left to the Jacobi core
+__global__ __launch_bounds__(kB) void k_h16_cw_planes_fb(H16Args a, const CwSums* __restrict__ sums, const int64_t* __restrict__ list,
+                                                         const uint32_t* __restrict__ nlist, pcp_plane* __restrict__ out_nrm) {
+    const uint32_t m = *nlist;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const int64_t s = list[i];
+        double C[9], xa, ya, za;
+        cw_cov(a, s, sums[s], C, xa, ya, za);
+        pcp_plane pl;
+        plane_from_cov(C, xa, ya, za, pl);
+        out_nrm[a.mapping[s]] = pl;
+    }
+}
+
+// the planes of k_h16_cw's sums (sorted order): H16Acc::finish's fp64 covariance, then h16_plane
+__global__ __launch_bounds__(kB) void k_h16_cw_planes(H16Args a, const CwSums* __restrict__ sums, pcp_plane* __restrict__ out_nrm,
+                                                      int64_t* __restrict__ fb, uint32_t* __restrict__ nfb) {
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < a.n; s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t caller = a.mapping[s];
+        if (caller >= a.n_owned) continue;
+        const CwSums q = sums[s];
+        pcp_plane pl{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
+        if (q.n > 0) {
+            double C[9], xa, ya, za;
+            cw_cov(a, s, q, C, xa, ya, za);
+            if (!h16_plane(C, xa, ya, za, pl)) {
+                fb[atomicAdd(nfb, 1u)] = s;
+                continue;
+            }
+        }
+        out_nrm[caller] = pl;
+    }
+}
+
 H16Args make_args(const pcp_index* ix, float r, int64_t n_owned) {
     H16Args a{};
     a.g = ix->g;
@@ -735,6 +1145,15 @@ bool h16_direct_mode() {
 }
 // the fused count (1, default) or count-only + full fill (PCP_H16_FUSED=0); PCP_H16_FUSED_STRIDE
 // overrides the staging stride (tests force overflowing rows with a small one)
+// the cell-wave kernels (1, default) or the per-lane / tile forms (PCP_H16_CW=0, for A/B)
+bool h16_cw_mode() {
+    const char* e = getenv("PCP_H16_CW");
+    return e ? atoi(e) != 0 : PCP_H16_CW_DEFAULT != 0;
+}
+unsigned cw_blocks(int64_t n) {
+    const int64_t waves = (n + 63) / 64;
+    return (unsigned)std::min<int64_t>(std::max<int64_t>((waves + kCwWaves - 1) / kCwWaves, 1), 1 << 20);
+}
 bool h16_fused_mode() {
     const char* e = getenv("PCP_H16_FUSED");
     return e ? atoi(e) != 0 : PCP_H16_FUSED_DEFAULT != 0;
@@ -813,6 +1232,12 @@ int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_
         ixm->h16_inv_cap = n_owned;
     }
     ixm->h16_fused_r = -1.f;
+    if (h16_cw_mode()) {
+        hipLaunchKernelGGL(k_h16_cw<false>, dim3(cw_blocks(ix->n)), dim3(kB), 0, ctx->stream, a, count_dev,
+                           (const int64_t*)nullptr, (const int32_t*)nullptr, (int32_t*)nullptr, (CwSums*)nullptr);
+        PCP_LAUNCH_CHECK(ctx);
+        return PCP_OK;
+    }
     if (!h16_tile_mode() && h16_fused_mode()) {
         // the fused count: rows, planes and the overflow list for the fill; needs ~4 x stride
         // bytes per point of staging, so it gives way to the two-pass form when that is not there
@@ -923,6 +1348,36 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
                            n_owned);
     if (ix->n == 0) return PCP_OK;
     const H16Args a = make_args(ix, radius, n_owned);
+    if (h16_cw_mode()) {  // rows straight into the caller's CSR, sums in sorted order, then the planes
+        int32_t* ids = nullptr;
+        CwSums* sm = nullptr;
+        struct Free {
+            pcp_ctx* c; int32_t** a; CwSums** b;
+            ~Free() { dfree(c, *a); dfree(c, *b); }
+        } fr{ctx, &ids, &sm};
+        PCP_TRY(dmalloc(ctx, &ids, (size_t)ix->n));
+        if (normals_dev) PCP_TRY(dmalloc(ctx, &sm, (size_t)ix->n));
+        hipLaunchKernelGGL(k_h16_ids, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, (const int32_t*)ix->mapping,
+                           global_id_dev, ix->n, ids);
+        hipLaunchKernelGGL(k_h16_cw<true>, dim3(cw_blocks(ix->n)), dim3(kB), 0, ctx->stream, a, (int32_t*)nullptr,
+                           offsets_dev, (const int32_t*)ids, idx_dev, sm);
+        if (normals_dev) {
+            int64_t* fb = nullptr;
+            struct FreeFb {
+                pcp_ctx* c; int64_t** a;
+                ~FreeFb() { dfree(c, *a); }
+            } ffb{ctx, &fb};
+            PCP_TRY(dmalloc(ctx, &fb, (size_t)ix->n + 1));
+            uint32_t* nfb = (uint32_t*)(fb + ix->n);
+            PCP_HIP(ctx, hipMemsetAsync(nfb, 0, sizeof(uint32_t), ctx->stream));
+            hipLaunchKernelGGL(k_h16_cw_planes, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a,
+                               (const CwSums*)sm, normals_dev, fb, nfb);
+            hipLaunchKernelGGL(k_h16_cw_planes_fb, dim3(256), dim3(kB), 0, ctx->stream, a, (const CwSums*)sm,
+                               (const int64_t*)fb, (const uint32_t*)nfb, normals_dev);
+        }
+        PCP_LAUNCH_CHECK(ctx);
+        return PCP_OK;
+    }
     int64_t total = 0;
     PCP_HIP(ctx, hipMemcpyAsync(&total, offsets_dev + n_owned, sizeof(total), hipMemcpyDeviceToHost, ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -144,6 +144,7 @@ def test_h16_tile_matches_per_lane_kernel(ctx, scene, monkeypatch):
     per-candidate arithmetic and visiting order); both are checked against the oracle above."""
     from pointcloudprocess_amd import ops
     out = {}
+    monkeypatch.setenv("PCP_H16_CW", "0")  # the forms before the cell-wave kernels
     for mode in ("1", "0"):
         monkeypatch.setenv("PCP_H16_TILE", mode)
         ix = ops.H16Index(ctx, torch.from_numpy(scene).to(ctx.device), cell_size=R)
@@ -159,6 +160,7 @@ def test_h16_direct_fill_matches_staged(ctx, scene, monkeypatch):
     (PCP_H16_DIRECT=1) against the staged rows + copy pass (0): byte-identical CSR and normals."""
     from pointcloudprocess_amd import ops
     out = {}
+    monkeypatch.setenv("PCP_H16_CW", "0")
     monkeypatch.setenv("PCP_H16_TILE", "1")  # the direct fill is a form of the tile kernel
     for mode in ("1", "0"):
         monkeypatch.setenv("PCP_H16_DIRECT", mode)
@@ -184,6 +186,7 @@ def test_h16_fused_count_matches_two_pass(ctx, scene, monkeypatch):
     gid = torch.from_numpy(np.random.default_rng(11).permutation(n).astype(np.int32) * 3 + 5).to(ctx.device)
     lib = ctx.lib
     out = {}
+    monkeypatch.setenv("PCP_H16_CW", "0")
     for mode, stride in (("0", None), ("1", None), ("1", "32"), ("1", "16")):
         monkeypatch.setenv("PCP_H16_FUSED", mode)
         if stride:
@@ -210,3 +213,69 @@ def test_h16_fused_count_matches_two_pass(ctx, scene, monkeypatch):
     for key in (("1", None), ("1", "32"), ("1", "16")):
         for a, b in zip(out[key], ref):
             assert torch.equal(a, b), key
+
+
+def _radius_all(ctx, xyz, gid=None, n_owned=None):
+    """count + scan + fill through the C-ABI (caller ids, and global ids when given)."""
+    import ctypes as C
+    from pointcloudprocess_amd import ops
+    n = xyz.shape[0]
+    no = n if n_owned is None else n_owned
+    ix = ops.H16Index(ctx, torch.from_numpy(xyz).to(ctx.device), cell_size=R)
+    offs, idx, nrm = ix.radius_normals(R, n_owned=no)
+    res = [offs.cpu(), idx.cpu(), nrm.cpu()]
+    if gid is not None:
+        idx_g = torch.empty_like(idx)
+        nrm_g = torch.empty_like(nrm)
+        ctx.check(ctx.lib.pcp_h16_radius_fill(ctx.h, ix.h, float(R), no, C.c_void_p(offs.data_ptr()),
+                                              C.c_void_p(gid.data_ptr()), C.c_void_p(idx_g.data_ptr()),
+                                              C.c_void_p(nrm_g.data_ptr())))
+        torch.cuda.synchronize()
+        res += [idx_g.cpu(), nrm_g.cpu()]
+    ix.close()
+    return res
+
+
+def _normals_close(a, b):
+    """Two F1 plane arrays from the same rows with fp32 sums in different orders."""
+    a, b = a.numpy().astype(np.float64), b.numpy().astype(np.float64)
+    dot = np.abs((a[:, :3] * b[:, :3]).sum(1))
+    ok = np.isfinite(dot)
+    d = 1 - dot[ok]
+    curv = np.abs(a[ok, 4] - b[ok, 4])
+    print(f"cw vs per-lane normals: 1-|dot| p99 {np.percentile(d, 99):.3e} p99.99 {np.percentile(d, 99.99):.3e} "
+          f"max {d.max():.3e}; curvature diff max {curv.max():.3e}")
+    return np.percentile(d, 99.99) < 1e-5 and curv.max() < 1e-3
+
+
+def test_h16_cell_wave_matches_per_lane_kernel(ctx, scene, monkeypatch):
+    """The cell-wave kernels (default: one wave per query cell, lanes = candidates, hits
+    compacted by ballot straight into the caller CSR) against the per-lane kernel (PCP_H16_CW=0):
+    the same row lengths and the same rows in the same order, byte for byte, with caller indices,
+    with global ids and with an owned prefix (halo queries skipped); normals from the same rows
+    with fp32 sums in another order (tree, not sequential) agree to 1e-5 in 1-|n.n'|.  The
+    cloud adds a 4000-point clump inside one cell (a cell of more than 64 queries whose
+    neighbourhood overflows the 384 register candidates: the segment and block loops)."""
+    rng = np.random.default_rng(21)
+    base = scene[:500_000]
+    c0 = base[12345].astype(np.float64)
+    clump = (c0 + rng.uniform(-0.04, 0.04, size=(4000, 3))).astype(np.float32)
+    xyz = np.concatenate([base, clump])
+    n = xyz.shape[0]
+    perm = rng.permutation(n)
+    xyz = xyz[perm]  # the clump spread over caller order
+    gid = torch.from_numpy(rng.permutation(n).astype(np.int32) * 3 + 5).to(ctx.device)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PCP_H16_CW", mode)
+        out[mode] = (_radius_all(ctx, xyz, gid), _radius_all(ctx, xyz, n_owned=n // 3))
+    (a, ah), (b, bh) = out["1"], out["0"]
+    lens = (b[0][1:] - b[0][:-1]).numpy()
+    print(f"rows: mean {lens.mean():.1f}, max {lens.max()}")
+    assert lens.max() > 500  # the clump's rows
+    for i in (0, 1, 3):
+        assert torch.equal(a[i], b[i]), i
+    for i in (0, 1):
+        assert torch.equal(ah[i], bh[i]), ("owned", i)
+    assert _normals_close(a[2], b[2]) and _normals_close(a[4], b[4]) and _normals_close(ah[2], bh[2])
+    assert torch.equal(a[2].view(torch.int32), a[4].view(torch.int32))  # ids do not change the planes

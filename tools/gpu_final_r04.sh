@@ -16,7 +16,7 @@ python3 tools/pmc_summary.py $O/fetch $O/write > $O/pmc_traffic.json
 cp $O/pmc_traffic.json $P/pmc_traffic.json
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/C5fetch -o run -- python3 bench.py --config C5 --no-cpu --steps 1 --warmup 0 > $O/C5fetch.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/C5write -o run -- python3 bench.py --config C5 --no-cpu --steps 1 --warmup 0 > $O/C5write.log 2>&1
-python3 tools/pmc_summary.py --src=h16.hip $O/C5fetch $O/C5write k_h16_radius k_h16_tile k_h16_rows_to_caller tile_scan k_h16_ids k_h16_plane_default k_h16_sorted_counts > $O/pmc_traffic_C5.json
+python3 tools/pmc_summary.py --src=h16.hip $O/C5fetch $O/C5write k_h16_radius k_h16_tile k_h16_rows_to_caller tile_scan k_h16_ids k_h16_plane_default k_h16_sorted_counts k_h16_overflow k_h16_cw k_h16_cw_planes > $O/pmc_traffic_C5.json
 cp $O/pmc_traffic_C5.json $P/pmc_traffic_C5.json
 timeout -k 10 600 python3 -u bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu --steps 2 --warmup 1 > $O/trace_bench.log 2>&1
