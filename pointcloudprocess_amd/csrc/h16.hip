@@ -98,7 +98,24 @@ struct H16Args {
     uint32_t* nspill;
     uint32_t spill_rows;
     int64_t spill_base;
+    double inv_nx, inv_nxy;  // 1 / n[0], 1 / (n[0] n[1]): cell coordinates without integer division
 };
+
+// (cx, cy, cz) of dense cell id c: fp64 reciprocal products, each corrected by one step (the
+// product of a 32-bit id and a rounded reciprocal is off by < 2^-20, so the floor by at most one)
+__device__ __forceinline__ void cell_xyz(const GridDesc& g, const H16Args& a, uint32_t c, int& cx, int& cy, int& cz) {
+    const uint32_t nx = (uint32_t)g.n[0], nxy = nx * (uint32_t)g.n[1];
+    uint32_t z = (uint32_t)((double)c * a.inv_nxy);
+    z -= (uint64_t)z * nxy > c ? 1u : 0u;
+    z += (uint64_t)(z + 1u) * nxy <= c ? 1u : 0u;
+    const uint32_t rxy = c - z * nxy;
+    uint32_t y = (uint32_t)((double)rxy * a.inv_nx);
+    y -= y * nx > rxy ? 1u : 0u;
+    y += (y + 1u) * nx <= rxy ? 1u : 0u;
+    cx = (int)(rxy - y * nx);
+    cy = (int)y;
+    cz = (int)z;
+}
 
 // one lane per sorted point; halo points (caller index >= n_owned) are not queries
 // the id each sorted point is reported under (the global id of its caller index, or that index):
@@ -788,6 +805,7 @@ __global__ __launch_bounds__(kB, PCP_H16_CW_MINB) void k_h16_cw(H16Args a, int32
                                                const int32_t* __restrict__ ids, int32_t* __restrict__ out_idx,
                                                CwSums* __restrict__ sums) {
     __shared__ uint4 s_row[kCwWaves][9];  // per neighbour row: kk = j + off, the query column [b1, b2)
+    __shared__ float2 s_rdz[kCwWaves][9];  // per neighbour row: its dy h, dz h
     __shared__ float s_sum[kCwWaves][64 * 9];
     const GridDesc& g = a.g;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -805,9 +823,8 @@ __global__ __launch_bounds__(kB, PCP_H16_CW_MINB) void k_h16_cw(H16Args a, int32
             const uint32_t cid = (uint32_t)__builtin_amdgcn_readlane((int)cp, hl);
             const int64_t cs = w * 64 + hl;
             const int64_t ce = (int64_t)g.cstart[(int64_t)cid + 1];
-            const int cx = (int)(cid % (uint32_t)g.n[0]);
-            const int cy = (int)((cid / (uint32_t)g.n[0]) % (uint32_t)g.n[1]);
-            const int cz = (int)(cid / ((uint32_t)g.n[0] * (uint32_t)g.n[1]));
+            int cx, cy, cz;
+            cell_xyz(g, a, cid, cx, cy, cz);
             // the 9 rows (lane r: dz = r / 3 - 1, dy = r % 3 - 1), cells [cx - 1, cx + 1] clipped
             uint32_t len = 0;
             if (lane < 9) {
@@ -828,6 +845,7 @@ __global__ __launch_bounds__(kB, PCP_H16_CW_MINB) void k_h16_cw(H16Args a, int32
                     pre += k < lane ? lk : 0u;
                 }
                 s_row[wid][lane] = make_uint4(k0 - pre, b1, b2, pre);
+                s_rdz[wid][lane] = make_float2((float)(lane % 3 - 1) * hf, (float)(lane / 3 - 1) * hf);
             }
             uint32_t P[9];  // wave-uniform row starts in the concatenated list, and M
             {
@@ -864,8 +882,9 @@ __global__ __launch_bounds__(kB, PCP_H16_CW_MINB) void k_h16_cw(H16Args a, int32
                     coz[s] = h_lo(pr.y);
                     // past the list: a finite far offset (d2 ~ 1e38 >= r^2, never a hit)
                     cdx[s] = ok ? (kk < row.y ? -hf : (kk < row.z ? 0.f : hf)) : 1e19f;
-                    cdy[s] = (float)(r % 3 - 1) * hf;
-                    cdz[s] = (float)(r / 3 - 1) * hf;
+                    const float2 rdz = s_rdz[wid][r];
+                    cdy[s] = rdz.x;
+                    cdz[s] = rdz.y;
                 }
             };
             // the per-lane kernel's expression (h16_point), op for op: same d2, same hit set
@@ -1069,10 +1088,8 @@ __device__ inline void cw_cov(const H16Args& a, int64_t s, const CwSums& q, doub
     const GridDesc& g = a.g;
     const uint2 qr = a.rec[s];
     const float qx = h_lo(qr.x), qy = h_hi(qr.x), qz = h_lo(qr.y);
-    const uint32_t cid = a.cell[s];
-    const int cx = (int)(cid % (uint32_t)g.n[0]);
-    const int cy = (int)((cid / (uint32_t)g.n[0]) % (uint32_t)g.n[1]);
-    const int cz = (int)(cid / ((uint32_t)g.n[0] * (uint32_t)g.n[1]));
+    int cx, cy, cz;
+    cell_xyz(g, a, a.cell[s], cx, cy, cz);
     const double nn = (double)q.n;
     const double m0 = q.S0 / nn, m1 = q.S1 / nn, m2 = q.S2 / nn;
     C[0] = q.S00 - nn * m0 * m0; C[1] = q.S01 - nn * m0 * m1; C[2] = q.S02 - nn * m0 * m2;
@@ -1127,6 +1144,8 @@ H16Args make_args(const pcp_index* ix, float r, int64_t n_owned) {
     a.n_owned = n_owned;
     a.hf = (float)ix->g.h;
     a.r2 = r * r;
+    a.inv_nx = 1.0 / (double)ix->g.n[0];
+    a.inv_nxy = 1.0 / ((double)ix->g.n[0] * (double)ix->g.n[1]);
     const float rc = r * 1.0001f + 2e-4f;  // conservative: fp16 offsets and fp32 face gaps
     a.rcut2 = rc * rc;
     return a;
