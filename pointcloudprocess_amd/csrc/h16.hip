@@ -1235,8 +1235,10 @@ int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_
     PCP_TRY(check_query(ctx, ix, radius, n_owned));
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     if (n_owned == 0) return PCP_OK;
-    // rows of owned points the build dropped as non-finite stay empty
-    PCP_HIP(ctx, hipMemsetAsync(count_dev, 0, (size_t)n_owned * sizeof(int32_t), ctx->stream));
+    // rows of owned points the build dropped as non-finite stay empty (the cell-wave count writes
+    // every point of the index, so with nothing dropped there is nothing to clear)
+    if (!(h16_cw_mode() && ix->n == ix->n_in))
+        PCP_HIP(ctx, hipMemsetAsync(count_dev, 0, (size_t)n_owned * sizeof(int32_t), ctx->stream));
     if (ix->n == 0) return PCP_OK;
     const H16Args a = make_args(ix, radius, n_owned);
     // keep the sorted-order row lengths and the inverse map for the fill of the same query set
@@ -1362,7 +1364,8 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
         PCP_LAUNCH_CHECK(ctx);
         return PCP_OK;
     }
-    if (normals_dev)
+    // planes of points the build dropped; the cell-wave fill writes every point of the index
+    if (normals_dev && !(h16_cw_mode() && ix->n == ix->n_in))
         hipLaunchKernelGGL(k_h16_plane_default, dim3(grid_for(n_owned, kB)), dim3(kB), 0, ctx->stream, normals_dev,
                            n_owned);
     if (ix->n == 0) return PCP_OK;

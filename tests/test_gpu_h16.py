@@ -306,3 +306,27 @@ def test_h16_cell_wave_radius_below_cell_and_tiny_clouds(ctx, scene, monkeypatch
             assert torch.allclose(a[2], b[2], atol=1e-6, equal_nan=True), (len(xyz), a[2], b[2])
         else:
             assert _normals_close(a[2], b[2])
+
+
+def test_h16_cell_wave_dropped_points(ctx, scene, monkeypatch):
+    """Non-finite points are dropped by the build: their rows stay empty and their planes keep the
+    default, in the cell-wave path (which skips the clears when nothing was dropped) as in the
+    per-lane one."""
+    from pointcloudprocess_amd import ops
+    xyz = np.ascontiguousarray(scene[:50_000]).copy()
+    xyz[[3, 777, 4000]] = np.nan
+    xyz[12345, 1] = np.inf
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PCP_H16_CW", mode)
+        ix = ops.H16Index(ctx, torch.from_numpy(xyz).to(ctx.device), cell_size=R)
+        offs, idx, nrm = ix.radius_normals(R)
+        out[mode] = (offs.cpu(), idx.cpu(), nrm.cpu())
+        ix.close()
+    a, b = out["1"], out["0"]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    lens = a[0][1:] - a[0][:-1]
+    for k in (3, 777, 4000, 12345):
+        assert int(lens[k]) == 0
+        assert torch.equal(a[2][k], torch.tensor([0.0, 0.0, 0.0, 0.0, 1.0, 0.0]))
+    assert _normals_close(a[2], b[2])
