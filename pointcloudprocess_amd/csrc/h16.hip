@@ -870,9 +870,12 @@ __global__ __launch_bounds__(kB, PCP_H16_CW_MINB) void k_h16_cw(H16Args a, int32
                     if (blk + 64u * s >= M) break;  // (uniform) the block's steps past the list are never read
                     const uint32_t j = blk + 64u * s + (uint32_t)lane;
                     const bool ok = j < M;
-                    int r = 0;
-#pragma unroll
-                    for (int k = 1; k < 9; k++) r += j >= P[k] ? 1 : 0;
+                    // the row of list entry j: the largest r with P[r] <= j (binary search over the
+                    // uniform row starts; P[8] then settles the last row)
+                    int r = j >= P[4] ? 4 : 0;
+                    r += j >= (r ? P[6] : P[2]) ? 2 : 0;
+                    r += j >= (r == 0 ? P[1] : r == 2 ? P[3] : r == 4 ? P[5] : P[7]) ? 1 : 0;
+                    r += (r == 7 && j >= P[8]) ? 1 : 0;
                     const uint4 row = s_row[wid][r];
                     const uint32_t kk = ok ? j + row.x : 0u;
                     const uint2 pr = a.rec[kk];
@@ -909,14 +912,13 @@ __global__ __launch_bounds__(kB, PCP_H16_CW_MINB) void k_h16_cw(H16Args a, int32
                     if (FILL && caller < a.n_owned) base = offsets[caller];
                 }
                 int32_t cntv = 0;  // lane i: the row length of query i of the segment
+                const uint64_t ownm = __ballot(lane < nseg && caller < a.n_owned);  // the segment's queries
                 if constexpr (!FILL) {
                     // count: two queries at a time (the tests as packed fp32: v_pk_add/mul/fma_f32
                     // round each half exactly as the scalar ops), one ballot per query and step
                     for (int qi = 0; qi < nseg; qi += 2) {
                         const int q1 = min(qi + 1, 63);
-                        const bool a0 = __builtin_amdgcn_readlane(caller, qi) < a.n_owned;
-                        const bool a1 = qi + 1 < nseg && __builtin_amdgcn_readlane(caller, q1) < a.n_owned;
-                        if (!a0 && !a1) continue;
+                        if (!((ownm >> qi) & 3ull)) continue;
                         const f2 sx = {__int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), qi)),
                                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), q1))};
                         const f2 sy = {__int_as_float(__builtin_amdgcn_readlane(__float_as_int(qy), qi)),
@@ -956,7 +958,7 @@ __global__ __launch_bounds__(kB, PCP_H16_CW_MINB) void k_h16_cw(H16Args a, int32
                             sqx[qi] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), q));
                             sqy[qi] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qy), q));
                             sqz[qi] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qz), q));
-                            act[qi] = qb + qi < nseg && __builtin_amdgcn_readlane(caller, q) < a.n_owned;
+                            act[qi] = (ownm >> q) & 1ull && qb + qi < nseg;
                             const uint64_t bq = (uint64_t)base;
                             sbase[qi] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bq, q)) |
                                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bq >> 32), q) << 32));
@@ -1377,12 +1379,17 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
             pcp_ctx* c; int32_t** a; CwSums** b;
             ~Free() { dfree(c, *a); dfree(c, *b); }
         } fr{ctx, &ids, &sm};
-        PCP_TRY(dmalloc(ctx, &ids, (size_t)ix->n));
         if (normals_dev) PCP_TRY(dmalloc(ctx, &sm, (size_t)ix->n));
-        hipLaunchKernelGGL(k_h16_ids, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, (const int32_t*)ix->mapping,
-                           global_id_dev, ix->n, ids);
+        // the reported ids: the caller indices (the index's own mapping), or their global ids
+        const int32_t* rep_ids = ix->mapping;
+        if (global_id_dev) {
+            PCP_TRY(dmalloc(ctx, &ids, (size_t)ix->n));
+            hipLaunchKernelGGL(k_h16_ids, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream,
+                               (const int32_t*)ix->mapping, global_id_dev, ix->n, ids);
+            rep_ids = ids;
+        }
         hipLaunchKernelGGL(k_h16_cw<true>, dim3(cw_blocks(ix->n)), dim3(kB), 0, ctx->stream, a, (int32_t*)nullptr,
-                           offsets_dev, (const int32_t*)ids, idx_dev, sm);
+                           offsets_dev, rep_ids, idx_dev, sm);
         if (normals_dev) {
             int64_t* fb = nullptr;
             struct FreeFb {
