@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--no-alt", action="store_true", help="N > 1: skip the alt_modes runs")
     ap.add_argument("--c5-points", type=int, default=200_000_000,
                     help="--config C5: points per GPU (the 200M-pt scene fits one GPU)")
+    ap.add_argument("--c5-check", type=int, default=0,
+                    help="--config C5 at N > 1: after timing, compare this many sampled rows per rank with the "
+                         "single-process rows (rehearsal check)")
     ap.add_argument("--config", choices=("C1", "C2", "C3", "C4", "C5"), default="C4")
     return ap.parse_args()
 
@@ -94,12 +97,15 @@ def launch(args):
     return subprocess.call(cmd, env=env)
 
 
-def pmc_traffic():
+def pmc_traffic(workload):
     """HBM bytes per ICP iteration (k_icp_verify + k_icp_octant + k_icp_ring, FETCH_SIZE x2 +
     WRITE_SIZE, summed over the profiled launches / iterations) from the newest
-    profiles/*/pmc_traffic.json measured on THIS icp.hip (sha1 match), else None.
+    profiles/*/pmc_traffic.json measured on THIS icp.hip (sha1 match) AND on this run's workload
+    (its "workload" record equals `workload`: points per cloud, world size, mode), else None --
+    counters of another size or rank count say nothing about this line's kernels.
     Made by: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) of
-    `bench.py --steps 1 --warmup 0 --no-cpu`, summarised by tools/pmc_summary.py."""
+    `bench.py --steps 1 --warmup 0 --no-cpu`, summarised by tools/pmc_summary.py --key=n=...
+    --key=world=... --key=mode=..."""
     src = os.path.join(ROOT, "pointcloudprocess_amd", "csrc", "icp.hip")
     sha = hashlib.sha1(open(src, "rb").read()).hexdigest()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), key=os.path.getmtime,
@@ -108,7 +114,7 @@ def pmc_traffic():
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("icp_hip_sha1") != sha:
+        if d.get("icp_hip_sha1") != sha or d.get("workload") != workload:
             continue
         ks = d["kernels"]
         if "k_icp_octant" not in ks:
@@ -397,7 +403,7 @@ def main():
 
     if rank == 0:
         r = main_rec
-        traffic = pmc_traffic()
+        traffic = pmc_traffic({"n": n, "world": world, "mode": args.mode})
         k_avg_ms = r["kernel_avg_ms"]
         achieved = BYTES_PER_CORR * r["units_per_launch"] / (k_avg_ms * 1e-3) / 1e9  # algorithmic GB/s per launch
         par = {"slab": f"x-slabs x{world}: owned queries + targets of the slab +- {args.halo} m halo per rank; "
@@ -441,7 +447,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": round(traffic[0] / (k_avg_ms * 1e-3) / 1e9, 2) if traffic else None,
                 "traffic_bytes_per_launch": round(traffic[0]) if traffic else None,
-                "traffic_source": traffic[1] if traffic else None,
+                "traffic_source": traffic[1] if traffic else "none: no sha-matched PMC record of this workload "
+                                                             f"(n {n}, world {world}, mode {args.mode})",
                 "kernel_avg_ms": round(k_avg_ms, 4),
                 "bytes_per_unit": BYTES_PER_CORR,
                 "units_per_launch": r["units_per_launch"],

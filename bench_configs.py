@@ -54,17 +54,18 @@ _ORA = {}
 PMC_KERNELS = {
     "C2": ("knn_bf.hip", ("k_bf_mfma", "k_bf_fallback", "k_bf_targets", "k_bf_pad")),
     "C3": ("knn.hip", ("k_normals_tile", "k_normals", "k_normals_coop", "k_brick_keys", "k_plane_default")),
-    "C5": ("h16.hip", ("k_h16_radius", "k_h16_tile", "k_h16_rows_to_caller", "tile_scan", "k_h16_ids",
-                       "k_h16_plane_default", "k_h16_sorted_counts", "k_h16_overflow", "k_h16_cw", "k_h16_cw_planes")),
+    "C5": ("h16.hip", ("k_h16_mx", "k_h16_mx_planes", "k_h16_mx_planes_fb", "tile_scan", "k_h16_ids",
+                       "k_h16_plane_default")),
 }
 
 
-def pmc_traffic(cfg, calls=1):
+def pmc_traffic(cfg, workload, calls=1):
     """HBM bytes per timed call (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction)
     of the config's kernels, from the newest profiles/*/pmc_traffic_<cfg>.json measured on the
-    current source of those kernels (sha1 match), else None.  Made by tools/pmc_summary.py
-    --src=<file> from separate FETCH_SIZE / WRITE_SIZE passes of `bench.py --config <cfg> --steps 1
-    --warmup 0 --no-cpu` (one timed call)."""
+    current source of those kernels (sha1 match) and on this run's workload (its "workload" record
+    equals `workload`: points per rank, world size, split), else None.  Made by tools/pmc_summary.py
+    --src=<file> --key=... from separate FETCH_SIZE / WRITE_SIZE passes of `bench.py --config <cfg>
+    --steps 1 --warmup 0 --no-cpu` (one timed call)."""
     import glob
     import hashlib
     src, kernels = PMC_KERNELS[cfg]
@@ -75,7 +76,7 @@ def pmc_traffic(cfg, calls=1):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("src_sha1") != sha:
+        if d.get("src_sha1") != sha or d.get("workload") != workload:
             continue
         tot = 0.0
         for k in kernels:
@@ -86,12 +87,15 @@ def pmc_traffic(cfg, calls=1):
     return None
 
 
-def _with_traffic(roof, cfg):
-    t = pmc_traffic(cfg)
+def _with_traffic(roof, cfg, workload):
+    t = pmc_traffic(cfg, workload)
     if roof is not None and t is not None:
         roof["traffic"] = round(t[0] / (roof["kernel_avg_ms"] * 1e-3) / 1e9, 2)
         roof["traffic_bytes_per_launch"] = round(t[0])
         roof["traffic_source"] = t[1]
+    elif roof is not None:
+        roof["traffic"] = None
+        roof["traffic_source"] = f"none: no sha-matched PMC record of this workload {workload}"
     return roof
 
 
@@ -285,38 +289,94 @@ def cfg_c3(ctx, args, rank, timer):
 
 
 def cfg_c5(ctx, args, rank, timer):
+    """N = 1: the 200M-point scene on one GPU.  N > 1 (strong scaling): the SAME scene split into
+    equal-count x-slabs, each rank indexing its slab plus the points within r of its faces (the
+    halo) and producing the rows and planes of its owned points with global ids; no collective
+    (distributed.radius_slab_split_dev)."""
+    from pointcloudprocess_amd import distributed as D
     from pointcloudprocess_amd import ops, synth
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    R = 0.2
     n = int(args.c5_points)
     side = math.sqrt(n / 1.5e6) * 40.0  # the C5 test density (1.5M pts on 40 x 40 m)
-    xyz = synth.street_scene(n, 5001 + 1000 * rank, extent=(side, side), device=ctx.device)
+    xyz = synth.street_scene(n, 5001, extent=(side, side), device=ctx.device)
+    own = halo = gid = None
+    if world > 1:
+        own, halo = D.radius_slab_split_dev(xyz[:, 0].contiguous(), world, rank, R)
+        gid_t = torch.cat([own, halo])
+        xyz = xyz[gid_t].contiguous()
+        gid = gid_t.to(torch.int32)
+        del gid_t
+    n_owned = n if own is None else int(own.numel())
     ktimer = Timer()
+    btimer = Timer()
     state = {}
 
     def step(timed):
         def run():
-            ix = ops.H16Index(ctx, xyz, cell_size=0.2)
-            if timed:
-                offs, idx, nrm = ktimer(lambda: ix.radius_normals(0.2))
-            else:
-                offs, idx, nrm = ix.radius_normals(0.2)
+            ix = btimer(lambda: ops.H16Index(ctx, xyz, cell_size=R)) if timed else ops.H16Index(ctx, xyz, cell_size=R)
+            fn = lambda: ix.radius_normals(R, n_owned=n_owned, global_id=gid)
+            offs, idx, nrm = ktimer(fn) if timed else fn()
             state["nnz"] = idx.numel()
             ix.close()
             return nrm
         timer(run) if timed else run()
 
-    info = {"unit": "Mpoints/s", "units_per_step": n, "dtype": "fp16 coords / f32 accum",
-            "workload": f"C5: radiusSearch r=0.2 + normals over the fp16 cell-relative index, {n} pts per GPU "
-                        f"({side:.0f} x {side:.0f} m street scene at the 200M-pt scene's density)"}
+    par = (f"x-slabs x{world}: a rank indexes its equal-count slab + the points within r of its faces "
+           f"(halo) and writes its owned points' rows (global ids) and planes; no collective") if world > 1 else \
+        "x1"
+    info = {"unit": "Mpoints/s", "units_per_step": n_owned, "units_all_ranks_per_step": n,
+            "scaling": "strong" if world > 1 else "weak", "parallelism": par,
+            "dtype": "fp16 coords / f32 accum",
+            "pmc_key": {"n": n, "world": world},
+            "workload": f"C5: radiusSearch r=0.2 + normals over the fp16 cell-relative index, the {n}-pt street "
+                        f"scene ({side:.0f} x {side:.0f} m)" + (f", split into {world} x-slabs with an r halo"
+                                                               if world > 1 else " on one GPU")}
+
+    def per_rank():
+        return {"owned_points": n_owned, "halo_points": 0 if halo is None else int(halo.numel()),
+                "index_build_ms": round(btimer.avg, 3), "rows_normals_ms": round(ktimer.avg, 3)}
+    info["per_rank_fn"] = per_rank
 
     def roof(ms_step):
         ms = ktimer.avg
-        nbar = state["nnz"] / n
-        byts = n * (6 + 4 * nbar + 16 + 4)
-        return {"bound": "hbm", "kernel": "pcp_h16_radius_count + scan + pcp_h16_radius_fill (rows + normals)",
+        nbar = state["nnz"] / max(n_owned, 1)
+        byts = n_owned * (6 + 4 * nbar + 16 + 4)
+        return {"bound": "hbm", "kernel": "pcp_h16_radius_count + scan + pcp_h16_radius_fill (rows + normals; "
+                                          "k_h16_mx on the matrix cores)",
                 "achieved": round(byts / ms / 1e6, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None, "kernel_avg_ms": round(ms, 4),
-                "units_per_launch": n, "bytes_per_unit": round(6 + 4 * nbar + 16 + 4, 2), "nbar": round(nbar, 2)}
+                "units_per_launch": n_owned, "bytes_per_unit": round(6 + 4 * nbar + 16 + 4, 2), "nbar": round(nbar, 2)}
     info["roofline_fn"] = roof
+
+    def check(nsample=20_000):
+        """N > 1: this rank's rows of a seeded global sample of its owned points against the rows of
+        the whole cloud indexed on this rank (single-process rows): equal as sets except pairs
+        within the fp16 band of r (the slab's grid origin quantises differently)."""
+        full = synth.street_scene(n, 5001, extent=(side, side), device=ctx.device)
+        ixf = ops.H16Index(ctx, full, cell_size=R)
+        offs_f, idx_f, _ = ixf.radius_normals(R, normals=False)
+        ixf.close()
+        ix = ops.H16Index(ctx, xyz, cell_size=R)
+        offs_l, idx_l, _ = ix.radius_normals(R, n_owned=n_owned, global_id=gid, normals=False)
+        ix.close()
+        g = torch.Generator(device="cpu")
+        g.manual_seed(77 + rank)
+        pick = torch.randint(0, n_owned, (nsample,), generator=g).to(ctx.device)
+        gq = own[pick]
+
+        def pairs(offs, idx, s):  # (sample slot * n + neighbour id) of the rows of queries s
+            lens = offs[s + 1] - offs[s]
+            row_of = torch.repeat_interleave(torch.arange(s.numel(), device=s.device), lens)
+            pos = offs[s][row_of] + (torch.arange(row_of.numel(), device=s.device) - (torch.cumsum(lens, 0) - lens)[row_of])
+            return row_of * n + idx[pos].long()
+        keys, cnt = torch.unique(torch.cat([pairs(offs_l, idx_l, pick), pairs(offs_f, idx_f, gq)]), return_counts=True)
+        odd = keys[cnt == 1]  # in one of the two rows only
+        d = torch.linalg.norm(full[odd % n].double() - full[gq[odd // n]].double(), dim=1)
+        diff_out = int(odd.numel())
+        bad = int(((d - R).abs() >= 3e-4).sum())
+        return {"sampled_rows": nsample, "pairs_differing": diff_out, "pairs_differing_outside_band": bad}
+    info["check_fn"] = check
 
     def cpu():
         ora = _oracle()
@@ -345,10 +405,15 @@ def main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("PCP_BENCH_DEVICE", local))  # rehearsal: every rank on one device
+    backend = os.environ.get("PCP_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     ctx = ops.Context(local)
 
     def barrier():
@@ -366,7 +431,23 @@ def main(args):
     step, info, cpu = {"C1": cfg_c1, "C2": cfg_c2, "C3": cfg_c3, "C5": cfg_c5}[args.config](ctx, args, rank, timer)
     dt = run_steps(step, args.steps, args.warmup, barrier)
     dt = reduce(dt, dist.ReduceOp.MAX if world > 1 else None)
-    units = info["units_per_step"] * args.steps * world
+    units = info.get("units_all_ranks_per_step", info["units_per_step"] * world) * args.steps
+    per_rank = None
+    if "per_rank_fn" in info and world > 1:
+        mine = info["per_rank_fn"]()
+        keys = sorted(mine)
+        slots = torch.zeros(world * len(keys), dtype=torch.float64, device=dev)
+        for j, k in enumerate(keys):
+            slots[rank * len(keys) + j] = float(mine[k])
+        dist.all_reduce(slots, op=dist.ReduceOp.SUM)
+        slots = slots.cpu().tolist()
+        per_rank = [{"rank": r, **{k: slots[r * len(keys) + j] for j, k in enumerate(keys)}} for r in range(world)]
+    check = None
+    if getattr(args, "c5_check", 0) and "check_fn" in info and world > 1:
+        mine = info["check_fn"](args.c5_check)
+        t = torch.tensor([float(mine[k]) for k in sorted(mine)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        check = {k: int(v) for k, v in zip(sorted(mine), t.cpu().tolist())}
     roof = info.get("roofline_fn")
     line = {
         "metric": f"{args.config} throughput ({info['unit']})",
@@ -377,13 +458,17 @@ def main(args):
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": info.get("scaling", "weak"),
         "vs_baseline": None,
         "dtype": info["dtype"],
         "data": "synthetic (seeded); every rank its own batch",
-        "config": {"workload": info["workload"], "parallelism": f"x{world} independent batches, no collective"},
+        "config": {"workload": info["workload"],
+                   "parallelism": info.get("parallelism", f"x{world} independent batches, no collective")},
+        "per_rank": per_rank,
+        "slab_rows_check": check,
         "device_ms_per_step": round(timer.avg, 3),
-        "roofline": _with_traffic(roof(timer.avg), args.config) if roof else None,
+        "roofline": _with_traffic(roof(timer.avg), args.config, info.get("pmc_key", {"n": info["units_per_step"],
+                                                                                     "world": world})) if roof else None,
         "build_id": ctx.lib.pcp_build_id().decode(),  # SHA-1 of the libpcp sources (provenance)
         "cpu_baseline": None,
     }

@@ -124,17 +124,13 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_
  * rows in index order (radiusSearch with setSortedResults(false), kd_tree.h:739-753,863-903)
  * as global_id_dev[caller] (or the caller index when NULL), and optionally one F1 plane per
  * row (calculate_plan_parameter(cloud, radius), calculate_feature.h:15) from fp32 sums.
- * Distances are fp32 of fp16 offsets: pairs within 3e-4 m of the radius may differ from an
- * exact search.
- * Memory: the count also stages every row and plane in the index (rows at a fixed stride of 96
- * entries + a spill pool: ~400 B per indexed point, held until the next count or
- * pcp_index_destroy) so that the fill only moves them; when that memory is not available the
- * count keeps only the row lengths and the fill searches again (same results).
- * Threading: the count keeps its sorted-order row lengths in the index for the fill of the
- * same (radius, n_owned) that follows it, so count -> fill pairs on ONE index must not
- * interleave across threads or streams (serialize them, or give each caller its own index);
- * a fill whose count was superseded still returns the right rows (it gathers the lengths
- * back from its offsets) only when the interleaving count finished before it started. */
+ * The hit test and the plane sums run on the matrix cores (fp32 d^2 - r^2 expansion, f16 moment
+ * features with fp32 accumulation): pairs within 3e-4 m of the radius may differ from an exact
+ * search (the fp16 offsets' quantisation).  n_owned must not exceed the indexed
+ * cloud's size (PCP_ERR_ARG).
+ * Memory: the fill takes ~48 B per indexed point of scratch for the plane sums (with normals),
+ * released when it returns; neither call keeps state in the index between calls, so calls on
+ * one index from different threads only need the context's usual serialisation. */
 int pcp_index_build_h16(pcp_ctx* ctx, const float* xyz_dev, size_t stride_bytes, int64_t n,
                         double cell_size, pcp_index** out);
 int pcp_h16_radius_count(pcp_ctx* ctx, const pcp_index* index, float radius, int64_t n_owned,
@@ -258,6 +254,25 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q_dev,
  * nq >= 2^31 or a negative size, PCP_ERR_CAPACITY for a target of 2^28 - 1 or more valid
  * points (the search passes address the fp32 target with 32-bit byte offsets). */
 int pcp_icp_check_sizes(int64_t n_target, int64_t nq);
+/* pcp_index_build_f32 + pcp_icp_create in one call: the query set's sort runs on a second
+ * stream while the target's cell sort runs (the two radix sorts of the create overlap).  Same
+ * results and handles as the two calls; destroy both (the ICP handle first). */
+int pcp_icp_create_with_target(pcp_ctx* ctx, const float* target_dev, size_t target_stride_bytes,
+                               int64_t n_target, double cell_size, const float* q_dev,
+                               size_t q_stride_bytes, int64_t nq, pcp_index** index_out,
+                               pcp_icp** icp_out);
+/* Test / profiling controls of an ICP handle (not needed by callers):
+ *   oct_lanes_first, oct_lanes_list: lanes per query of the octant search pass at the first
+ *     launch and over the later search lists (1, 2, 4, 8; 0 = by the list's density);
+ *   ring_lanes: lanes per query of the fallback pass (1, 2, 4, 8; 0 = by the list's length);
+ *   ablate: PCP_ICP_ABLATE_* flags that switch passes off for profiling -- results are WRONG
+ *     while any is set.
+ * Results are identical for every lane choice. */
+#define PCP_ICP_ABLATE_NO_SCAN 1
+#define PCP_ICP_ABLATE_NO_ACCUM 4
+#define PCP_ICP_ABLATE_NO_FALLBACK 8
+#define PCP_ICP_ABLATE_NO_VERIFY 64
+int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, int ring_lanes, int ablate);
 int pcp_icp_destroy(pcp_icp* icp);
 /* One iteration at pose T (row-major 4x4 double, cast to fp32 for the kernel):
  * correspondences within rmax + the 24 accumulators ([23] = queries that

@@ -81,6 +81,8 @@ SIGNATURES = [
     ("pcp_icp_create", _i32, [_vp, _vp, _vp, _sz, _i64, _P(_vp)]),
     ("pcp_icp_check_sizes", _i32, [_i64, _i64]),
     ("pcp_icp_destroy", _i32, [_vp]),
+    ("pcp_icp_create_with_target", _i32, [_vp, _vp, _sz, _i64, _f64, _vp, _sz, _i64, _P(_vp), _P(_vp)]),
+    ("pcp_icp_set_options", _i32, [_vp, _i32, _i32, _i32, _i32]),
     ("pcp_icp_step", _i32, [_vp, _vp, _P(_f64), _f32, _vp, _vp, _vp]),
     ("pcp_icp_keys", _i32, [_vp, _vp, _P(_f64), _f32, _i64, _vp]),
     ("pcp_icp_accumulate_keys", _i32, [_vp, _vp, _P(_f64), _vp, _i64, _i64, _vp, _sz, _vp]),
@@ -122,8 +124,11 @@ def load(path=LIB_PATH, bind_all=True):
             f"libpcp.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; "
             "g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
     lib = C.CDLL(path)
+    ab_build = bool(os.environ.get("PCP_LIB"))  # an A/B build of an older tree may lack newer symbols
     if bind_all:
         for name, res, args in SIGNATURES:
+            if ab_build and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)  # AttributeError if the ABI symbol is missing
             fn.restype = res
             fn.argtypes = args

@@ -180,7 +180,7 @@ def do_mul_frame_icp(ctx, line, stamp_file, start_index, end_index, grid, valid_
     loaded = [load_cloud(p) for _, p in frames]  # (:754-765)
     clouds = [c[0] if isinstance(c, tuple) else c for c in loaded]
     def _finite(rec):  # a plain tensor carries no flag: its is_dense is the data's finiteness
-        xyz = rec.view(torch.float64).reshape(-1, 6)[:, :3]
+        xyz = rec.contiguous().view(torch.float64).reshape(-1, 6)[:, :3]  # any row / column slice
         return bool(torch.isfinite(xyz).all())
     dense = all(c[1] if isinstance(c, tuple) else _finite(c) for c in loaded)  # operator+= (point_cloud.h:143-146)
     frame = torch.cat(clouds) if clouds else torch.empty((0, 48), dtype=torch.uint8, device=ctx.device)

@@ -16,6 +16,9 @@ struct pcp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    // a non-blocking stream for work that overlaps the main stream inside one call (the query
+    // sort of pcp_icp_create_with_target); created on first use, ordered by events both ways
+    hipStream_t side = nullptr;
     std::string last_error;
     // grow-only scratch arena (one per context; contexts are not shared across threads)
     void* scratch = nullptr;
@@ -51,6 +54,8 @@ int set_error(pcp_ctx* ctx, int code, const char* fmt, ...);
 int hip_fail(pcp_ctx* ctx, hipError_t e, const char* what, const char* file, int line);
 // scratch of at least `bytes` (invalidates earlier scratch pointers)
 int scratch(pcp_ctx* ctx, size_t bytes, void** out);
+// the context's side stream (created on first use)
+int side_stream(pcp_ctx* ctx, hipStream_t* out);
 
 #define PCP_HIP(ctx, expr)                                                           \
     do {                                                                             \
@@ -148,24 +153,5 @@ struct pcp_index {
     int is_h16 = 0;
     uint2* h16 = nullptr;
     uint32_t* cell = nullptr;
-    // the last radius count's sorted-order row lengths (padded to 4) and caller -> sorted
-    // position, for the fill that follows it (same radius and n_owned)
-    int32_t* h16_cnt_s = nullptr;
-    int32_t* h16_inv = nullptr;
-    int64_t h16_inv_cap = 0;
-    float h16_last_r = -1.f;
-    int64_t h16_last_owned = -1;
-    // the fused count (h16.hip, PCP_H16_FUSED): the count pass also writes every row (fixed
-    // stride, sorted order, caller indices), the planes (caller order) and the list of rows longer
-    // than the stride; the fill of the same radius and query set then only moves them
-    int32_t* h16_rows = nullptr;
-    int64_t h16_rows_cap = 0;    // entries
-    pcp_plane* h16_planes = nullptr;
-    int32_t* h16_ovf = nullptr;  // sorted positions of the overflowed rows (+ their count, the spill count)
-    int32_t* h16_spill_of = nullptr;  // caller -> spill row (rows longer than the stride)
-    int64_t h16_ovf_cap = 0;
-    float h16_fused_r = -1.f;
-    int64_t h16_fused_owned = -1;
-    uint32_t h16_fused_stride = 0;
     pcp_ctx* owner = nullptr;
 };

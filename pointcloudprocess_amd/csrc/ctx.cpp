@@ -138,8 +138,15 @@ static void ctx_finish(pcp_ctx* ctx) {
     ctx->block_size.clear();
     for (hipEvent_t ev : ctx->event_pool) (void)hipEventDestroy(ev);
     ctx->event_pool.clear();
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+int side_stream(pcp_ctx* ctx, hipStream_t* out) {
+    if (!ctx->side) PCP_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+    *out = ctx->side;
+    return PCP_OK;
 }
 
 void ctx_retain(pcp_ctx* ctx) {
@@ -263,21 +270,22 @@ bool g_fault_installed = false;
 
 void fault_write(const char* s) { (void)!write(2, s, std::strlen(s)); }
 
-// async-signal-safe formatting (no snprintf in the handler): decimal and hex into a caller buffer
-char* fault_dec(char* p, unsigned long v) {
+// async-signal-safe formatting (no snprintf in the handler): decimal and hex into a caller
+// buffer, each clamped to `end` like fault_str (a long symbol name may fill the buffer)
+char* fault_dec(char* p, unsigned long v, const char* end) {
     char t[24];
     int n = 0;
     do { t[n++] = (char)('0' + v % 10); v /= 10; } while (v);
-    while (n) *p++ = t[--n];
+    while (n && p < end) *p++ = t[--n];
     return p;
 }
-char* fault_hex(char* p, unsigned long v) {
-    *p++ = '0';
-    *p++ = 'x';
+char* fault_hex(char* p, unsigned long v, const char* end) {
     char t[20];
     int n = 0;
     do { t[n++] = "0123456789abcdef"[v & 15]; v >>= 4; } while (v);
-    while (n) *p++ = t[--n];
+    t[n++] = 'x';
+    t[n++] = '0';
+    while (n && p < end) *p++ = t[--n];
     return p;
 }
 char* fault_str(char* p, const char* s, const char* end) {
@@ -296,19 +304,19 @@ void fault_handler(int sig, siginfo_t* si, void* ucv) {
     Dl_info di{};
     const bool named = pc && dladdr(pc, &di) && di.dli_fname;
     char* p = fault_str(buf, "[pcp fault] signal ", end);
-    p = fault_dec(p, (unsigned long)sig);
+    p = fault_dec(p, (unsigned long)sig, end);
     p = fault_str(p, " at address ", end);
-    p = fault_hex(p, (unsigned long)(si ? si->si_addr : nullptr));
+    p = fault_hex(p, (unsigned long)(si ? si->si_addr : nullptr), end);
     p = fault_str(p, ", pc ", end);
-    p = fault_hex(p, (unsigned long)pc);
+    p = fault_hex(p, (unsigned long)pc, end);
     p = fault_str(p, " in ", end);
     p = fault_str(p, named ? di.dli_fname : "?", end);
     p = fault_str(p, " (", end);
     p = fault_str(p, named && di.dli_sname ? di.dli_sname : "?", end);
     p = fault_str(p, "+", end);
-    p = fault_hex(p, named ? (unsigned long)((char*)pc - (char*)(di.dli_sname ? di.dli_saddr : di.dli_fbase)) : 0ul);
-    *p++ = ')';
-    *p++ = '\n';
+    p = fault_hex(p, named ? (unsigned long)((char*)pc - (char*)(di.dli_sname ? di.dli_saddr : di.dli_fbase)) : 0ul, end);
+    p = fault_str(p, ")", end);
+    *p++ = '\n';  // end leaves room for it
     (void)!write(2, buf, (size_t)(p - buf));
     void* frames[48];
     const int n = backtrace(frames, 48);

@@ -296,27 +296,6 @@ __global__ void k_cell_keys_rec(GridDesc g, const float* cxyz, size_t stride_f, 
     }
 }
 
-// (PCP_TSORT_IDX variant of the fp32 build) the cell key and the point's own index; the sorted
-// records are gathered once afterwards (k_gather_rec) instead of riding through every radix pass
-__global__ void k_cell_keys_idx(GridDesc g, const float* cxyz, size_t stride_f, int64_t n, uint32_t* key,
-                                uint32_t* idx) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int cx, cy, cz;
-        cell_of_point<float>(g, cxyz + stride_f * i, cx, cy, cz);
-        key[i] = (uint32_t)cell_id(g, cx, cy, cz);
-        idx[i] = (uint32_t)i;
-    }
-}
-__global__ void k_gather_rec(const float* cxyz, size_t stride_f, const int32_t* mapping, const uint32_t* idx,
-                             int64_t n, float4* rec) {
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n;
-         s += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t i = idx[s];
-        const float* p = cxyz + stride_f * i;
-        rec[s] = make_float4(p[0], p[1], p[2], __int_as_float(mapping ? mapping[i] : (int32_t)i));
-    }
-}
 
 // Radix-sort build: key = cell id (cstart index) of each compacted point, value = its
 // internal index.  A stable LSD sort then yields cell order with ties in input order
@@ -378,19 +357,10 @@ bool make_geometry(GridDesc& g, const double mn[3], const double mx[3], double h
     return true;
 }
 
-#ifndef PCP_TSORT_IDX_DEFAULT
-#define PCP_TSORT_IDX_DEFAULT 0
-#endif
-// fp32 build: sort (cell id, index) pairs and gather the records (PCP_TSORT_IDX=1, A/B) or carry
-// the 16-byte records through the radix passes (0)
-bool tsort_idx() {
-    const char* e = getenv("PCP_TSORT_IDX");
-    return e ? atoi(e) != 0 : PCP_TSORT_IDX_DEFAULT != 0;
-}
-
 template <typename T>
 int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const int32_t* indices,
-               double cell_size, int is_f64, pcp_index** out, bool force_sparse = false) {
+               double cell_size, int is_f64, pcp_index** out, bool force_sparse = false,
+               const GeomHook* on_geom = nullptr) {
     if (!ctx || !out || n_in < 0 || (n_in > 0 && !xyz)) return PCP_ERR_ARG;
     if (n_in >= (int64_t)1 << 31) return set_error(ctx, PCP_ERR_ARG, "index supports < 2^31 points");
     PCP_HIP(ctx, hipSetDevice(ctx->device));
@@ -514,6 +484,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         dfree(ctx, rank); dfree(ctx, skey); dfree(ctx, cxyz);
         return fail(rc);
     }
+    bool hooked = false;
     for (int attempt = 0; attempt < 3; attempt++) {
         GridDesc g{};
         while (!make_geometry(g, mn, mx, h, cap)) h *= 2.0;
@@ -548,6 +519,10 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             g.brick = ix->brick;
             ncells = (int64_t)nslots * 64;
         }
+        if (on_geom && *on_geom && !auto_h && !hooked) {  // the geometry is final: let the caller start
+            hooked = true;                                  // work that needs only it (overlaps the sort)
+            if ((rc = (*on_geom)(g))) break;
+        }
         if ((rc = dmalloc(ctx, &count, ncells + 1))) break;
         // ---- stable radix sort by cell id.  fp32: the payload is the point record itself, so
         // the sort output is the cell-ordered point array (no gather).  fp64: the payload is the
@@ -572,23 +547,6 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
                 if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
                     PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u,
                                                            bits, st));
-            } else if (tsort_idx()) {
-                // (key, index) pairs through the radix passes, then one gather of the records
-                const float* src = direct ? (const float*)xyz : (const float*)cxyz;
-                const size_t sf = direct ? stride / sizeof(float) : (size_t)3;
-                uint32_t *i0 = nullptr, *i1 = nullptr;
-                if (!(rc = dmalloc(ctx, &i0, n)) && !(rc = dmalloc(ctx, &i1, n))) {
-                    hipLaunchKernelGGL(k_cell_keys_idx, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, src, sf, n, skey, i0);
-                    PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, i0, i1, (size_t)n, 0u, bits, st));
-                    if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
-                        PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, key1, i0, i1, (size_t)n, 0u, bits, st));
-                    if (!rc)
-                        hipLaunchKernelGGL(k_gather_rec, dim3(grid_for(n, kB)), dim3(kB), 0, st, src, sf,
-                                           direct ? (const int32_t*)nullptr : (const int32_t*)ix->mapping,
-                                           (const uint32_t*)i1, n, (float4*)ix->pts);
-                }
-                dfree(ctx, i0);
-                dfree(ctx, i1);
             } else {
                 // no brick marks: the fp32 index serves ICP only, whose dense-grid searches never
                 // read brick occupancy (its brick table stays all-zero = "occupied")
@@ -664,6 +622,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     dfree(ctx, rank);
     dfree(ctx, skey);
     dfree(ctx, cxyz);
+    if (!rc && on_geom && *on_geom && !hooked) rc = (*on_geom)(ix->g);  // auto cell size: after the refinement
     if (rc) return fail(rc);
     PCP_HIP(ctx, hipGetLastError());
     PCP_HIP(ctx, hipStreamSynchronize(st));
@@ -672,6 +631,12 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
 }
 
 }  // namespace
+
+int index_build_f32_hooked(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size,
+                           pcp_index** out, const GeomHook& on_geom) {
+    if (stride == 0) stride = 3 * sizeof(float);
+    return build_impl<float>(ctx, xyz, stride, n, nullptr, cell_size, 0, out, false, &on_geom);
+}
 
 }  // namespace pcp
 
@@ -700,12 +665,6 @@ int pcp_index_destroy(pcp_index* ix) {
     pcp::dfree(ix->owner, ix->pos_of_j);
     pcp::dfree(ix->owner, ix->h16);
     pcp::dfree(ix->owner, ix->cell);
-    pcp::dfree(ix->owner, ix->h16_cnt_s);
-    pcp::dfree(ix->owner, ix->h16_inv);
-    pcp::dfree(ix->owner, ix->h16_rows);
-    pcp::dfree(ix->owner, ix->h16_planes);
-    pcp::dfree(ix->owner, ix->h16_ovf);
-    pcp::dfree(ix->owner, ix->h16_spill_of);
     pcp_ctx* owner = ix->owner;
     delete ix;
     pcp::ctx_release(owner);

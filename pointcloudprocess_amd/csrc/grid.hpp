@@ -6,9 +6,17 @@
 // Bricks of 4x4x4 cells; brick table -> slot; cell (slot, local) owns sorted points
 // [cstart[64*slot+local], cstart[64*slot+local+1]).
 #pragma once
+#include <functional>
+
 #include "common.hpp"
 
 namespace pcp {
+
+// the fp32 build with a callback once the grid geometry is final (before the cell sort is
+// enqueued on the context's stream): pcp_icp_create_with_target starts the query sort there
+using GeomHook = std::function<int(const GridDesc&)>;
+int index_build_f32_hooked(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size,
+                           pcp_index** out, const GeomHook& on_geom);
 
 template <typename T> struct Real;
 template <> struct Real<float> {

@@ -21,10 +21,6 @@
 #include "grid.hpp"
 #include "wave_acc.hpp"
 
-#ifndef PCP_OCT_GLIST  // lanes per query of the octant pass over the verify pass's search lists
-#define PCP_OCT_GLIST 0  // 0: by the list's density (octant_lanes)
-#endif
-
 namespace pcp {
 // a sorted query's coordinates: 12 bytes (one global_load_dwordx3 per lane)
 struct QXyz {
@@ -40,14 +36,11 @@ struct pcp_icp {
     int64_t nq_in = 0;            // queries passed to pcp_icp_create
     pcp::QXyz* q = nullptr;       // sorted queries, 12-byte xyz (the verify stream reads 12 B, not 16)
     int32_t* qidx = nullptr;      // their original indices (read only for caller-order outputs)
-    uint4* cand = nullptr;        // per sorted query: sorted-target positions of its kCache nearest targets
-                                  // at its last search (~0u = empty slot); the winner is always among them
-    float4* hot = nullptr;        // per sorted query (PCP_VER_HOT): 2 records {x,y,z,dlb word}, {x,y,z,0}:
-                                  // the two nearest of cand (the winner among them) with D folded
-                                  // down to the third's distance -- all the verify pass reads
-    uint32_t* dlb = nullptr;      // per sorted query: (float bits of D) & ~0xff | s, where s = the launch
-                                  // (mod 256) of its last search and D a lower bound (m) on the distance
-                                  // from the query, at that launch's pose, to every target NOT in cand
+    uint4* cand = nullptr;        // per sorted query: sorted-target positions of its 3 nearest targets at
+                                  // its last search (~0u = empty slot; the winner is always among them)
+                                  // and (float bits of D) & ~0xff | s, where s = the launch (mod 256) of
+                                  // that search and D a lower bound on the distance from the query, at
+                                  // that launch's pose, to every target NOT cached
     float* pose_hist = nullptr;   // 256 x 12 floats: the pose of launch t at slot t & 255
     int64_t launches = 0;         // correspondence launches so far (the first has nothing to verify)
     bool last_verified = false;   // the last launch ran the verify pass
@@ -67,23 +60,14 @@ struct pcp_icp {
     double* acc = nullptr;        // 24 (scratch for pcp_icp_run)
     int nb_fast = 0, nb_ring = 0;
     int nb_fast_l = 0;            // octant grid of the list launches (<= nb_fast)
-    int engine_tile = 0;          // dense grids: 1 = the LDS-tiled streaming search (env
-                                  // PCP_ICP_ENGINE=tile), 0 = the cached verify / octant / ring passes
-    int nb_tile = 0;
-    int32_t* bstart = nullptr;    // tile engine: first sorted query of each query brick (+ nq), nbk + 1
-    int64_t nbk = 0;              // query bricks
-    uint32_t* fb_base = nullptr;  // tile engine: per workgroup, its fallback segment's start              // tile engine: workgroups (grid-stride over the tiles)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr, ev_ver = nullptr;
     float* pose_dev = nullptr;    // 24 floats: this launch's pose (R row-major, t), then the previous one
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-launch timing events (device loop)
     size_t ntev = 0;              // pairs recorded since the last pcp_icp_kernel_ms
-    int dbg = 0;                  // PCP_ICP_ABLATE flags (profiling only)
+    int dbg = 0;                  // ablation flags (pcp_icp_set_options; profiling only: results are wrong)
     int oct_g_first = 1;          // lanes per query of the octant pass: first launch (all queries)
-    int oct_g_list = PCP_OCT_GLIST;  // ... and the verify pass's search lists (PCP_OCT_G=first,list)
-    int ring_g = 0;               // lanes per query of the fallback pass (env PCP_RING_LANES), 0 = by length
-    int ver_dense = 0;            // verify: whole-chunk search threshold (PCP_VER_DENSE, env PCP_VER_DENSE)
-    unsigned long long* dbgcnt = nullptr;  // kDbgCount: [candidates, rows, queries]
-    uint2* dbgfz = nullptr;       // kDbgCount: per 64-query chunk {slack bits, launch} (freeze model)
+    int oct_g_list = 0;           // ... and the verify pass's search lists (0: by the list's density)
+    int ring_g = 0;               // lanes per query of the fallback pass, 0 = by the list's length
     double last_ms = 0.0;
     int last_launches = 0;
     uint32_t last_fallback = 0;
@@ -100,18 +84,12 @@ constexpr int kIcpBlock = 256;
 #ifndef PCP_OCT_WAVES
 #define PCP_OCT_WAVES 6
 #endif
-#ifndef PCP_VER_XCD  // verify work split: 1 = XCD-blocked grid-stride, 0 = contiguous per wave
-#define PCP_VER_XCD 0
-#endif
 #ifndef PCP_VER_WAVES   // verify (per-lane accumulators: ~100 VGPRs)
 #define PCP_VER_WAVES 4
 #endif
 
 #ifndef PCP_RING_WAVES
 #define PCP_RING_WAVES 6
-#endif
-#ifndef PCP_VER_HOT  // verify reads per-query hot records (positions inline) instead of gathering
-#define PCP_VER_HOT 0
 #endif
 constexpr int kAcc = 24;
 
@@ -130,8 +108,6 @@ struct IcpArgs {
     float mc;           // cell-unit margin for pruning
     double* partials;
     uint4* cand;
-    float4* hot;
-    uint32_t* dlb;
     const float* pose_hist;
     uint32_t launch;    // this launch's index (mod 2^32)
     uint32_t ntp;       // target points (tp[ntp] is the far sentinel)
@@ -147,13 +123,10 @@ struct IcpArgs {
     int nb_fast;
     int64_t nseg;       // fallback segments (= waves of the octant kernel)
     int ring_all;       // ring kernel: process every query (sparse grid) instead of the list
-    int dbg;            // ablation flags (PCP_ICP_ABLATE, profiling builds of the bench only)
+    int dbg;            // ablation flags (pcp_icp_set_options; profiling only)
     int oct_g;          // octant pass lanes per query: 1, 2, 4, 8, or 0 = by the list's density
     int ring_g;         // fallback pass lanes per query: 1, 2, 4, 8, or 0 = PCP_RING_G / by length
-    int ver_dense;      // verify: a 64-query chunk with at least this many failures is searched whole (0: off)
     const float* pose;  // device poses (current, previous: 24 floats) overriding R/t, Rp/tq, or null
-    unsigned long long* dbgcnt;  // kDbgCount counters, or null
-    uint2* dbgfz;       // kDbgCount: chunk freeze model state
 };
 
 // sorted query i as {x, y, z, 0}
@@ -178,9 +151,10 @@ __device__ __forceinline__ void load_prev_pose(IcpArgs& a) {
     for (int k = 0; k < 3; k++) a.tq[k] = a.pose[21 + k];
 }
 
-// Ablation switches for profiling (env PCP_ICP_ABLATE); results are wrong when any is set.
-constexpr int kDbgNoScan = 1, kDbgNoAccum = 4, kDbgNoFallback = 8, kDbgCount = 16, kDbgNoVerify = 64,
-              kDbgTileOctOnly = 128, kDbgTileNone = 256;
+// Ablation switches for profiling (pcp_icp_set_options, PCP_ICP_ABLATE_*); results are wrong
+// when any is set.
+constexpr int kDbgNoScan = PCP_ICP_ABLATE_NO_SCAN, kDbgNoAccum = PCP_ICP_ABLATE_NO_ACCUM,
+              kDbgNoFallback = PCP_ICP_ABLATE_NO_FALLBACK, kDbgNoVerify = PCP_ICP_ABLATE_NO_VERIFY;
 
 __device__ __forceinline__ void xform(const IcpArgs& a, const float4 q, float& x, float& y, float& z) {
     // q' = R q + t: x' = fmaf(R02,z,fmaf(R01,y,fmaf(R00,x,t0)))
@@ -227,7 +201,6 @@ struct Best {
     int bj;
     uint32_t bk;
     float px, py, pz;  // filled by fetch() once the scan is over (or tracked, PCP_TRACK_BEST)
-    uint32_t dbg_len = 0;  // kDbgCount: candidates scanned
     __device__ __forceinline__ void consider(float qx, float qy, float qz, const float4 p, uint32_t k) {
         const float d2 = icp_d2(qx, qy, qz, p);
         const int id = __float_as_int(p.w);
@@ -262,7 +235,6 @@ struct Best {
                                               float qx, float qy, float qz) {
         static_assert(NR == 3 || NR == 4, "3 or 4 rows");
         const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = NR == 4 ? c3 + rn[NR - 1] : c3;
-        dbg_len = L;
         const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[NR - 1] - c3;
         const uint32_t c3e = NR == 4 ? c3 : 0xffffffffu;  // 3 rows: never past the third
         auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3e, o0, o1, o2, o3); };
@@ -313,7 +285,6 @@ struct Best {
         }
         static_assert(NR == 3 || NR == 4, "3 or 4 rows");
         const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = NR == 4 ? c3 + rn[NR - 1] : c3;
-        dbg_len = L;
         const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[NR - 1] - c3;
         const uint32_t c3e = NR == 4 ? c3 : 0xffffffffu;
         auto addr = [=](uint32_t v) { return cat_addr(v, c1, c2, c3e, o0, o1, o2, o3); };
@@ -535,12 +506,8 @@ __device__ __forceinline__ void write_wave_partials(double (*s_acc)[kAcc], doubl
 // kFlush chunks (and at the end) the wave reduces them with DPP adds and lane 0 un-centres the
 // totals in fp64 into the wave's LDS accumulators.  A stretch is at most kFlush * 64
 // consecutive sorted queries (a few metres), so the centred fp32 products stay small.
-#ifndef PCP_KFLUSH  // chunks per accumulator stretch (XCD split: a wave's chunks are far apart)
-#if PCP_VER_XCD
-#define PCP_KFLUSH 8
-#else
+#ifndef PCP_KFLUSH  // chunks per accumulator stretch
 #define PCP_KFLUSH 32
-#endif
 #endif
 constexpr int kFlush = PCP_KFLUSH;
 #ifndef PCP_FLUSH_INLINE  // 1: inline the stretch flush (no call frame spilled to scratch)
@@ -603,19 +570,15 @@ struct LaneAcc {
 
 // ---- candidate cache (a Verlet-style neighbour list per query)
 // The search that last settled query i left cand[i] = the positions of its kCache nearest
-// targets (or fewer) and D = dlb[i], a lower bound on the distance from the query, at the
+// targets (or fewer) and D = the dlb word cand[i].w, a lower bound on the distance from the query, at the
 // previous launch's pose q_s, to every target point NOT in cand[i].  With q_t the query at the
 // current pose and Delta = |q_t - q_s|, every uncached point p has |q_t - p| >= D - Delta
 // (triangle inequality).  So if the nearest cached point is closer than D - Delta (with
 // relative margins far above the fp32 rounding of d2), it is the exact 1-NN under the
 // contract -- the same (d2, index) winner an exhaustive search returns, cached ties included
 // -- and the query is settled without a search; the bound moves to D - Delta.
-#ifndef PCP_CACHE3
-#define PCP_CACHE3 1
-#endif
-// kCache = 3: cand = {3 positions, dlb word} (one 16-byte record per query); 4: cand = 4 positions
-// and a separate dlb array
-constexpr int kCache = PCP_CACHE3 ? 3 : 4;
+// kCache = 3: cand = {3 positions, dlb word} (one 16-byte record per query)
+constexpr int kCache = 3;
 
 // the cached candidates' winner under the current pose, by (d2, target index)
 struct CacheBest {
@@ -625,7 +588,7 @@ struct CacheBest {
     float4 P = make_float4(0.f, 0.f, 0.f, 0.f);
 };
 __device__ __forceinline__ CacheBest cache_best(const float4* tp, const uint4 cd, float qx, float qy, float qz) {
-    const uint32_t c[4] = {cd.x, cd.y, cd.z, cd.w};  // with kCache = 3, .w is the dlb word
+    const uint32_t c[3] = {cd.x, cd.y, cd.z};  // .w is the dlb word
     float4 p[kCache];
 #pragma unroll
     for (int s = 0; s < kCache; s++) p[s] = c[s] != ~0u ? tp[c[s]] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -677,120 +640,63 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;
     const int64_t nch = (a.nq + 63) / 64;
-#if PCP_VER_XCD
-    // XCD-blocked grid-stride: the waves of one XCD sweep its eighth of the queries together,
-    // so neighbouring chunks (which share cached targets) run on one L2 at the same time
-    const XcdSplit xs = xcd_split(nch, kW);
-    const int64_t cstart_ = xs.c0 + xs.w, cstep = xs.nw;
-    const int64_t nsteps = cstart_ < xs.c1 ? (xs.c1 - cstart_ + cstep - 1) / cstep : 0;
-#else
     // contiguous ranges: wave w owns chunks [w*nch/nwaves, (w+1)*nch/nwaves)
     const int64_t nwaves = (int64_t)gridDim.x * kW;
-    const int64_t cstart_ = gw * nch / nwaves, cstep = 1;
+    const int64_t cstart_ = gw * nch / nwaves;
     const int64_t nsteps = (gw + 1) * nch / nwaves - cstart_;
-#endif
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
     __syncthreads();
     uint32_t svn = 0;
     LaneAcc acc;
     acc.zero();
     const float r2m = a.r2 * 1.0003f;
-#if PCP_VER_HOT
-    // software pipeline: the query and its two hot cache records two chunks ahead (plain
-    // coalesced streams, no gathers)
-    const float4 far4 = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
-    auto raw = [&](int64_t k, float4& q, float4& h0, float4& h1) {
-        const int64_t i = (cstart_ + k * cstep) * 64 + lane;
-        if (k < nsteps && i < a.nq) {
-            q = ldq(a, i);
-            h0 = a.hot[2 * i];
-            h1 = a.hot[2 * i + 1];
-        } else {
-            q = make_float4(0.f, 0.f, 0.f, 0.f);
-            h0 = far4;
-            h1 = far4;
-        }
-    };
-    float4 q1, q2, a1, a2, b1, b2;
-    raw(0, q1, a1, b1);
-    raw(1, q2, a2, b2);
-#else
     // software pipeline: the query, cache and bound words two chunks ahead, the cached points'
     // gathers one chunk ahead (this chunk's were issued during the previous one)
     const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
-    auto raw = [&](int64_t k, float4& q, uint4& cd, uint32_t& D) {
-        const int64_t i = (cstart_ + k * cstep) * 64 + lane;
+    auto raw = [&](int64_t k, float4& q, uint4& cd) {
+        const int64_t i = (cstart_ + k) * 64 + lane;
         if (k < nsteps && i < a.nq) {
             q = ldq(a, i);
             cd = a.cand[i];
-            D = PCP_CACHE3 ? cd.w : a.dlb[i];
         } else {
             q = make_float4(0.f, 0.f, 0.f, 0.f);
             cd = none;
-            D = 0u;
+            cd.w = 0u;
         }
     };
-    auto gather = [&](const uint4 cd, float4& p0, float4& p1, float4& p2, float4& p3) {
+    auto gather = [&](const uint4 cd, float4& p0, float4& p1, float4& p2) {
         // an empty slot reads the far sentinel tp[ntp]: d2 = inf
         p0 = ld16(a.tp, min(cd.x, a.ntp));
         p1 = ld16(a.tp, min(cd.y, a.ntp));
         p2 = ld16(a.tp, min(cd.z, a.ntp));
-        p3 = PCP_CACHE3 ? make_float4(INFINITY, INFINITY, INFINITY, 0.f) : ld16(a.tp, min(cd.w, a.ntp));
     };
     float4 q1, q2;
     uint4 c1_, c2_;
-    uint32_t D1, D2;
-    float4 g0, g1, g2, g3;
-    raw(0, q1, c1_, D1);
-    raw(1, q2, c2_, D2);
-    gather(c1_, g0, g1, g2, g3);
-#endif
+    float4 g0, g1, g2;
+    raw(0, q1, c1_);
+    raw(1, q2, c2_);
+    gather(c1_, g0, g1, g2);
     for (int64_t k0 = 0; k0 < nsteps; k0 += kFlush) {  // stretches of kFlush chunks
         const int64_t k1 = min(k0 + (int64_t)kFlush, nsteps);
         // centre: the stretch's first query under the current pose (wave-uniform)
         float ccx, ccy, ccz;
-        xform(a, ldq(a, (cstart_ + k0 * cstep) * 64), ccx, ccy, ccz);
+        xform(a, ldq(a, (cstart_ + k0) * 64), ccx, ccy, ccz);
         ccx = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccx)));
         ccy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccy)));
         ccz = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ccz)));
         for (int64_t k = k0; k < k1; k++) {
-            const int64_t i = (cstart_ + k * cstep) * 64 + lane;
+            const int64_t i = (cstart_ + k) * 64 + lane;
             const bool valid = i < a.nq;
             const float4 qq = q1;
-#if PCP_VER_HOT
-            const float4 p0 = a1, p1 = b1, p2 = far4;
-            const uint32_t Dw = valid ? __float_as_uint(a1.w) : 0u;
-            q1 = q2;
-            a1 = a2;
-            b1 = b2;
-            raw(k + 2, q2, a2, b2);
-#else
-            const uint32_t Dw = valid ? D1 : 0u;
-            const float4 p0 = g0, p1 = g1, p2 = g2, p3 = g3;
+            const uint32_t Dw = valid ? c1_.w : 0u;
+            const float4 p0 = g0, p1 = g1, p2 = g2;
             // issue chunk c+1's gathers and chunk c+2's words before using chunk c's
-            gather(c2_, g0, g1, g2, g3);
+            gather(c2_, g0, g1, g2);
             q1 = q2;
             c1_ = c2_;
-            D1 = D2;
-            raw(k + 2, q2, c2_, D2);
-#endif
+            raw(k + 2, q2, c2_);
             float qx, qy, qz;
             xform(a, qq, qx, qy, qz);
-#if PCP_VER_HOT
-            // winner of the two hot points by d2; an exact tie within rmax (the index decides,
-            // which the hot records do not carry) is searched
-            float m = icp_d2(qx, qy, qz, p0), px = p0.x, py = p0.y, pz = p0.z;
-            bool tie;
-            {
-                const float e = icp_d2(qx, qy, qz, p1);
-                tie = e == m && e <= a.r2;
-                const bool t = e < m;
-                m = t ? e : m;
-                px = t ? p1.x : px;
-                py = t ? p1.y : py;
-                pz = t ? p1.z : pz;
-            }
-#else
             // winner among the cached points by (d2, target index); an empty slot never wins
             float m = INFINITY, px = 0.f, py = 0.f, pz = 0.f;
             int mj = 0x7fffffff;
@@ -807,9 +713,6 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             take(p0);
             take(p1);
             take(p2);
-            if (!PCP_CACHE3) take(p3);
-            const bool tie = false;
-#endif
             // the query at the pose of its last search
             const uint32_t sl = Dw & 0xffu;
             const float4 A = s_pose[sl][0], B = s_pose[sl][1], C = s_pose[sl][2];
@@ -820,114 +723,24 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             const float lb = __uint_as_float(Dw & ~0xffu) * 0.99998f - delta;  // every uncached point is >= lb
             // the nearest cached point is the exact 1-NN (it beats lb), or nothing is within rmax
             const float thr = fminf(m * 1.0003f, r2m);
-            bool ok = valid && !tie && ((a.launch - Dw) & 0xffu) < kMaxAge && lb > 0.f && thr + 1e-12f < lb * lb;
+            bool ok = valid && ((a.launch - Dw) & 0xffu) < kMaxAge && lb > 0.f && thr + 1e-12f < lb * lb;
             ok = ok && !(a.dbg & kDbgNoVerify);
-            // a chunk where many queries fail is searched whole: the search list then holds runs
-            // of 64 neighbouring queries, which the search pass scans at its dense cost (the
-            // lanes share candidate lines), and the chunk's caches are all refreshed
-            if (a.ver_dense && (int)__popcll(__ballot(valid && !ok)) >= a.ver_dense) ok = false;
             const bool srch = valid && !ok;
             const uint64_t msk = __ballot(srch);
             if (srch) {
-#if PCP_VER_XCD
-                // one 64-entry segment per chunk: the compacted list keeps query order whatever
-                // the work split
-                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-                a.sv[(cstart_ + k * cstep) * 64 + pos] = (int32_t)i;
-#else
                 const uint32_t pos = svn + __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32),
                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
                 a.sv[gw * a.sv_seg + pos] = (int32_t)i;
-#endif
             }
-#if PCP_VER_XCD
-            if (lane == 0) {
-                const int64_t ch = cstart_ + k * cstep;
-                a.sv_count[ch] = (uint32_t)__popcll(msk);
-                a.sv_off[ch] = (uint32_t)__popcll(msk);  // scanned in place into the segment offsets
-                if (ch == 0) a.sv_off[a.nseg_v] = 0u;
-            }
-#endif
             svn += (uint32_t)__popcll(msk);
-            if ((a.dbg & kDbgCount) && valid) {
-                // why queries are searched: reason and where the winner sits relative to D
-                const float Dv = __uint_as_float(Dw & ~0xffu);
-                if (ok) {
-                    atomicAdd(a.dbgcnt + 20, 1ull);
-#if !PCP_VER_HOT
-                    // would a one-gather first tier have settled it: the first cached point
-                    // beats the others' distances at the search pose less the motion
-                    const float qsx = qx - ex, qsy = qy - ey, qsz = qz - ez;
-                    const float s1 = sqrtf(icp_d2(qsx, qsy, qsz, p1)), s2 = sqrtf(icp_d2(qsx, qsy, qsz, p2));
-                    const float lb1 = fminf(fminf(s1, s2), __uint_as_float(Dw & ~0xffu)) * 0.99998f - delta;
-                    const float e0 = icp_d2(qx, qy, qz, p0);
-                    if (lb1 > 0.f && fminf(e0 * 1.0003f, r2m) + 1e-12f < lb1 * lb1) atomicAdd(a.dbgcnt + 31, 1ull);
-#endif
-                } else if (((a.launch - Dw) & 0xffu) >= kMaxAge) {
-                    atomicAdd(a.dbgcnt + 21, 1ull);
-                } else if (Dv == 0.f) {
-                    atomicAdd(a.dbgcnt + 22, 1ull);
-                } else {
-                    const float r = sqrtf(m) / Dv;
-                    atomicAdd(a.dbgcnt + (r < 0.5f ? 23 : r < 0.75f ? 24 : r < 1.f ? 25 : 26), 1ull);
-                    const float rd = delta / Dv;
-                    atomicAdd(a.dbgcnt + (rd < 0.1f ? 27 : rd < 0.25f ? 28 : rd < 0.5f ? 29 : 30), 1ull);
-                }
-            }
-            if (a.dbg & kDbgCount) {
-                // chunk freeze model (counts only): a chunk frozen at launch s with slack tau (the
-                // min over members of the gap that keeps the winner) stays valid while every
-                // member moved less than tau since s
-                const int64_t ch = cstart_ + k * cstep;
-                const uint2 fz = a.dbgfz[ch];
-                const float tau = __uint_as_float(fz.x);
-                const uint32_t fsl = fz.y & 0xffu;
-                const float4 FA = s_pose[fsl][0], FB = s_pose[fsl][1], FC = s_pose[fsl][2];
-                const float fx_ = qx - __fmaf_rn(FA.z, qq.z, __fmaf_rn(FA.y, qq.y, __fmaf_rn(FA.x, qq.x, FC.y)));
-                const float fy_ = qy - __fmaf_rn(FB.y, qq.z, __fmaf_rn(FB.x, qq.y, __fmaf_rn(FA.w, qq.x, FC.z)));
-                const float fz_ = qz - __fmaf_rn(FC.x, qq.z, __fmaf_rn(FB.w, qq.y, __fmaf_rn(FB.z, qq.x, FC.w)));
-                float dq = valid ? sqrtf(fz_ * fz_ + fy_ * fy_ + fx_ * fx_) : 0.f;
-                for (int o = 32; o > 0; o >>= 1) dq = fmaxf(dq, __shfl_xor(dq, o, 64));
-                const bool skip = fz.y != 0u && tau > 0.f && ((a.launch - fz.y) & 0xffu) < kMaxAge && dq < tau;
-                const uint32_t nsrch = (uint32_t)__popcll(msk);
-                if (skip) {
-                    if (lane == 0) {
-                        atomicAdd(a.dbgcnt + 16, 1ull);
-                        atomicAdd(a.dbgcnt + 17, (unsigned long long)nsrch);  // must stay 0
-                    }
-                } else {
-                    float sl = INFINITY;
-                    if (valid) {
-                        if (!ok) {
-                            sl = 0.f;
-                        } else {
-                            float e0 = icp_d2(qx, qy, qz, p0), e1 = icp_d2(qx, qy, qz, p1), e2 = icp_d2(qx, qy, qz, p2);
-                            const float lo = fminf(e0, fminf(e1, e2));
-                            const float m2 = e0 == lo ? fminf(e1, e2) : (e1 == lo ? fminf(e0, e2) : fminf(e0, e1));
-                            const float d0 = sqrtf(m), d1 = sqrtf(m2);
-                            sl = fminf(0.5f * (fminf(lb, d1) - d0), fabsf(d0 - sqrtf(a.r2)));
-                            sl = fmaxf(sl * 0.999f - 1e-6f, 0.f);
-                        }
-                    }
-                    for (int o = 32; o > 0; o >>= 1) sl = fminf(sl, __shfl_xor(sl, o, 64));
-                    if (lane == 0) {
-                        a.dbgfz[ch] = make_uint2(__float_as_uint(sl), a.launch | 0x80000000u);
-                        if (sl > 0.f) atomicAdd(a.dbgcnt + 19, 1ull);
-                    }
-                }
-                if (lane == 0) atomicAdd(a.dbgcnt + 18, 1ull);
-            }
             if (ok && m <= a.r2 && !(a.dbg & kDbgNoAccum)) acc.add(qx, qy, qz, px, py, pz, m, ccx, ccy, ccz);
         }
         acc.flush(s_acc[wid], lane, ccx, ccy, ccz);
     }
     if (lane == 0) {
-#if !PCP_VER_XCD
         a.sv_count[gw] = svn;
         a.sv_off[gw] = svn;  // scanned in place into the segment offsets
         if (gw == 0) a.sv_off[a.nseg_v] = 0u;
-#endif
     }
     write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
 }
@@ -1094,31 +907,13 @@ struct Top3P {
 // wave-uniform trip count; a chunk with a list longer than 256 candidates (the key's low byte)
 // uses the compare-swap form (Top3).  Both end in the same OctResult: the exact (d2, index)
 // winner among the 3 kept, its coordinates, the 3 cached positions and the first-uncached bound.
-static_assert(PCP_CACHE3, "the search pass keeps a 3-point cache");
-
 struct OctResult {
     float d0 = INFINITY;       // exact d2 of the winner among the kept points
     uint32_t win = ~0u;        // its sorted position (~0u: nothing scanned)
     float wx = 0.f, wy = 0.f, wz = 0.f;
     uint32_t c0 = ~0u, c1 = ~0u, c2 = ~0u;  // the cache: positions of the 3 kept points
     float dnext = INFINITY;    // lower bound on the d2 of every scanned point not kept
-    float4 h0 = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h1 = h0;  // the hot pair: the kept points less the last by (d2, index)
-    float edrop = INFINITY;    // exact d2 of the dropped (third) kept point
 };
-
-// the hot pair of the 3 kept points: drop the largest by (d2, index), so the winner stays
-__device__ __forceinline__ void hot_pair(OctResult& o, const float4 p0, const float4 p1, const float4 p2, float qx,
-                                         float qy, float qz) {
-    const float e0 = icp_d2(qx, qy, qz, p0), e1 = icp_d2(qx, qy, qz, p1), e2 = icp_d2(qx, qy, qz, p2);
-    const int i0 = __float_as_int(p0.w), i1 = __float_as_int(p1.w), i2 = __float_as_int(p2.w);
-    const bool d1 = e1 > e0 || (e1 == e0 && i1 > i0);  // p1 above p0
-    const float em = d1 ? e1 : e0;
-    const int im = d1 ? i1 : i0;
-    const bool d2 = e2 > em || (e2 == em && i2 > im);  // p2 is the largest
-    o.edrop = d2 ? e2 : em;
-    o.h0 = d2 || d1 ? p0 : p1;
-    o.h1 = d2 ? p1 : p2;
-}
 
 __device__ __forceinline__ void take_exact(OctResult& o, const float4 p, uint32_t pos, float qx, float qy, float qz,
                                            int& wj) {
@@ -1151,7 +946,6 @@ __device__ __forceinline__ OctResult octant_packed(const IcpArgs& a, const uint3
     take_exact(o, p0, o.c0, qx, qy, qz, wj);
     take_exact(o, p1, o.c1, qx, qy, qz, wj);
     take_exact(o, p2, o.c2, qx, qy, qz, wj);
-    if (PCP_VER_HOT) hot_pair(o, p0, p1, p2, qx, qy, qz);
     o.dnext = k.t3 == kKeyMax ? INFINITY : __uint_as_float(k.t3 & ~0xffu);
     return o;
 }
@@ -1172,7 +966,6 @@ __device__ __noinline__ OctResult octant_exact(const IcpArgs& a, uint32_t rs0, u
     take_exact(o, p0, o.c0, qx, qy, qz, wj);
     take_exact(o, p1, o.c1, qx, qy, qz, wj);
     take_exact(o, p2, o.c2, qx, qy, qz, wj);
-    if (PCP_VER_HOT) hot_pair(o, p0, p1, p2, qx, qy, qz);
     o.dnext = b.d3;
     return o;
 }
@@ -1249,19 +1042,6 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
             else
                 o = octant_exact(a, rs[0], rs[1], rs[2], rs[3], rn[0], rn[1], rn[2], rn[3], qx, qy, qz);
         }
-        if ((a.dbg & kDbgCount) && lead) {
-            atomicAdd(a.dbgcnt, (unsigned long long)len);
-            atomicAdd(a.dbgcnt + 2, 1ull);
-            if (Lw > kMaxOctList) atomicAdd(a.dbgcnt + 3, 1ull);
-            // per chunk: the wave's longest list (what sets the chunk's time) and its histogram
-            if (lane == 0) {
-                atomicAdd(a.dbgcnt + 1, (unsigned long long)Lw);
-                atomicAdd(a.dbgcnt + 4, 1ull);
-                int bkt = 0;
-                while (bkt < 7 && Lw >= (32u << bkt)) bkt++;
-                atomicAdd(a.dbgcnt + 8 + bkt, 1ull);
-            }
-        }
         bool settled = false, found = false;
         if (valid) {
             // this query's certified radius (cells): its distance to the nearest face of the
@@ -1280,15 +1060,6 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
             const float D = outside ? dout * 0.9999f
                                     : (settled ? fminf(sqrtf(o.dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : o.dnext);
             if (lead) a.cand[i] = make_uint4(o.c0, o.c1, o.c2, pack_dlb(D, a.launch));
-#if PCP_VER_HOT
-            // the verify pass's records: D folded down to the dropped point's distance (0 when
-            // unsettled: the fallback pass rewrites them)
-            if (lead) {
-                const float Dh = settled ? fminf(D, sqrtf(o.edrop) * 0.9999f) : 0.f;
-                a.hot[2 * i] = make_float4(o.h0.x, o.h0.y, o.h0.z, __uint_as_float(pack_dlb(Dh, a.launch)));
-                a.hot[2 * i + 1] = make_float4(o.h1.x, o.h1.y, o.h1.z, 0.f);
-            }
-#endif
         }
         // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
         const bool fb = valid && lead && !settled;
@@ -1308,490 +1079,6 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
         a.fb_off[gw] = fbn;  // scanned in place into the segment offsets
         if (gw == 0) a.fb_off[a.nseg] = 0u;
     }
-}
-
-// ---- LDS-tiled streaming search (dense grid; opt-in PCP_ICP_ENGINE=tile, measured slower than
-// the cached engine: DESIGN.md §5.1)
-// One pass over the sorted queries per launch, no per-query state.  The queries are sorted
-// once by 8x8x8-cell brick of the target grid (pcp_icp_create); a workgroup takes whole query
-// bricks, transforms their queries, and stages in LDS every target of the box of cells
-// [min c - 1, max c + 1] around the brick's query cells c: per (y, z) row of the box one
-// contiguous range of the dense table, plus a table of the rows' cell starts.  Each query then
-// runs, entirely in LDS:
-//   1. the 2x2x2 octant block (the four x-rows [floor(f - 1/2), +1]) keeping its 3 nearest on
-//      packed keys (Top3 as the octant pass), settled when the exact winner among them is
-//      within the block's certified radius (>= 1/2 cell) and beats the 4th key;
-//   2. otherwise the 3x3x3 cells around it (1-NN by (d2, index), certified within >= 1 cell);
-//   3. otherwise the global fallback list (k_icp_ring's exact box search).
-// Both stages read the same float4 records as a global search, so d2 and the winner are
-// bit-identical to the contract.  A brick whose box exceeds the LDS capacity is staged per
-// 256-query round; a round still too large sends its queries to the fallback list.
-// Accumulation as the octant pass (fp32 per 64-query chunk, centred, un-centred in fp64).
-constexpr int kTilePts = 3584;    // LDS points (56 KB; the last slot holds the far sentinel)
-constexpr int kTileTab = 3072;    // LDS cell-start table entries
-constexpr int kTileRows = 384;    // box rows (y, z)
-constexpr int kTileW = kIcpBlock / 64;
-constexpr int kStageU = 4;        // staging: global loads in flight per thread
-
-struct TileShared {
-    float4 pts[kTilePts];
-    uint32_t tab[kTileTab];        // local start of cell x0 + j of row r: tab[r * (nx + 1) + j]
-    uint32_t rgs[kTileRows];       // per row: global sorted position of its first staged point
-    uint32_t rls[kTileRows + 1];   // per row: local start (exclusive prefix of the row lengths)
-    int box[8];                    // x0, x1, y0, y1, z0, z1, ok, npts
-    int red[kTileW][6];
-    uint32_t fbw[2][kTileW];       // per round (parity): each wave's fallback count
-    double acc[kTileW][kAcc];
-};
-
-// position in LDS of candidate v of four concatenated LDS row ranges (rows past the list: the
-// far sentinel `sent`)
-__device__ __forceinline__ uint32_t tile_addr(uint32_t v, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t L,
-                                              uint32_t o0, uint32_t o1, uint32_t o2, uint32_t o3, uint32_t sent) {
-    return cat_addr_l(v, c1, c2, c3, L, o0, o1, o2, o3, sent);
-}
-
-// Stage the box of cells around the queries of one (sub)tile.  Every thread passes the cell
-// coordinates of its queries (in-grid ones; others pass inq = false).  Returns false (uniform)
-// when the box exceeds the LDS capacity.
-__device__ __forceinline__ bool tile_stage(const IcpArgs& a, TileShared& S, const int (&cmin)[3], const int (&cmax)[3]) {
-    const GridDesc& g = a.g;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    // block-wide min / max of the query cells
-    int v[6] = {cmin[0], cmin[1], cmin[2], -cmax[0], -cmax[1], -cmax[2]};
-#pragma unroll
-    for (int k = 0; k < 6; k++) v[k] = wave_min_i(v[k]);
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < 6; k++) S.red[wid][k] = v[k];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int m[6];
-        for (int k = 0; k < 6; k++) {
-            m[k] = S.red[0][k];
-            for (int w = 1; w < kTileW; w++) m[k] = min(m[k], S.red[w][k]);
-        }
-        const int x0 = max(m[0] - 1, 0), y0 = max(m[1] - 1, 0), z0 = max(m[2] - 1, 0);
-        const int x1 = min(-m[3] + 1, g.n[0] - 1), y1 = min(-m[4] + 1, g.n[1] - 1), z1 = min(-m[5] + 1, g.n[2] - 1);
-        const bool any = m[0] <= -m[3];
-        const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
-        const bool fits = any && (int64_t)ny * nz <= kTileRows && (int64_t)ny * nz * (nx + 1) <= kTileTab;
-        S.box[0] = x0; S.box[1] = x1; S.box[2] = y0; S.box[3] = y1; S.box[4] = z0; S.box[5] = z1;
-        S.box[6] = fits ? 1 : 0;
-    }
-    __syncthreads();
-    if (!S.box[6]) return false;
-    const int x0 = S.box[0], x1 = S.box[1], y0 = S.box[2], y1 = S.box[3], z0 = S.box[4], z1 = S.box[5];
-    const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nrows = ny * (z1 - z0 + 1);
-    // row ranges: [cstart(x0), cstart(x1 + 1)) (x1 + 1 == n0 reads the next row's start = this row's end)
-    for (int r = threadIdx.x; r < nrows; r += blockDim.x) {
-        const int y = y0 + r % ny, z = z0 + r / ny;
-        const uint32_t s = g.cstart[dense_id(g, x0, y, z)], e = g.cstart[dense_id(g, x1, y, z) + 1];
-        S.rgs[r] = s;
-        S.rls[r + 1] = e - s;  // lengths, scanned below
-    }
-    __syncthreads();
-    if (wid == 0) {  // exclusive scan of the row lengths (one wave, 64 rows per step)
-        uint32_t carry = 0;
-        for (int r0 = 0; r0 < nrows; r0 += 64) {
-            const int r = r0 + lane;
-            uint32_t x = r < nrows ? S.rls[r + 1] : 0u;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-                if (lane >= o) x += y;
-            }
-            if (r < nrows) S.rls[r + 1] = carry + x;
-            carry += (uint32_t)__shfl((int)x, 63, 64);
-        }
-        if (lane == 0) {
-            S.rls[0] = 0;
-            S.box[7] = (int)carry;
-            S.box[6] = carry + 1 <= (uint32_t)kTilePts ? 1 : 0;
-        }
-    }
-    __syncthreads();
-    if (!S.box[6]) return false;
-    const int npts = S.box[7];
-    // the cell-start table (local positions) and the points: flat over the entries, kStageU
-    // independent global loads in flight per thread
-    constexpr int U = kStageU;
-    const int ne = nrows * (nx + 1);
-    for (int e0 = threadIdx.x; e0 < ne; e0 += U * kIcpBlock) {
-        uint32_t v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int e = e0 + u * kIcpBlock;
-            if (e < ne) {
-                const int r = e / (nx + 1), j = e - r * (nx + 1);
-                v[u] = g.cstart[dense_id(g, x0, y0 + r % ny, z0 + r / ny) + j];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int e = e0 + u * kIcpBlock;
-            if (e < ne) {
-                const int r = e / (nx + 1);
-                S.tab[e] = S.rls[r] + (v[u] - S.rgs[r]);
-            }
-        }
-    }
-    for (int e0 = threadIdx.x; e0 < npts; e0 += U * kIcpBlock) {
-        float4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int e = e0 + u * kIcpBlock;
-            if (e < npts) {
-                // the row holding local position e: the last r with rls[r] <= e
-                int lo = 0, hi = nrows - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (S.rls[mid] <= (uint32_t)e) lo = mid; else hi = mid - 1;
-                }
-                v[u] = ld16(a.tp, S.rgs[lo] + ((uint32_t)e - S.rls[lo]));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int e = e0 + u * kIcpBlock;
-            if (e < npts) S.pts[e] = v[u];
-        }
-    }
-    if (threadIdx.x == 0) {
-        S.pts[npts] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(0x7fffffff));
-        if (a.dbg & kDbgCount) {
-            atomicAdd(a.dbgcnt + 10, (unsigned long long)npts);
-            atomicAdd(a.dbgcnt + 11, 1ull);
-            atomicAdd(a.dbgcnt + 14, (unsigned long long)nrows);
-        }
-    }
-    __syncthreads();
-    return true;
-}
-
-// one query against the staged box: octant, then the 3x3x3 cells; returns settled (else it goes
-// to the fallback list) and the winner (found: d2, coordinates, global sorted position)
-struct TileRes {
-    bool settled = false, found = false;
-    float d2 = INFINITY, px = 0.f, py = 0.f, pz = 0.f;
-    uint32_t gpos = ~0u;
-    int stage = 0;  // settled by: 1 the octant, 2 the 3x3x3 cells
-};
-// Every lane of the wave must call it (the octant's trip count is a wave reduction); a lane
-// with no query (active = false) scans nothing and returns unsettled.
-__device__ __forceinline__ TileRes tile_query(const IcpArgs& a, const TileShared& S, bool active, float qx, float qy,
-                                              float qz, float fx, float fy, float fz) {
-    const GridDesc& g = a.g;
-    const int x0 = S.box[0], y0 = S.box[2], z0 = S.box[4];
-    const int nx = S.box[1] - x0 + 1, ny = S.box[3] - y0 + 1;
-    const int nxe = nx + 1;
-    const uint32_t sent = (uint32_t)S.box[7];
-    auto row_of = [&](int y, int z) { return (z - z0) * ny + (y - y0); };
-    TileRes res;
-    // ---- 1. octant (2x2x2 block at floor(f - 1/2))
-    const int bx = (int)floorf(fx - a.rho), by = (int)floorf(fy - a.rho), bz = (int)floorf(fz - a.rho);
-    const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
-    uint32_t rs[4], rn[4], rd[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int y = by + (r & 1), z = bz + (r >> 1);
-        const bool in = active && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
-        const int R = in ? row_of(y, z) : 0;
-        const uint32_t s = in ? S.tab[R * nxe + (xa - x0)] : 0u, e = in ? S.tab[R * nxe + (xb + 1 - x0)] : 0u;
-        rs[r] = s;
-        rn[r] = e - s;
-        rd[r] = in ? S.rgs[R] - S.rls[R] : 0u;  // local -> global sorted position
-    }
-    const uint32_t c1 = rn[0], c2 = c1 + rn[1], c3 = c2 + rn[2], L = c3 + rn[3];
-    const uint32_t o0 = rs[0], o1 = rs[1] - c1, o2 = rs[2] - c2, o3 = rs[3] - c3;
-    const uint32_t Lw = (uint32_t)__builtin_amdgcn_readfirstlane(wave_max_u((int)L));
-    if ((a.dbg & kDbgCount) && (threadIdx.x & 63) == 0) {
-        atomicAdd(a.dbgcnt + 12, (unsigned long long)Lw);
-        atomicAdd(a.dbgcnt + 13, 1ull);
-    }
-    float d0 = INFINITY, dnext = INFINITY, wx = 0.f, wy = 0.f, wz = 0.f;
-    int wj = 0x7fffffff;
-    uint32_t wv = ~0u;
-    if (Lw <= kMaxOctList) {
-        Top3P k;
-        uint32_t v = 0;
-        constexpr int U = 4;
-        for (; v < Lw; v += U) {
-            float4 p[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) p[u] = S.pts[tile_addr(v + u, c1, c2, c3, L, o0, o1, o2, o3, sent)];
-#pragma unroll
-            for (int u = 0; u < U; u++) k.consider(qx, qy, qz, p[u], v + u);
-        }
-        const uint32_t kt[3] = {k.t0, k.t1, k.t2};
-#pragma unroll
-        for (int s = 0; s < 3; s++) {
-            if (kt[s] == kKeyMax) continue;
-            const uint32_t vv = kt[s] & 0xffu;
-            const float4 p = S.pts[tile_addr(vv, c1, c2, c3, L, o0, o1, o2, o3, sent)];
-            const float e = icp_d2(qx, qy, qz, p);
-            const int id = __float_as_int(p.w);
-            const bool t = e < d0 || (e == d0 && id < wj);
-            d0 = t ? e : d0;
-            wj = t ? id : wj;
-            wv = t ? vv : wv;
-            wx = t ? p.x : wx;
-            wy = t ? p.y : wy;
-            wz = t ? p.z : wz;
-        }
-        dnext = k.t3 == kKeyMax ? INFINITY : __uint_as_float(k.t3 & ~0xffu);
-    } else {  // a list of 256 or more: compare-swap top 3 on exact d2
-        Top3 b;
-        for (uint32_t v = 0; v < L; v++) b.consider(qx, qy, qz, S.pts[tile_addr(v, c1, c2, c3, L, o0, o1, o2, o3, sent)], v);
-        const uint32_t kp[3] = {b.p0, b.p1, b.p2};
-#pragma unroll
-        for (int s = 0; s < 3; s++) {
-            if (kp[s] == ~0u) continue;
-            const float4 p = S.pts[tile_addr(kp[s], c1, c2, c3, L, o0, o1, o2, o3, sent)];
-            const float e = icp_d2(qx, qy, qz, p);
-            const int id = __float_as_int(p.w);
-            const bool t = e < d0 || (e == d0 && id < wj);
-            d0 = t ? e : d0;
-            wj = t ? id : wj;
-            wv = t ? kp[s] : wv;
-            wx = t ? p.x : wx;
-            wy = t ? p.y : wy;
-            wz = t ? p.z : wz;
-        }
-        dnext = b.d3;
-    }
-    if (!active) return res;
-    {
-        const float m = fminf(fminf(fminf(fx - (float)bx, (float)(bx + 2) - fx), fminf(fy - (float)by, (float)(by + 2) - fy)),
-                              fminf(fz - (float)bz, (float)(bz + 2) - fz)) - a.mc;
-        const float rr = m * g.hf;
-        const float cert2 = fmaxf(a.cert2, rr * rr * (1.f - 2e-5f));
-        const bool found = d0 <= a.r2;
-        if (found ? (d0 < dnext && d0 <= cert2) : a.r2 <= cert2) {
-            res.settled = true;
-            res.stage = 1;
-            res.found = found;
-            res.d2 = d0;
-            res.px = wx;
-            res.py = wy;
-            res.pz = wz;
-            if (found) {
-                const uint32_t rw = wv < c1 ? 0u : wv < c2 ? 1u : wv < c3 ? 2u : 3u;
-                const uint32_t loc = tile_addr(wv, c1, c2, c3, L, o0, o1, o2, o3, sent);
-                res.gpos = loc + (rw == 0 ? rd[0] : rw == 1 ? rd[1] : rw == 2 ? rd[2] : rd[3]);
-            }
-            return res;
-        }
-    }
-    if (a.dbg & kDbgTileOctOnly) return res;
-    // ---- 2. the 3x3x3 cells around the query's cell, from the octant's winner as the bound
-    const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
-    const float lx = fx - (float)cx, ly = fy - (float)cy, lz = fz - (float)cz;
-    const float inv_h2 = g.inv_hf * g.inv_hf;
-    const float gxl = sq_gap(lx, a.mc), gxr = sq_gap(1.f - lx, a.mc);
-    float bd = a.r2;
-    int bj = 0x7fffffff;
-    uint32_t bl = ~0u, bg = ~0u;
-    if (d0 <= a.r2) {
-        bd = d0;
-        bj = wj;
-    }
-    for (int dz = -1; dz <= 1; dz++) {
-        const int z = cz + dz;
-        if (z < 0 || z >= g.n[2]) continue;
-        const float gz2 = sq_gap(axis_gap<float>(z, cz, lz), a.mc);
-        for (int dy = -1; dy <= 1; dy++) {
-            const int y = cy + dy;
-            if (y < 0 || y >= g.n[1]) continue;
-            const float lim = bd * 1.00002f * inv_h2;
-            const float gyz = gz2 + sq_gap(axis_gap<float>(y, cy, ly), a.mc);
-            if (gyz > lim) continue;
-            int xlo = max(cx - 1, 0), xhi = min(cx + 1, g.n[0] - 1);
-            if (xlo == cx - 1 && gyz + gxl > lim) xlo = cx;
-            if (xhi == cx + 1 && gyz + gxr > lim) xhi = cx;
-            if (xlo > xhi) continue;
-            const int R = row_of(y, z);
-            const uint32_t s = S.tab[R * nxe + (xlo - x0)], e = S.tab[R * nxe + (xhi + 1 - x0)];
-            const uint32_t del = S.rgs[R] - S.rls[R];
-            for (uint32_t k = s; k < e; k++) {
-                const float4 p = S.pts[k];
-                const float d2 = icp_d2(qx, qy, qz, p);
-                const int id = __float_as_int(p.w);
-                const bool t = d2 < bd || (d2 == bd && id <= bj);
-                bd = t ? d2 : bd;
-                bj = t ? id : bj;
-                bl = t ? k : bl;
-                bg = t ? k + del : bg;
-            }
-        }
-    }
-    const float m3 = fminf(fminf(fminf(fx - (float)(cx - 1), (float)(cx + 2) - fx), fminf(fy - (float)(cy - 1), (float)(cy + 2) - fy)),
-                           fminf(fz - (float)(cz - 1), (float)(cz + 2) - fz)) - a.mc;
-    const float r3 = m3 * g.hf;
-    const float c3e = r3 * r3 * (1.f - 2e-5f);
-    const bool found3 = bj != 0x7fffffff;
-    if (found3 ? bd <= c3e : a.r2 <= c3e) {
-        res.settled = true;
-        res.stage = 2;
-        res.found = found3;
-        if (found3) {
-            const float4 p = S.pts[bl];
-            res.d2 = bd;
-            res.px = p.x;
-            res.py = p.y;
-            res.pz = p.z;
-            res.gpos = bg;
-        }
-    }
-    return res;
-}
-
-// query i of the sorted set under the iteration's pose: coordinates, cell coordinates, in-grid
-// (staged search) or, outside, whether it is farther than rmax from the grid (no correspondence)
-struct TileQ {
-    float x, y, z, fx, fy, fz;
-    bool inq, out;
-};
-__device__ __forceinline__ TileQ tile_load_query(const IcpArgs& a, int64_t i) {
-    const GridDesc& g = a.g;
-    TileQ t;
-    xform(a, ldq(a, i), t.x, t.y, t.z);
-    t.fx = cell_f<float>(g, t.x, 0);
-    t.fy = cell_f<float>(g, t.y, 1);
-    t.fz = cell_f<float>(g, t.z, 2);
-    t.inq = t.fx >= 0.f && t.fx < (float)g.n[0] && t.fy >= 0.f && t.fy < (float)g.n[1] && t.fz >= 0.f &&
-            t.fz < (float)g.n[2];
-    t.out = false;
-    if (!t.inq) {
-        const float ox = fmaxf(fmaxf(-t.fx, t.fx - (float)g.n[0]), 0.f);
-        const float oy = fmaxf(fmaxf(-t.fy, t.fy - (float)g.n[1]), 0.f);
-        const float oz = fmaxf(fmaxf(-t.fz, t.fz - (float)g.n[2]), 0.f);
-        const float dout = fmaxf(sqrtf(__fmaf_rn(oz, oz, __fmaf_rn(oy, oy, ox * ox))) - a.mc, 0.f) * g.hf;
-        t.out = dout * dout > a.r2 * 1.0001f;
-    }
-    return t;
-}
-
-// first position p in [0, n] with v[p] >= key (v ascending)
-__device__ __forceinline__ int64_t lower_bound_i32(const int32_t* v, int64_t n, int64_t key) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)v[mid] < key) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
-// Workgroup w takes the query bricks (runs of sorted queries of one 8x8x8-cell brick,
-// bstart[0..nbk], bstart[nbk] = nq) starting in [w Q, (w + 1) Q), Q = ceil(nq / grid): a
-// contiguous query range [qlo, qhi) about Q long.  Per brick: one pass over its queries for
-// the box of their cells under the pose, the box staged once, then its queries in rounds of
-// 256.  Fallback queries are written in query order at fb[qlo ..] (workgroup segment).
-__global__ void __launch_bounds__(kIcpBlock, 2) k_icp_tile(IcpArgs a, const int32_t* __restrict__ bstart, int64_t nbk,
-                                                           uint32_t* __restrict__ fb_base, int write_cand) {
-    __shared__ TileShared S;
-    load_pose(a);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane < kAcc) S.acc[wid][lane] = 0.0;
-    const int64_t Q = (a.nq + gridDim.x - 1) / gridDim.x;
-    const int64_t b0 = lower_bound_i32(bstart, nbk, (int64_t)blockIdx.x * Q);
-    const int64_t b1 = lower_bound_i32(bstart, nbk, (int64_t)(blockIdx.x + 1) * Q);
-    const int64_t qlo = bstart[b0];
-    uint32_t fbn = 0;  // the workgroup's fallback count so far (same in every thread)
-    int par = 0;
-    for (int64_t b = b0; b < b1; b++) {
-        const int64_t s = bstart[b], e = bstart[b + 1];
-        // 1. the box of the brick's query cells under the pose
-        int cmin[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, cmax[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
-        for (int64_t i = s + threadIdx.x; i < e; i += kIcpBlock) {
-            const TileQ t = tile_load_query(a, i);
-            if (t.inq) {
-                const int c[3] = {(int)floorf(t.fx), (int)floorf(t.fy), (int)floorf(t.fz)};
-#pragma unroll
-                for (int d = 0; d < 3; d++) {
-                    cmin[d] = min(cmin[d], c[d]);
-                    cmax[d] = max(cmax[d], c[d]);
-                }
-            }
-        }
-        const bool whole = tile_stage(a, S, cmin, cmax);
-        if ((a.dbg & kDbgCount) && threadIdx.x == 0) {
-            atomicAdd(a.dbgcnt + 0, 1ull);
-            if (whole) atomicAdd(a.dbgcnt + 1, 1ull);
-        }
-        // 2. its queries, 256 per round
-#pragma unroll 1
-        for (int64_t r0 = s; r0 < e; r0 += kIcpBlock) {
-            const int64_t i = r0 + threadIdx.x;
-            const bool val = i < e;
-            TileQ t{};
-            if (val) t = tile_load_query(a, i);
-            bool staged = whole;
-            if (!whole) {  // the round on its own
-                int rmin[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, rmax[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
-                if (val && t.inq) {
-                    rmin[0] = rmax[0] = (int)floorf(t.fx);
-                    rmin[1] = rmax[1] = (int)floorf(t.fy);
-                    rmin[2] = rmax[2] = (int)floorf(t.fz);
-                }
-                __syncthreads();  // the previous round's readers are done with the LDS
-                staged = tile_stage(a, S, rmin, rmax);
-                if ((a.dbg & kDbgCount) && threadIdx.x == 0) atomicAdd(a.dbgcnt + (staged ? 2 : 3), 1ull);
-            }
-            // full wave: the octant's trip count is reduced over the wave
-            TileRes r = tile_query(a, S, val && !t.out && t.inq && staged && !(a.dbg & kDbgTileNone), t.x, t.y, t.z,
-                                   t.fx, t.fy, t.fz);
-            bool fb = false;
-            if (val) {
-                if (t.out) r.settled = true;  // farther than rmax from the grid: no correspondence
-                fb = !r.settled;
-                if (write_cand && r.settled)
-                    a.cand[i] = make_uint4(r.found ? r.gpos : ~0u, ~0u, ~0u, pack_dlb(0.f, a.launch));
-            }
-            // fallback list in query order: this wave's place among the workgroup's four
-            const uint64_t fbm = __ballot(fb);
-            if (lane == 0) S.fbw[par][wid] = (uint32_t)__popcll(fbm);
-            __syncthreads();
-            uint32_t before = 0, tot = 0;
-#pragma unroll
-            for (int w = 0; w < kTileW; w++) {
-                const uint32_t c = S.fbw[par][w];
-                before += w < wid ? c : 0u;
-                tot += c;
-            }
-            par ^= 1;
-            if (fb) {
-                const uint32_t pos = fbn + before + __builtin_amdgcn_mbcnt_hi((uint32_t)(fbm >> 32),
-                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)fbm, 0u));
-                a.fb[qlo + pos] = (int32_t)i;
-            }
-            fbn += tot;
-            if (a.dbg & kDbgCount) {
-                const uint64_t m4 = __ballot(val && r.stage == 1), m5 = __ballot(val && r.stage == 2);
-                const uint64_t m6 = __ballot(fb && t.inq && staged), m7 = __ballot(fb && t.inq && !staged);
-                const uint64_t m8 = __ballot(fb && !t.inq), m9 = __ballot(val && t.out);
-                if (lane == 0) {
-                    atomicAdd(a.dbgcnt + 24, (unsigned long long)__popcll(m4));
-                    atomicAdd(a.dbgcnt + 25, (unsigned long long)__popcll(m5));
-                    atomicAdd(a.dbgcnt + 26, (unsigned long long)__popcll(m6));
-                    atomicAdd(a.dbgcnt + 27, (unsigned long long)__popcll(m7));
-                    atomicAdd(a.dbgcnt + 28, (unsigned long long)__popcll(m8));
-                    atomicAdd(a.dbgcnt + 29, (unsigned long long)__popcll(m9));
-                }
-            }
-            const bool acc_ok = val && r.settled && r.found && !(a.dbg & kDbgNoAccum);
-            const Best w{r.d2, 0, 0u, r.px, r.py, r.pz};
-            chunk_accumulate(acc_ok, t.x, t.y, t.z, w, S.acc[wid], lane);
-        }
-        __syncthreads();  // the LDS box is reused by the next brick
-    }
-    if (threadIdx.x == 0) {
-        a.fb_count[blockIdx.x] = fbn;
-        a.fb_off[blockIdx.x] = fbn;
-        fb_base[blockIdx.x] = (uint32_t)qlo;
-        if (blockIdx.x == 0) a.fb_off[gridDim.x] = 0u;
-    }
-    write_wave_partials(S.acc, a.partials + (int64_t)blockIdx.x * kAcc);
 }
 
 // Lanes per query by the list's density (measured per launch on the C4 bench registration,
@@ -1882,11 +1169,7 @@ __device__ __forceinline__ void ring_run(IcpArgs& a, double (*s_acc)[kAcc], cons
             // the search pass left this launch's octant message: the 4th smallest d2 of its
             // octant.  Above the cached best, every octant point tied with that best is cached,
             // so the cached best IS the octant's (d2, index) winner and its cells need no rescan.
-#if PCP_CACHE3
             const uint32_t msg = cd.w;
-#else
-            const uint32_t msg = a.dlb[i];
-#endif
             const bool skip_oct = !a.ring_all && ((msg ^ a.launch) & 0xffu) == 0u &&
                                   __uint_as_float(msg & ~0xffu) > cbst.bd;
             bool done = false;
@@ -1934,20 +1217,11 @@ __device__ __forceinline__ void ring_run(IcpArgs& a, double (*s_acc)[kAcc], cons
                 const bool found = b.bj != 0x7fffffff;
                 done = (found && b.bd <= c2) || (!found && a.r2 <= c2);
             }
-            if ((a.dbg & kDbgCount) && lead && done) atomicAdd(a.dbgcnt + 5, 1ull);
             if (!done) box_search<G>(a.g, a.tp, qx, qy, qz, a.mc, b, sub);
-            if ((a.dbg & kDbgCount) && lead && b.bj != 0x7fffffff) atomicAdd(a.dbgcnt + 6, 1ull);
             const bool ok = b.bj != 0x7fffffff;
             // no bound kept: the next launch searches it again
             if (lead) {
-#if PCP_CACHE3
                 a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, pack_dlb(0.f, a.launch));
-                if (PCP_VER_HOT)
-                    a.hot[2 * i] = make_float4(INFINITY, INFINITY, INFINITY, __uint_as_float(pack_dlb(0.f, a.launch)));
-#else
-                a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, ~0u);
-                a.dlb[i] = pack_dlb(0.f, a.launch);
-#endif
             }
         }
         const bool acc_ok = valid && lead && b.bj != 0x7fffffff && !(a.dbg & kDbgNoAccum);
@@ -2265,61 +1539,6 @@ __global__ void k_query_keys(GridDesc g, const float* q, size_t stride_f, int64_
     }
 }
 
-// (PCP_QSORT_IDX variant) the sort key and the query's own index only; the sorted records are
-// then gathered once (k_gather_queries) instead of riding through every radix pass
-__global__ void k_query_keys_idx(GridDesc g, const float* q, size_t stride_f, int64_t n, uint32_t* key,
-                                 uint32_t* idx) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float* p = q + (size_t)i * stride_f;
-        const float x = p[0], y = p[1], z = p[2];
-        uint32_t k = query_key_end(g);
-        if (isfinite(x) && isfinite(y) && isfinite(z)) {
-            const int cx = clampi((int)floorf(cell_f<float>(g, x, 0) - 0.5f), 0, g.n[0] - 1);
-            const int cy = clampi((int)floorf(cell_f<float>(g, y, 1) - 0.5f), 0, g.n[1] - 1);
-            const int cz = clampi((int)floorf(cell_f<float>(g, z, 2) - 0.5f), 0, g.n[2] - 1);
-            if (PCP_QBRICK != 4) {
-                constexpr int B = PCP_QBRICK;
-                const int64_t b = ((int64_t)(cz / B) * qbricks(g, 1) + cy / B) * qbricks(g, 0) + cx / B;
-                k = (uint32_t)(b * B * B * B + ((cz % B) * B + cy % B) * B + cx % B);
-            } else {
-                k = PCP_QKEY_LOCAL ? (uint32_t)(brick_of(g, cx, cy, cz) * 64 + local_of(cx, cy, cz))
-                                   : (uint32_t)brick_of(g, cx, cy, cz);
-            }
-        }
-        key[i] = k;
-        idx[i] = (uint32_t)i;
-    }
-}
-__global__ void k_gather_queries(const float* q, size_t stride_f, const uint32_t* idx, int64_t n, QXyz* q3,
-                                 int32_t* qi) {
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t i = idx[s];
-        const float* p = q + (size_t)i * stride_f;
-        q3[s] = QXyz{p[0], p[1], p[2]};
-        qi[s] = (int32_t)i;
-    }
-}
-
-// the first query of each query brick (PCP_QBRICK^3 cells) in the sorted keys (finite keys only)
-#ifndef PCP_QSORT_IDX_DEFAULT  // query sort: (key, index) pairs + one gather (1) or 16-byte records as payload (0)
-#define PCP_QSORT_IDX_DEFAULT 0
-#endif
-#ifndef PCP_VER_DENSE  // verify: failures per 64-query chunk from which the whole chunk is searched (0: off)
-#define PCP_VER_DENSE 0
-#endif
-#ifndef PCP_ICP_TILE_DEFAULT  // dense grids: 1 = the LDS-tiled engine by default, 0 = the cached engine
-#define PCP_ICP_TILE_DEFAULT 0
-#endif
-struct BrickHead {
-    const uint32_t* k;
-    uint32_t end;
-    __device__ bool operator()(int i) const {
-        constexpr uint32_t B3 = PCP_QBRICK * PCP_QBRICK * PCP_QBRICK;
-        const uint32_t v = k[i];
-        return v < end && (i == 0 || v / B3 != k[i - 1] / B3);
-    }
-};
-
 // the sorted {x, y, z, bits(index)} records -> 12-byte xyz + index arrays
 __global__ void k_split_queries(const float4* qs, int64_t n, QXyz* q, int32_t* qi) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -2490,8 +1709,6 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     const double rr = (0.5 - (double)a.mc) * a.g.h;
     a.cert2 = (float)(rr * rr * (1.0 - 1e-5));
     a.cand = icp->cand;
-    a.hot = icp->hot;
-    a.dlb = icp->dlb;
     a.pose_hist = icp->pose_hist;
     a.launch = (uint32_t)icp->launches;
     a.ntp = (uint32_t)tg->n;
@@ -2508,9 +1725,6 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.nseg = (int64_t)icp->nb_fast * (kIcpBlock / 64);
     a.ring_all = a.g.dense ? 0 : 1;
     a.dbg = icp->dbg;
-    a.ver_dense = icp->ver_dense;
-    a.dbgcnt = icp->dbgcnt;
-    a.dbgfz = icp->dbgfz;
     double* part_v = icp->partials;
     double* part_o = part_v + (int64_t)icp->nb_ver * kAcc;
     double* part_r = part_o + (int64_t)icp->nb_fast * kAcc;
@@ -2529,45 +1743,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
         e1 = icp->tev[icp->ntev].second;
         icp->ntev++;
     }
-    if (icp->dbgcnt) PCP_HIP(ctx, hipMemsetAsync(icp->dbgcnt, 0, 32 * sizeof(unsigned long long), ctx->stream));
     PCP_HIP(ctx, hipEventRecord(e0, ctx->stream));
-    if (a.g.dense && icp->engine_tile && icp->bstart) {
-        // the LDS-tiled streaming search of every query, then the exact fallback of the rest
-        icp->last_verified = false;
-        PCP_HIP(ctx, hipMemsetAsync(part_v, 0, (size_t)(icp->nb_ver + icp->nb_fast) * kAcc * sizeof(double),
-                                    ctx->stream));
-        a.partials = part_o;
-        a.nseg = icp->nb_tile;  // one fallback segment per workgroup
-        a.fb_seg = 0;
-        const int want_cand = (corr_idx != nullptr || args_out != nullptr) ? 1 : 0;
-        if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_ver, ctx->stream));
-        hipLaunchKernelGGL(k_icp_tile, dim3(icp->nb_tile), dim3(kIcpBlock), 0, ctx->stream, a,
-                           (const int32_t*)icp->bstart, icp->nbk, icp->fb_base, want_cand);
-        if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_mid, ctx->stream));
-        PCP_TRY(scan_u32_inplace(ctx, icp->fb_off, a.nseg + 1, nullptr));
-        hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)((a.nseg + 3) / 4)), dim3(256), 0, ctx->stream, icp->fb,
-                           (const uint32_t*)icp->fb_count, (const uint32_t*)icp->fb_off, a.nseg, (int64_t)0, icp->fbc,
-                           (const uint32_t*)icp->fb_base);
-        a.partials = part_r;
-        a.ring_g = icp->ring_g;
-        hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, ctx->stream, a, part_r,
-                           (const int32_t*)icp->fbc, (const uint32_t*)(icp->fb_off + a.nseg));
-        PCP_HIP(ctx, hipEventRecord(e1, ctx->stream));
-        hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kAcc * kRedGroups), 0, ctx->stream, icp->partials,
-                           icp->nb_ver + icp->nb_fast + icp->nb_ring, acc_dev, (const uint32_t*)(icp->fb_off + a.nseg));
-        if (corr_idx) {
-            if (icp->nq_in > icp->nq)
-                hipLaunchKernelGGL(k_fill_corr, dim3(grid_for(icp->nq_in, 256)), dim3(256), 0, ctx->stream, corr_idx,
-                                   corr_d2, icp->nq_in);
-            if (icp->nq > 0)
-                hipLaunchKernelGGL(k_scatter_corr, dim3(grid_for(icp->nq, 256)), dim3(256), 0, ctx->stream, a,
-                                   corr_idx, corr_d2);
-        }
-        if (args_out) *args_out = a;
-        icp->launches++;
-        PCP_LAUNCH_CHECK(ctx);
-        return PCP_OK;
-    }
     const bool verify = a.g.dense && icp->launches > 0;  // the first launch has nothing cached
     icp->last_verified = verify;
     if (a.g.dense) {
@@ -2681,6 +1857,156 @@ int pcp_icp_check_sizes(int64_t n_target, int64_t nq) {
     return PCP_OK;
 }
 
+}  // extern "C"
+
+namespace pcp {
+namespace {
+
+// the query sort of an ICP handle between its launch and its completion: keys of the octant-block
+// bricks of the target grid, a stable radix sort with the 16-byte records as payload, the count
+// of finite queries
+struct QuerySort {
+    uint32_t *k0 = nullptr, *k1 = nullptr;
+    float4 *r0 = nullptr, *qs = nullptr;
+    unsigned long long* d_cnt = nullptr;
+    void* tmp = nullptr;
+    hipEvent_t done = nullptr;
+    int64_t nq = 0;
+    void release(pcp_ctx* ctx) {  // stream-ordered on ctx->stream (after it waited for `done`)
+        dfree(ctx, k0); dfree(ctx, k1); dfree(ctx, r0); dfree(ctx, qs); dfree(ctx, d_cnt); dfree(ctx, tmp);
+        k0 = k1 = nullptr; r0 = qs = nullptr; d_cnt = nullptr; tmp = nullptr;
+        if (done) event_put(ctx, done);
+        done = nullptr;
+    }
+};
+
+int icp_check_grid(pcp_ctx* ctx, const GridDesc& g, int64_t n_target, int64_t nq) {
+    if (int rc = pcp_icp_check_sizes(n_target, nq))
+        return set_error(ctx, rc, rc == PCP_ERR_CAPACITY ? "ICP target must have < 2^28 - 1 points (32-bit record offsets)"
+                                                         : "ICP supports < 2^31 queries");
+    if (g.nbricks * 64 >= ((int64_t)1 << 32) ||
+        qbricks(g, 0) * qbricks(g, 1) * qbricks(g, 2) * PCP_QBRICK * PCP_QBRICK * PCP_QBRICK >= ((int64_t)1 << 32))
+        return set_error(ctx, PCP_ERR_UNSUPPORTED, "ICP target grid too large for 32-bit cell keys");
+    return PCP_OK;
+}
+
+// enqueue the query sort on `st` (after everything enqueued so far on ctx->stream); `s.done` is
+// recorded on `st` when it is complete
+int qsort_launch(pcp_ctx* ctx, hipStream_t st, const GridDesc& g, const float* q, size_t q_stride, int64_t nq,
+                 QuerySort& s) {
+    s.nq = nq;
+    int rc = PCP_OK;
+    if ((rc = dmalloc(ctx, &s.k0, nq)) || (rc = dmalloc(ctx, &s.k1, nq)) || (rc = dmalloc(ctx, &s.r0, nq)) ||
+        (rc = dmalloc(ctx, &s.qs, nq + 1)) || (rc = dmalloc(ctx, &s.d_cnt, 1)))
+        return rc;
+    PCP_HIP(ctx, event_get(ctx, &s.done));
+    if (st != ctx->stream) {  // the side stream starts after the main stream's work so far
+        hipEvent_t go = nullptr;
+        PCP_HIP(ctx, event_get(ctx, &go));
+        hipError_t e = hipEventRecord(go, ctx->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, go, 0);
+        event_put(ctx, go);  // (reused only by a later record on ctx->stream: stream-ordered)
+        if (e != hipSuccess) return hip_fail(ctx, e, "query sort stream order", __FILE__, __LINE__);
+    }
+    PCP_HIP(ctx, hipMemsetAsync(s.d_cnt, 0, sizeof(unsigned long long), st));
+    if (nq > 0) {
+        unsigned bits = 1;  // keys are in [0, query_key_end]
+        while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)query_key_end(g)) bits++;
+        size_t tb = 0;
+        hipLaunchKernelGGL(k_query_keys, dim3(grid_for(nq, 256)), dim3(256), 0, st, g, q, q_stride / sizeof(float), nq,
+                           s.k0, s.r0);
+        PCP_HIP(ctx, rocprim::radix_sort_pairs<RecSortConfig>(nullptr, tb, s.k0, s.k1, s.r0, s.qs, (size_t)nq, 0u, bits, st));
+        if ((rc = dmalloc(ctx, (char**)&s.tmp, tb))) return rc;
+        PCP_HIP(ctx, rocprim::radix_sort_pairs<RecSortConfig>(s.tmp, tb, s.k0, s.k1, s.r0, s.qs, (size_t)nq, 0u, bits, st));
+        hipLaunchKernelGGL(k_first_at_least, dim3(1), dim3(1), 0, st, s.k1, nq, query_key_end(g), s.d_cnt);
+    }
+    PCP_HIP(ctx, hipGetLastError());
+    PCP_HIP(ctx, hipEventRecord(s.done, st));
+    return PCP_OK;
+}
+
+// the sorted records -> 12-byte xyz + original indices, on ctx->stream after the sort
+int qsort_finish(pcp_ctx* ctx, QuerySort& s, QXyz** q3, int32_t** qi, int64_t* nfin) {
+    PCP_HIP(ctx, hipStreamWaitEvent(ctx->stream, s.done, 0));
+    unsigned long long hc = 0;
+    PCP_HIP(ctx, hipMemcpyAsync(&hc, s.d_cnt, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *nfin = (int64_t)hc;
+    int rc = PCP_OK;
+    if ((rc = dmalloc(ctx, q3, s.nq + 1)) || (rc = dmalloc(ctx, qi, s.nq + 1))) return rc;
+    if (*nfin > 0)
+        hipLaunchKernelGGL(k_split_queries, dim3(grid_for(*nfin, 256)), dim3(256), 0, ctx->stream,
+                           (const float4*)s.qs, *nfin, *q3, *qi);
+    PCP_HIP(ctx, hipGetLastError());
+    return PCP_OK;
+}
+
+// the handle over sorted queries (q3, qi: owned by the handle from here on)
+int icp_make(pcp_ctx* ctx, const pcp_index* target, QXyz* q3, int32_t* qi, int64_t nfin, int64_t nq, pcp_icp** out) {
+    pcp_icp* icp = new pcp_icp();
+    icp->ctx = ctx;
+    icp->owner = ctx;
+    ctx_retain(ctx);
+    icp->target = target;
+    icp->nq = nfin;
+    icp->nq_in = nq;
+    icp->q = q3;
+    icp->qidx = qi;
+    int dev_cus = 256;  // one attribute query (the whole hipDeviceProp_t costs ~0.1 ms per create)
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess && cus > 0)
+        dev_cus = cus;
+    const int64_t want = (icp->nq + kIcpBlock - 1) / kIcpBlock;
+    icp->nb_fast = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_OCT_WAVES));
+    icp->nb_fast_l = (int)std::max<int64_t>(1, std::min<int64_t>(icp->nb_fast, (int64_t)dev_cus * PCP_OCT_WAVES_LIST));
+    icp->nb_ring = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_RING_WAVES));
+    const int64_t nwaves = (int64_t)icp->nb_fast * (kIcpBlock / 64);
+    const int64_t nwaves_l = (int64_t)icp->nb_fast_l * (kIcpBlock / 64);  // the smaller grid: larger segments
+    const int64_t nchunks64 = (icp->nq + 63) / 64;
+    icp->fb_seg = ((nchunks64 + nwaves_l - 1) / nwaves_l) * 64;
+    icp->nb_ver = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_VER_WAVES));
+    const int64_t nwaves_v = (int64_t)icp->nb_ver * (kIcpBlock / 64);
+    icp->sv_seg = ((nchunks64 + nwaves_v - 1) / nwaves_v) * 64;  // contiguous ranges: <= this per wave
+    icp->nseg_v = nwaves_v;
+    int rc = dmalloc(ctx, &icp->partials, (size_t)(icp->nb_ver + icp->nb_fast + icp->nb_ring) * kAcc);
+    if (!rc) rc = dmalloc(ctx, &icp->acc, kAcc);
+    if (!rc) rc = dmalloc(ctx, &icp->pose_dev, 24);
+    if (!rc) rc = dmalloc(ctx, &icp->cand, icp->nq + 1);
+    if (!rc) rc = dmalloc(ctx, &icp->pose_hist, kHist * 12);
+    // the first launch over a dense grid (the octant pass over every query) writes every cache
+    // record before any pass reads one: only the sentinel record needs its value then (an 800 MB
+    // memset at 50M queries, ~0.1 ms of the pre-iteration span, otherwise)
+    const bool cand_all = !target->g.dense;
+    if (!rc && (hipMemsetAsync(icp->cand + (cand_all ? 0 : icp->nq), 0xff,
+                               (size_t)(cand_all ? icp->nq + 1 : 1) * sizeof(uint4), ctx->stream) != hipSuccess ||
+                hipMemsetAsync(icp->pose_hist, 0, kHist * 12 * sizeof(float), ctx->stream) != hipSuccess ||
+                hipMemsetAsync(icp->pose_dev, 0, 24 * sizeof(float), ctx->stream) != hipSuccess))
+        rc = set_error(ctx, PCP_ERR_HIP, "memset");
+    if (!rc) rc = dmalloc(ctx, &icp->sv, (size_t)icp->nseg_v * icp->sv_seg + 1);
+    if (!rc) rc = dmalloc(ctx, &icp->sv_count, (size_t)icp->nseg_v);
+    if (!rc) rc = dmalloc(ctx, &icp->sv_off, (size_t)icp->nseg_v + 1);
+    if (!rc) rc = dmalloc(ctx, &icp->svc, icp->nq + 1);
+    const int64_t fb_cap = std::max<int64_t>(nwaves * icp->fb_seg, icp->nq);
+    if (!rc) rc = dmalloc(ctx, &icp->fb, (size_t)fb_cap + 1);
+    if (!rc) rc = dmalloc(ctx, &icp->fb_count, (size_t)nwaves);
+    if (!rc) rc = dmalloc(ctx, &icp->fb_off, (size_t)nwaves + 1);
+    if (!rc) rc = dmalloc(ctx, &icp->fbc, icp->nq + 1);
+    if (!rc && (event_get(ctx, &icp->ev0) != hipSuccess || event_get(ctx, &icp->ev1) != hipSuccess ||
+                event_get(ctx, &icp->ev_mid) != hipSuccess || event_get(ctx, &icp->ev_ver) != hipSuccess))
+        rc = set_error(ctx, PCP_ERR_HIP, "hipEventCreate failed");
+    if (rc) {
+        pcp_icp_destroy(icp);
+        return rc;
+    }
+    *out = icp;
+    return PCP_OK;
+}
+
+}  // namespace
+}  // namespace pcp
+
+extern "C" {
+
 int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t q_stride, int64_t nq,
                    pcp_icp** out) {
     if (!ctx || !target || !out || nq < 0 || (nq > 0 && !q)) return PCP_ERR_ARG;
@@ -2689,225 +2015,73 @@ int pcp_icp_create(pcp_ctx* ctx, const pcp_index* target, const float* q, size_t
     *out = nullptr;
     if (q_stride == 0) q_stride = 3 * sizeof(float);
     if (q_stride % sizeof(float)) return pcp::set_error(ctx, PCP_ERR_ARG, "query stride must be whole floats");
-    if (int rc = pcp_icp_check_sizes(target->n, nq)) {
-        return pcp::set_error(ctx, rc, rc == PCP_ERR_CAPACITY ? "ICP target must have < 2^28 - 1 points (32-bit record offsets)"
-                                                              : "ICP supports < 2^31 queries");
-    }
-    if (target->g.nbricks * 64 >= ((int64_t)1 << 32) ||
-        pcp::qbricks(target->g, 0) * pcp::qbricks(target->g, 1) * pcp::qbricks(target->g, 2) * PCP_QBRICK *
-                PCP_QBRICK * PCP_QBRICK >= ((int64_t)1 << 32))
-        return pcp::set_error(ctx, PCP_ERR_UNSUPPORTED, "ICP target grid too large for 32-bit cell keys");
-    // sort the query set once by target-grid brick (stable radix sort, record as payload)
-    hipStream_t st = ctx->stream;
-    float4* qs = nullptr;
-    pcp::QXyz* q3 = nullptr;  // the sorted records split: 12-byte xyz + original index
+    PCP_TRY(pcp::icp_check_grid(ctx, target->g, target->n, nq));
+    pcp::QuerySort s;
+    pcp::QXyz* q3 = nullptr;
     int32_t* qi = nullptr;
     int64_t nfin = 0;
-    int32_t* bst = nullptr;  // query bricks (dense target grids, tile engine)
-    int64_t nbk = 0;
-    int engine_tile = PCP_ICP_TILE_DEFAULT;
-    if (const char* eg = std::getenv("PCP_ICP_ENGINE"))
-        engine_tile = std::strcmp(eg, "tile") == 0 ? 1 : std::strcmp(eg, "cache") == 0 ? 0 : engine_tile;
-    {
-        uint32_t *k0 = nullptr, *k1 = nullptr;
-        float4* r0 = nullptr;
-        unsigned long long* d_cnt = nullptr;
-        void* tmp = nullptr;
-        int rc = pcp::dmalloc(ctx, &k0, nq);
-        if (!rc) rc = pcp::dmalloc(ctx, &k1, nq);
-        if (!rc) rc = pcp::dmalloc(ctx, &r0, nq);
-        if (!rc) rc = pcp::dmalloc(ctx, &qs, nq + 1);
-        if (!rc) rc = pcp::dmalloc(ctx, &d_cnt, 2);
-        if (!rc && hipMemsetAsync(d_cnt, 0, 2 * sizeof(unsigned long long), st) != hipSuccess)
-            rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
-        // PCP_QSORT_IDX=1 (A/B): sort (key, u32 index) pairs and gather the records once, instead
-        // of carrying the 16-byte records through every radix pass
-        const char* qsi = std::getenv("PCP_QSORT_IDX");
-        const bool sort_idx = qsi ? std::atoi(qsi) != 0 : PCP_QSORT_IDX_DEFAULT != 0;
-        uint32_t *i0 = nullptr, *i1 = nullptr;
-        if (!rc && nq > 0) {
-            unsigned bits = 1;  // keys are in [0, query_key_end]
-            while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)pcp::query_key_end(target->g)) bits++;
-            size_t tb = 0;
-            hipError_t e = hipSuccess;
-            if (sort_idx) {
-                rc = pcp::dmalloc(ctx, &i0, nq);
-                if (!rc) rc = pcp::dmalloc(ctx, &i1, nq);
-                if (!rc) {
-                    hipLaunchKernelGGL(pcp::k_query_keys_idx, dim3(pcp::grid_for(nq, 256)), dim3(256), 0, st, target->g,
-                                       q, q_stride / sizeof(float), nq, k0, i0);
-                    e = rocprim::radix_sort_pairs(nullptr, tb, k0, k1, i0, i1, (size_t)nq, 0u, bits, st);
-                    if (e == hipSuccess && !(rc = pcp::dmalloc(ctx, (char**)&tmp, tb)))
-                        e = rocprim::radix_sort_pairs(tmp, tb, k0, k1, i0, i1, (size_t)nq, 0u, bits, st);
-                }
-            } else {
-                hipLaunchKernelGGL(pcp::k_query_keys, dim3(pcp::grid_for(nq, 256)), dim3(256), 0, st, target->g, q,
-                                   q_stride / sizeof(float), nq, k0, r0);
-                e = rocprim::radix_sort_pairs<pcp::RecSortConfig>(nullptr, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
-                if (e == hipSuccess && !(rc = pcp::dmalloc(ctx, (char**)&tmp, tb)))
-                    e = rocprim::radix_sort_pairs<pcp::RecSortConfig>(tmp, tb, k0, k1, r0, qs, (size_t)nq, 0u, bits, st);
-            }
-            if (!rc && e == hipSuccess)
-                hipLaunchKernelGGL(pcp::k_first_at_least, dim3(1), dim3(1), 0, st, k1, nq,
-                                   pcp::query_key_end(target->g), d_cnt);
-            // the tile engine's query bricks: heads of the brick runs -> k0 (as int32)
-            const bool bricks = target->g.dense && engine_tile;  // only the tile engine reads them
-            if (!rc && e == hipSuccess && bricks) {
-                const pcp::BrickHead head{k1, pcp::query_key_end(target->g)};
-                size_t tb2 = 0;
-                e = rocprim::select(nullptr, tb2, rocprim::counting_iterator<int>(0), (int*)k0, d_cnt + 1, (size_t)nq,
-                                    head, st);
-                if (e == hipSuccess && tb2 > tb) {
-                    pcp::dfree(ctx, tmp);
-                    tmp = nullptr;
-                    rc = pcp::dmalloc(ctx, (char**)&tmp, tb2);
-                    tb = tb2;
-                }
-                if (!rc && e == hipSuccess)
-                    e = rocprim::select(tmp, tb2, rocprim::counting_iterator<int>(0), (int*)k0, d_cnt + 1, (size_t)nq,
-                                        head, st);
-            }
-            unsigned long long hc[2] = {0, 0};
-            if (!rc && e == hipSuccess) e = hipMemcpyAsync(hc, d_cnt, sizeof(hc), hipMemcpyDeviceToHost, st);
-            if (!rc && e == hipSuccess) e = hipStreamSynchronize(st);
-            if (!rc && e != hipSuccess) rc = pcp::hip_fail(ctx, e, "query sort", __FILE__, __LINE__);
-            nfin = (int64_t)hc[0];
-            if (!rc && bricks && hc[1] > 0) {
-                nbk = (int64_t)hc[1];
-                const int32_t last = (int32_t)nfin;
-                rc = pcp::dmalloc(ctx, &bst, (size_t)nbk + 1);
-                if (!rc && (hipMemcpyAsync(bst, k0, (size_t)nbk * sizeof(int32_t), hipMemcpyDeviceToDevice, st) != hipSuccess ||
-                            hipMemcpyAsync(bst + nbk, &last, sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
-                            hipStreamSynchronize(st) != hipSuccess))
-                    rc = pcp::set_error(ctx, PCP_ERR_HIP, "query bricks");
-            }
-        }
-        if (!rc) rc = pcp::dmalloc(ctx, &q3, nq + 1);
-        if (!rc) rc = pcp::dmalloc(ctx, &qi, nq + 1);
-        if (!rc && nfin > 0) {
-            if (sort_idx)
-                hipLaunchKernelGGL(pcp::k_gather_queries, dim3(pcp::grid_for(nfin, 256)), dim3(256), 0, st, q,
-                                   q_stride / sizeof(float), (const uint32_t*)i1, nfin, q3, qi);
-            else
-                hipLaunchKernelGGL(pcp::k_split_queries, dim3(pcp::grid_for(nfin, 256)), dim3(256), 0, st,
-                                   (const float4*)qs, nfin, q3, qi);
-            if (hipGetLastError() != hipSuccess) rc = pcp::set_error(ctx, PCP_ERR_HIP, "query split");
-        }
-        pcp::dfree(ctx, i0);
-        pcp::dfree(ctx, i1);
-        pcp::dfree(ctx, k0);
-        pcp::dfree(ctx, k1);
-        pcp::dfree(ctx, r0);
-        pcp::dfree(ctx, d_cnt);
-        pcp::dfree(ctx, tmp);
-        pcp::dfree(ctx, qs);  // (stream-ordered: the cache hands it out again only to later work)
-        if (rc) {
-            pcp::dfree(ctx, q3);
-            pcp::dfree(ctx, qi);
-            pcp::dfree(ctx, bst);
-            return rc;
-        }
-    }
-    pcp_icp* icp = new pcp_icp();
-    icp->ctx = ctx;
-    icp->owner = ctx;
-    pcp::ctx_retain(ctx);
-    icp->target = target;
-    icp->nq = nfin;
-    icp->nq_in = nq;
-    icp->q = q3;
-    icp->qidx = qi;
-    icp->bstart = bst;
-    icp->nbk = nbk;
-    int dev_cus = 256;  // one attribute query (the whole hipDeviceProp_t costs ~0.1 ms per create)
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess && cus > 0)
-        dev_cus = cus;
-    const int64_t want = (icp->nq + pcp::kIcpBlock - 1) / pcp::kIcpBlock;
-    icp->nb_fast = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_OCT_WAVES));
-    icp->nb_fast_l = (int)std::max<int64_t>(1, std::min<int64_t>(icp->nb_fast, (int64_t)dev_cus * PCP_OCT_WAVES_LIST));
-    icp->nb_ring = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_RING_WAVES));
-    const int64_t nwaves = (int64_t)icp->nb_fast * (pcp::kIcpBlock / 64);
-    const int64_t nwaves_l = (int64_t)icp->nb_fast_l * (pcp::kIcpBlock / 64);  // the smaller grid: larger segments
-    const int64_t nchunks64 = (icp->nq + 63) / 64;
-    icp->fb_seg = ((nchunks64 + nwaves_l - 1) / nwaves_l) * 64;
-    // tile engine: two workgroups per CU (LDS-bound), each a contiguous range of query bricks
-    // (capped at nb_fast: a tile workgroup writes its accumulators into the octant pass's partials
-    // region, which holds nb_fast blocks; sparse queries over many bricks would otherwise spill into
-    // the fallback pass's region and past the allocation)
-    icp->nb_tile = (int)std::max<int64_t>(
-        1, std::min<int64_t>({icp->nbk, (int64_t)dev_cus * 2, (int64_t)icp->nb_fast}));
-    icp->engine_tile = engine_tile;
-    icp->ver_dense = PCP_VER_DENSE;
-    if (const char* vd = std::getenv("PCP_VER_DENSE")) icp->ver_dense = std::max(0, std::min(64, std::atoi(vd)));
-    icp->nb_ver = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)dev_cus * PCP_VER_WAVES));
-    const int64_t nwaves_v = (int64_t)icp->nb_ver * (pcp::kIcpBlock / 64);
-#if PCP_VER_XCD
-    icp->sv_seg = 64;  // one segment per chunk
-    icp->nseg_v = nchunks64;
-#else
-    icp->sv_seg = ((nchunks64 + nwaves_v - 1) / nwaves_v) * 64;  // contiguous ranges: <= this per wave
-    icp->nseg_v = nwaves_v;
-#endif
-    int rc = pcp::dmalloc(ctx, &icp->partials, (size_t)(icp->nb_ver + icp->nb_fast + icp->nb_ring) * pcp::kAcc);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->acc, pcp::kAcc);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_dev, 24);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->cand, icp->nq + 1);
-    if (!rc && !PCP_CACHE3) rc = pcp::dmalloc(ctx, &icp->dlb, icp->nq + 1);  // else packed in cand.w
-    if (!rc && PCP_VER_HOT) rc = pcp::dmalloc(ctx, &icp->hot, 2 * (icp->nq + 1));
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->pose_hist, pcp::kHist * 12);
-    // the cached engine's first launch (the dense octant pass over every query) writes every cache
-    // record before any pass reads one: only the sentinel record needs its value then (an 800 MB
-    // memset at 50M queries, ~0.1 ms of the pre-iteration span, otherwise)
-    const bool cand_all = !(target->g.dense && !engine_tile);
-    if (!rc && (hipMemsetAsync(icp->cand + (cand_all ? 0 : icp->nq), 0xff,
-                               (size_t)(cand_all ? icp->nq + 1 : 1) * sizeof(uint4), ctx->stream) != hipSuccess ||
-                (icp->hot && hipMemsetAsync(icp->hot, 0, (size_t)2 * (icp->nq + 1) * sizeof(float4), ctx->stream) !=
-                                 hipSuccess) ||
-
-                (icp->dlb && hipMemsetAsync(icp->dlb, 0, (size_t)(icp->nq + 1) * sizeof(uint32_t), ctx->stream) !=
-                                 hipSuccess) ||
-                hipMemsetAsync(icp->pose_hist, 0, pcp::kHist * 12 * sizeof(float), ctx->stream) != hipSuccess ||
-                hipMemsetAsync(icp->pose_dev, 0, 24 * sizeof(float), ctx->stream) != hipSuccess))
-        rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv, (size_t)icp->nseg_v * icp->sv_seg + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_count, (size_t)icp->nseg_v);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->sv_off, (size_t)icp->nseg_v + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->svc, icp->nq + 1);
-
-    // fallback segments: the octant pass's or the tile engine's, whichever needs more
-    const int64_t nseg_t = icp->nb_tile;  // the tile engine's segments sit at their query range
-    const int64_t fb_cap = std::max<int64_t>(nwaves * icp->fb_seg, icp->nq);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb, (size_t)fb_cap + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_count, (size_t)std::max<int64_t>(nwaves, nseg_t));
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_off, (size_t)std::max<int64_t>(nwaves, nseg_t) + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->fbc, icp->nq + 1);
-    if (!rc) rc = pcp::dmalloc(ctx, &icp->fb_base, (size_t)icp->nb_tile);
-    if (!rc && (pcp::event_get(ctx, &icp->ev0) != hipSuccess || pcp::event_get(ctx, &icp->ev1) != hipSuccess ||
-                pcp::event_get(ctx, &icp->ev_mid) != hipSuccess || pcp::event_get(ctx, &icp->ev_ver) != hipSuccess))
-        rc = pcp::set_error(ctx, PCP_ERR_HIP, "hipEventCreate failed");
-    if (const char* ab = std::getenv("PCP_ICP_ABLATE")) icp->dbg = std::atoi(ab);
-    if (const char* og = std::getenv("PCP_OCT_G")) {  // A/B: lanes per query, "first,list"
-        int f = 1, l = 1;
-        if (std::sscanf(og, "%d,%d", &f, &l) == 2) {
-            auto ok = [](int v) { return v == 1 || v == 2 || v == 4 || v == 8; };
-            if (ok(f) || f == 0) icp->oct_g_first = f;
-            if (ok(l) || l == 0) icp->oct_g_list = l;
-        }
-    }
-    if (const char* rg = std::getenv("PCP_RING_LANES")) {  // A/B and tests: fallback-pass lanes per query
-        const int g = std::atoi(rg);
-        if (g == 0 || g == 1 || g == 2 || g == 4 || g == 8) icp->ring_g = g;
-    }
-    if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgcnt, 32);
-    if (!rc && (icp->dbg & pcp::kDbgCount)) rc = pcp::dmalloc(ctx, &icp->dbgfz, icp->nq / 64 + 2);
-    if (!rc && icp->dbgfz && hipMemsetAsync(icp->dbgfz, 0, (icp->nq / 64 + 2) * sizeof(uint2), ctx->stream) != hipSuccess)
-        rc = pcp::set_error(ctx, PCP_ERR_HIP, "memset");
+    int rc = pcp::qsort_launch(ctx, ctx->stream, target->g, q, q_stride, nq, s);
+    if (!rc) rc = pcp::qsort_finish(ctx, s, &q3, &qi, &nfin);
+    s.release(ctx);
     if (rc) {
-        pcp_icp_destroy(icp);
+        pcp::dfree(ctx, q3);
+        pcp::dfree(ctx, qi);
         return rc;
     }
-    *out = icp;
+    return pcp::icp_make(ctx, target, q3, qi, nfin, nq, out);
+}
+
+int pcp_icp_create_with_target(pcp_ctx* ctx, const float* target_xyz, size_t t_stride, int64_t n_target,
+                               double cell_size, const float* q, size_t q_stride, int64_t nq, pcp_index** index_out,
+                               pcp_icp** icp_out) {
+    if (!ctx || !index_out || !icp_out || nq < 0 || (nq > 0 && !q) || n_target < 0 || (n_target > 0 && !target_xyz))
+        return PCP_ERR_ARG;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    *index_out = nullptr;
+    *icp_out = nullptr;
+    if (q_stride == 0) q_stride = 3 * sizeof(float);
+    if (q_stride % sizeof(float)) return pcp::set_error(ctx, PCP_ERR_ARG, "query stride must be whole floats");
+    // the query sort needs only the target grid's geometry: it runs on the side stream while the
+    // target's cell sort runs on the main stream (two independent radix sorts overlapped)
+    pcp::QuerySort s;
+    bool launched = false;
+    const pcp::GeomHook hook = [&](const pcp::GridDesc& g) -> int {
+        PCP_TRY(pcp::icp_check_grid(ctx, g, n_target, nq));
+        hipStream_t side = nullptr;
+        PCP_TRY(pcp::side_stream(ctx, &side));
+        launched = true;
+        return pcp::qsort_launch(ctx, side, g, q, q_stride, nq, s);
+    };
+    pcp_index* ix = nullptr;
+    int rc = pcp::index_build_f32_hooked(ctx, target_xyz, t_stride, n_target, cell_size, &ix, hook);
+    pcp::QXyz* q3 = nullptr;
+    int32_t* qi = nullptr;
+    int64_t nfin = 0;
+    if (!rc && !launched) rc = pcp::qsort_launch(ctx, ctx->stream, ix->g, q, q_stride, nq, s);
+    if (!rc) rc = pcp::qsort_finish(ctx, s, &q3, &qi, &nfin);
+    if (rc && launched) (void)hipStreamSynchronize(ctx->side);  // the side stream's work is over
+    s.release(ctx);
+    if (!rc) rc = pcp::icp_make(ctx, ix, q3, qi, nfin, nq, icp_out);
+    else {
+        pcp::dfree(ctx, q3);
+        pcp::dfree(ctx, qi);
+    }
+    if (rc) {
+        if (ix) pcp_index_destroy(ix);
+        return rc;
+    }
+    *index_out = ix;
+    return PCP_OK;
+}
+
+int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, int ring_lanes, int ablate) {
+    if (!icp) return PCP_ERR_ARG;
+    auto lanes = [](int v) { return v == 0 || v == 1 || v == 2 || v == 4 || v == 8; };
+    if (!lanes(oct_lanes_first) || !lanes(oct_lanes_list) || !lanes(ring_lanes) || ablate < 0) return PCP_ERR_ARG;
+    icp->oct_g_first = oct_lanes_first ? oct_lanes_first : 1;
+    icp->oct_g_list = oct_lanes_list;
+    icp->ring_g = ring_lanes;
+    icp->dbg = ablate;
     return PCP_OK;
 }
 
@@ -2919,22 +2093,16 @@ int pcp_icp_destroy(pcp_icp* icp) {
     pcp::dfree(icp->owner, icp->partials);
     pcp::dfree(icp->owner, icp->acc);
     pcp::dfree(icp->owner, icp->cand);
-    pcp::dfree(icp->owner, icp->hot);
-    pcp::dfree(icp->owner, icp->dlb);
     pcp::dfree(icp->owner, icp->pose_hist);
     pcp::dfree(icp->owner, icp->sv);
     pcp::dfree(icp->owner, icp->sv_count);
     pcp::dfree(icp->owner, icp->sv_off);
     pcp::dfree(icp->owner, icp->svc);
 
-    pcp::dfree(icp->owner, icp->dbgcnt);
-    pcp::dfree(icp->owner, icp->dbgfz);
     pcp::dfree(icp->owner, icp->fb);
     pcp::dfree(icp->owner, icp->fb_count);
     pcp::dfree(icp->owner, icp->fb_off);
     pcp::dfree(icp->owner, icp->fbc);
-    pcp::dfree(icp->owner, icp->bstart);
-    pcp::dfree(icp->owner, icp->fb_base);
     pcp::dfree(icp->owner, icp->pose_dev);
     pcp::event_put(icp->owner, icp->ev0);
     pcp::event_put(icp->owner, icp->ev1);
@@ -2975,30 +2143,6 @@ int pcp_icp_step(pcp_ctx* ctx, pcp_icp* icp, const double T[16], float rmax, dou
         (void)hipEventElapsedTime(&mv, icp->ev0, icp->ev_ver);
         std::fprintf(stderr, "[pcp icp dbg=%d] verify %.4f ms  octant %.4f ms  fallback %.4f ms  searched %u  "
                      "n_fallback %u\n", icp->dbg, mv, m1 - mv, ms - m1, nsv, icp->last_fallback);
-        if (icp->dbgcnt && icp->engine_tile && icp->bstart) {
-            unsigned long long c[32];
-            PCP_HIP(ctx, hipMemcpy(c, icp->dbgcnt, sizeof(c), hipMemcpyDeviceToHost));
-            std::fprintf(stderr, "[pcp icp tile] bricks %llu whole %llu | rounds staged alone %llu failed %llu | settled octant %llu "
-                         "3x3x3 %llu | fallback staged %llu unstaged %llu outside %llu | no-corr outside %llu | "
-                         "points/staging %.1f rows/staging %.1f stagings %llu | octant trip/wave %.1f waves %llu\n",
-                         c[0], c[1], c[2], c[3], c[24], c[25], c[26], c[27], c[28], c[29], (double)c[10] / (double)(c[11] ? c[11] : 1),
-                         (double)c[14] / (double)(c[11] ? c[11] : 1), c[11], (double)c[12] / (double)(c[13] ? c[13] : 1), c[13]);
-        } else if (icp->dbgcnt) {
-            unsigned long long c[32];
-            PCP_HIP(ctx, hipMemcpy(c, icp->dbgcnt, sizeof(c), hipMemcpyDeviceToHost));
-            std::fprintf(stderr, "[pcp icp dbg] octant candidates/query %.2f  wave max list/chunk %.2f  chunks %llu (compare-swap %llu)  "
-                         "chunk max-list histogram <32,<64,<128,<256,<512,<1k,<2k,>=2k: %llu %llu %llu %llu %llu %llu %llu %llu\n",
-                         (double)c[0] / (double)(c[2] ? c[2] : 1), (double)c[1] / (double)(c[4] ? c[4] : 1), c[4], c[3],
-                         c[8], c[9], c[10], c[11], c[12], c[13], c[14], c[15]);
-            std::fprintf(stderr, "[pcp icp dbg] fallback: settled by the 3x3x3 stage %llu, with a correspondence %llu\n",
-                         c[5], c[6]);
-            std::fprintf(stderr, "[pcp icp dbg] freeze model: chunks %llu skippable %llu (searched lanes in them %llu) "
-                         "refrozen with slack>0 %llu\n", c[18], c[16], c[17], c[19]);
-            std::fprintf(stderr, "[pcp icp dbg] verify: one-gather tier would settle %llu of the settled\n", c[31]);
-            std::fprintf(stderr, "[pcp icp dbg] verify: settled %llu  searched: aged %llu  fallback-reset(D=0) %llu  "
-                         "d_win/D <.5 %llu <.75 %llu <1 %llu >=1 %llu | delta/D <.1 %llu <.25 %llu <.5 %llu >=.5 %llu\n",
-                         c[20], c[21], c[22], c[23], c[24], c[25], c[26], c[27], c[28], c[29], c[30]);
-        }
     }
     return PCP_OK;
 }

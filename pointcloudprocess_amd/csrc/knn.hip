@@ -1556,11 +1556,6 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* ix, const double* q, size_t qstride, 
     }
 #undef LAUNCH_KNN
     PCP_LAUNCH_CHECK(ctx);
-    if (getenv("PCP_KNN_DEBUG")) {
-        uint32_t c = 0;
-        hipMemcpy(&c, fb.f.count, 4, hipMemcpyDeviceToHost);
-        fprintf(stderr, "pcp_knn: k=%d nq=%lld deferred to the far pass: %u\n", k, (long long)nq, c);
-    }
     return PCP_OK;
 }
 
@@ -1639,14 +1634,9 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
     const double4* pts = (const double4*)ix->pts;
     FarBuf fb;
     PCP_TRY(fb.alloc(ctx, ix->n));
-    const char* tenv = getenv("PCP_NORMALS_TILE");
-    const int tile_R = tenv ? atoi(tenv) : (kk <= 8 ? 1 : 2);  // 0 disables the tiled kernel
-    if (ix->g.dense && tile_R > 0) {
-        unsigned long long* st = nullptr;
-        if (getenv("PCP_KNN_DEBUG")) {
-            PCP_TRY(dmalloc(ctx, &st, 32));
-            PCP_HIP(ctx, hipMemsetAsync(st, 0, 32 * sizeof(unsigned long long), ctx->stream));
-        }
+    const int tile_R = kk <= 8 ? 1 : 2;  // the tile's window half-width in cells
+    if (ix->g.dense) {
+        unsigned long long* st = nullptr;  // (per-phase counters of profiling builds)
         const unsigned nbt = (unsigned)std::min<int64_t>((ix->n + 63) / 64, 1 << 20);
         // brick order of the queries: (brick key, sorted position) radix-sorted
         uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *order = nullptr;
@@ -1678,12 +1668,10 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         FarBuf fb2;  // the near pass's own deferred queries
         PCP_TRY(fb2.alloc(ctx, ix->n));
         // the tile's uncertified queries: the lane-per-query near pass (cell rings), its own
-        // deferrals then the wave-per-query pass; or (PCP_NORMALS_NEAR=0) all of them straight
-        // to the wave-per-query pass -- a few thousand queries fill few waves one lane each
-        const char* nenv = getenv("PCP_NORMALS_NEAR");
-        const bool near_pass = nenv ? atoi(nenv) != 0 : PCP_NORMALS_NEAR_DEFAULT;
-        const char* lenv = getenv("PCP_TILE_LANE");  // A/B: 0 = every lane scans the union box
-        const int lane_mode = lenv ? atoi(lenv) : PCP_TILE_LANE_DEFAULT;
+        // deferrals then the wave-per-query pass (PCP_NORMALS_NEAR_DEFAULT; 0: all of them straight
+        // to the wave-per-query pass, measured slower)
+        const bool near_pass = PCP_NORMALS_NEAR_DEFAULT;
+        const int lane_mode = PCP_TILE_LANE_DEFAULT;  // 0: every lane scans the union box (slower)
 #define LAUNCH_TILE(KV)                                                                                          \
         hipLaunchKernelGGL((k_normals_tile<KV>), dim3(nbt), dim3(64), 0, ctx->stream, ix->g, pts, ix->mapping,      \
                            ix->identity, ix->n, kk, tile_R, mc, out, n_out, fb.f, st, order, lane_mode);          \
@@ -1702,39 +1690,6 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         }
 #undef LAUNCH_TILE
         PCP_LAUNCH_CHECK(ctx);
-        if (st) {
-            unsigned long long h[4] = {0, 0, 0, 0};
-            unsigned c = 0;
-            hipMemcpy(h, st, sizeof(h), hipMemcpyDeviceToHost);
-            hipMemcpy(&c, fb.f.count, 4, hipMemcpyDeviceToHost);
-            unsigned c2 = 0;
-            hipMemcpy(&c2, fb2.f.count, 4, hipMemcpyDeviceToHost);
-            fprintf(stderr, "pcp_normals_knn tile: the near pass deferred %u to the brick search\n", c2);
-            unsigned long long cd[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-            hipMemcpy(cd, st + 4, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-            double qd[4];
-            hipMemcpy(qd, st + 9, sizeof(qd), hipMemcpyDeviceToHost);
-            unsigned long long ph[2] = {0, 0};
-            hipMemcpy(ph, st + 13, sizeof(ph), hipMemcpyDeviceToHost);
-            unsigned long long sl[5] = {0, 0, 0, 0, 0};
-            hipMemcpy(sl, st + 15, sizeof(sl), hipMemcpyDeviceToHost);
-            fprintf(stderr, "pcp_normals_knn coop: the slowest query's cycles: ring phase %llu, shells' exact k-th %llu, "
-                    "brick occupancy %llu, rows and points %llu, mid-shell bounds %llu\n", sl[0], sl[1], sl[2], sl[3], sl[4]);
-            fprintf(stderr, "pcp_normals_knn coop: cycles per query: ring phase %.0f, global_kth in shells %.0f\n",
-                    cd[0] ? (double)ph[0] / cd[0] : 0.0, cd[0] ? (double)ph[1] / cd[0] : 0.0);
-            fprintf(stderr, "pcp_normals_knn coop: the slowest query at (%.3f, %.3f, %.3f), last k-th d2 %.4f; grid o (%.2f %.2f %.2f) h %.4f n %d %d %d\n",
-                    qd[0], qd[1], qd[2], qd[3], ix->g.o[0], ix->g.o[1], ix->g.o[2], ix->g.h, ix->g.n[0], ix->g.n[1], ix->g.n[2]);
-            fprintf(stderr, "pcp_normals_knn coop: queries %llu, brick shells mean %.2f max %llu, cycles mean %.0f max %llu\n",
-                    cd[0], cd[0] ? (double)cd[1] / cd[0] : 0.0, cd[2], cd[0] ? (double)cd[3] / cd[0] : 0.0, cd[4]);
-            fprintf(stderr, "pcp_normals_knn tile: k=%d R=%d n=%lld uncertified lanes: by the list bound %llu, by the "
-                    "box %llu; oversized-wave lanes: rows %llu, points %llu; deferred %u\n", k, tile_R,
-                    (long long)ix->n, h[0], h[2], h[1], h[3], c);
-            unsigned long long lp[2] = {0, 0};
-            hipMemcpy(lp, st + 20, sizeof(lp), hipMemcpyDeviceToHost);
-            fprintf(stderr, "pcp_normals_knn tile: groups scanned by lane windows %llu, by the union box %llu\n", lp[0],
-                    lp[1]);
-            dfree(ctx, st);
-        }
         return PCP_OK;
     }
 #define LAUNCH_NRM(KV)                                                                                              \

@@ -44,25 +44,29 @@ constexpr int kBlock = 64 * kWaves;
 #ifndef PCP_BF_UNROLL  // sub-tile steps per unrolled loop body
 #define PCP_BF_UNROLL 4
 #endif
-#ifndef PCP_BF_SIGN  // 1: thresholds in the MFMA's C operand, sign-bit hit test; 0: compares
-#define PCP_BF_SIGN 1
-#endif
-#ifndef PCP_BF_GLDS  // 1: target tiles staged by LDS-DMA into two LDS buffers; 0: through registers
-#define PCP_BF_GLDS 1
-#endif
-#ifndef PCP_BF_GROUP  // sub-tiles per hit test (1: every step)
-#define PCP_BF_GROUP 1
-#endif
 constexpr int kTile = PCP_BF_TILE;     // targets staged in LDS per step
+constexpr int kBfUnroll = PCP_BF_UNROLL;
+// s_waitcnt immediate for vmcnt(0) with expcnt / lgkmcnt left at their maxima (gfx9 encoding:
+// vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int kWaitVm0 = 0x0F70;
 constexpr int kPerThread = kTile / kBlock;
 
 __device__ __forceinline__ const double* dptr(const double* base, size_t stride, int64_t i) {
     return (const double*)((const char*)base + (size_t)i * stride);
 }
 
-// targets -> float4 {x, y, z, |p|^2}; non-finite -> |p|^2 = +inf (never ranked).  Per-block
-// max of |p|^2 (fp64) and finite count for the host.
-__global__ __launch_bounds__(256) void k_bf_targets(const double* t, size_t stride, int64_t n, float4* t4,
+// targets -> {x, y, z, |p|^2} in k-major groups of 16 (group g = targets 16g..16g+15 as x[16],
+// y[16], z[16], |p|^2[16]: the B fragment of a 16-target sub-tile, read by lane l as word
+// 16 (l >> 4) + (l & 15), is 64 consecutive LDS words, no bank conflicts); non-finite ->
+// |p|^2 = +inf (never ranked).  Per-block max of |p|^2 (fp64) and finite count for the host.
+__device__ __forceinline__ void bf_put(float* t4, int64_t i, float4 v) {
+    float* g = t4 + (i >> 4) * 64 + (i & 15);
+    g[0] = v.x;
+    g[16] = v.y;
+    g[32] = v.z;
+    g[48] = v.w;
+}
+__global__ __launch_bounds__(256) void k_bf_targets(const double* t, size_t stride, int64_t n, float* t4,
                                                     double* part) {
     double pmax = 0.0, cnt = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -77,7 +81,7 @@ __global__ __launch_bounds__(256) void k_bf_targets(const double* t, size_t stri
         } else {
             v.x = 0.f; v.y = 0.f; v.z = 0.f; v.w = INFINITY;
         }
-        t4[i] = v;
+        bf_put(t4, i, v);
     }
     for (int o = 32; o > 0; o >>= 1) {
         pmax = fmax(pmax, __shfl_xor(pmax, o, 64));
@@ -94,13 +98,13 @@ __global__ __launch_bounds__(256) void k_bf_targets(const double* t, size_t stri
     }
 }
 
-// the padding of the last target tile: never ranked (|p|^2 = +inf)
-__global__ void k_bf_pad(float4* t4, int64_t n) {
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) t4[i] = make_float4(0.f, 0.f, 0.f, INFINITY);
+// the padding [from, to) of the last target tile: never ranked (|p|^2 = +inf)
+__global__ void k_bf_pad(float* t4, int64_t from, int64_t to) {
+    for (int64_t i = from + threadIdx.x; i < to; i += blockDim.x) bf_put(t4, i, make_float4(0.f, 0.f, 0.f, INFINITY));
 }
 
 struct BfArgs {
-    const float4* t4;
+    const float* t4;   // k-major groups of 16 targets (k_bf_targets)
     const double* t;
     size_t tstride;
     int64_t nt;
@@ -140,11 +144,7 @@ __device__ __forceinline__ void group_min(double& d, int& j) {
 // QB blocks of 16 queries per wave; L = per-(row, class) list length.
 template <int L, int QB, int W>
 __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
-#if PCP_BF_GLDS
-    __shared__ float4 tiles[2][kTile];  // LDS-DMA double buffer (no staging registers)
-#else
-    __shared__ float4 tile[kTile];
-#endif
+    __shared__ float tiles[2][4 * kTile];  // LDS-DMA double buffer of k-major target groups
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int cls = lane & 15, grp = lane >> 4;
@@ -181,7 +181,6 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
 #pragma unroll
             for (int i = 0; i < L; i++) { ls[b][r][i] = INFINITY; lt[b][r][i] = -1; }
         }
-#if PCP_BF_SIGN
     // The filter rides in the MFMA: C = -thr per row, so an output is negative exactly when the
     // score is below the row's threshold (as of the MFMA's issue; thresholds only fall, so a
     // stale one lets more through), and the common path's hit test is two ORs of the sign bits
@@ -207,7 +206,6 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
             }
         }
     }
-#endif
     // wave-uniform fp32 score error bound E (largest |q| of the wave's queries)
     float ew;
     {
@@ -227,144 +225,54 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
     const bool use_theta = a.kk <= 16;
 
     const int64_t ntiles = (a.nt + kTile - 1) / kTile;
-#if PCP_BF_GLDS
     // global -> LDS directly (global_load_lds_dwordx4: wave-uniform LDS base + lane * 16 B), one
     // tile ahead into the other buffer; the target array is padded to whole tiles with
     // never-ranked records, so every lane's source address is valid
     auto fetch = [&](int64_t tb, int buf) {
 #pragma unroll
         for (int u = 0; u < kPerThread; u++) {
-            const float4* src = a.t4 + tb + u * kBlock + threadIdx.x;
+            const float* src = a.t4 + (tb + u * kBlock + threadIdx.x) * 4;  // 16 B per thread, in layout order
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)(&tiles[buf][u * kBlock] +
-                                                                                       (threadIdx.x & ~63u)),
+                                             (__attribute__((address_space(3))) void*)(&tiles[buf][(u * kBlock) * 4] +
+                                                                                       (threadIdx.x & ~63u) * 4),
                                              16, 0, 0);
         }
     };
     fetch(0, 0);
     for (int64_t tt = 0; tt < ntiles; tt++) {
-        __syncthreads();  // tile tt has landed (vmcnt(0)); every wave is done with tile tt - 1
+        // tile tt has landed: this wave's LDS-DMA loads are complete (an explicit vmcnt(0): a
+        // workgroup barrier's release fence waits only on lgkmcnt on gfx9), then every wave's are,
+        // and every wave is done with tile tt - 1
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        __syncthreads();
         if (tt + 1 < ntiles) fetch((tt + 1) * kTile, (int)((tt + 1) & 1));
-        float4* const tile = tiles[tt & 1];
-#else
-    float4 pre[kPerThread];
-    auto fetch = [&](int64_t tb) {
-#pragma unroll
-        for (int u = 0; u < kPerThread; u++) {
-            const int64_t ti = tb + u * kBlock + threadIdx.x;
-            pre[u] = ti < a.nt ? a.t4[ti] : make_float4(0.f, 0.f, 0.f, INFINITY);
-        }
-    };
-    fetch(0);
-    for (int64_t tt = 0; tt < ntiles; tt++) {
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kPerThread; u++) tile[u * kBlock + threadIdx.x] = pre[u];
-        __syncthreads();
-        if (tt + 1 < ntiles) fetch((tt + 1) * kTile);
-#endif
+        const float* const tf = tiles[tt & 1];
         const int tb = (int)(tt * kTile);
-        const float* tf = (const float*)tile;
-#if !PCP_BF_SIGN
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#endif
+        // B fragment of sub-tile s: word 64 s + 16 grp + cls (k-major group: conflict-free)
+        auto bfrag_at = [&](int sub) { return tf[sub * 64 + grp * 16 + cls]; };
         // software pipeline: the MFMAs of sub-tile s+1 are in flight while the scores of
         // sub-tile s are tested, so the matrix pipe never waits on the selection VALU work
         f32x4 cn[QB];
         float bnext;  // B fragment of sub-tile s+2, read from LDS a step ahead of its MFMA
-#if PCP_BF_SIGN
-#define PCP_BF_C(b) nthr[b]
-#else
-#define PCP_BF_C(b) z
-#endif
         {
-            const float bf0 = tf[cls * 4 + grp];
-            bnext = tf[(16 + cls) * 4 + grp];
+            const float bf0 = bfrag_at(0);
+            bnext = bfrag_at(1);
 #pragma unroll
-            for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf0, PCP_BF_C(b), 0, 0, 0);
+            for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf0, nthr[b], 0, 0, 0);
         }
-#if PCP_BF_SIGN && PCP_BF_GROUP > 1
-        // the hit test once per PCP_BF_GROUP sub-tiles, software-pipelined by whole groups: the
-        // next group's MFMAs are issued (independent: C = -thr, no accumulation) before this
-        // group's 4 x SG outputs are OR-ed into one sign word (v_or3_b32), so no test waits on an
-        // MFMA issued just before it; only a group with a hit walks its sub-tiles one by one
-        constexpr int SG = PCP_BF_GROUP;
-        constexpr int NSUB = kTile / 16;
-        static_assert(NSUB % SG == 0, "sub-tiles per group");
-        // B fragments two groups ahead: the LDS reads of group g + 2 are issued while group g is
-        // tested, so the MFMAs of group g + 1 never wait on a read issued just before them
-        f32x4 gn[SG][QB];
-        float bq[SG];
-#pragma unroll
-        for (int u = 0; u < SG; u++) {
-            const float bfr = tf[(u * 16 + cls) * 4 + grp];
-            bq[u] = tf[((SG + u) * 16 + cls) * 4 + grp];
-#pragma unroll
-            for (int b = 0; b < QB; b++) gn[u][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfr, nthr[b], 0, 0, 0);
-        }
-        for (int sub0 = 0; sub0 < NSUB; sub0 += SG) {
-            f32x4 cg[SG][QB];
-#pragma unroll
-            for (int u = 0; u < SG; u++)
-#pragma unroll
-                for (int b = 0; b < QB; b++) cg[u][b] = gn[u][b];
-            if (sub0 + SG < NSUB) {
-#pragma unroll
-                for (int u = 0; u < SG; u++) {
-                    const float bfr = bq[u];
-#pragma unroll
-                    for (int b = 0; b < QB; b++)
-                        gn[u][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfr, nthr[b], 0, 0, 0);
-                }
-                if (sub0 + 2 * SG < NSUB) {
-#pragma unroll
-                    for (int u = 0; u < SG; u++) bq[u] = tf[((sub0 + 2 * SG + u) * 16 + cls) * 4 + grp];
-                }
-            }
-            uint32_t sg = 0;
-#pragma unroll
-            for (int u = 0; u < SG; u++)
-#pragma unroll
-                for (int b = 0; b < QB; b++)
-                    sg |= __float_as_uint(cg[u][b][0]) | __float_as_uint(cg[u][b][1]) | __float_as_uint(cg[u][b][2]) |
-                          __float_as_uint(cg[u][b][3]);
-            if ((int32_t)sg < 0) {
-#pragma unroll
-                for (int u = 0; u < SG; u++) {
-                    const int sub = sub0 + u;
-                    const int tidx = tb + sub * 16 + cls;
-                    const float4 p = tile[sub * 16 + cls];
-#pragma unroll
-                    for (int b = 0; b < QB; b++)
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            if ((int32_t)__float_as_uint(cg[u][b][r]) >= 0) continue;
-                            const float x = __fmaf_rn(qm[b][r][2], p.z, __fmaf_rn(qm[b][r][1], p.y,
-                                                      __fmaf_rn(qm[b][r][0], p.x, p.w)));
-                            if (x < thr[b][r]) {
-                                list_insert<L>(ls[b][r], lt[b][r], x, tidx);
-                                thr[b][r] = fminf(ls[b][r][L - 1], thr[b][r]);
-                                nthr[b][r] = -thr[b][r];
-                            }
-                        }
-                }
-            }
-        }
-#else
-#pragma unroll PCP_BF_UNROLL
+#pragma unroll kBfUnroll
         for (int sub = 0; sub < kTile / 16; sub++) {
             f32x4 c[QB];
 #pragma unroll
             for (int b = 0; b < QB; b++) c[b] = cn[b];
             if (sub + 1 < kTile / 16) {
                 const float bfrag = bnext;
-                if (sub + 2 < kTile / 16) bnext = tf[((sub + 2) * 16 + cls) * 4 + grp];
+                if (sub + 2 < kTile / 16) bnext = bfrag_at(sub + 2);
 #pragma unroll
                 for (int b = 0; b < QB; b++)
-                    cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfrag, PCP_BF_C(b), 0, 0, 0);
+                    cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfrag, nthr[b], 0, 0, 0);
             }
             // one combined test per step; the insertion path runs only when a lane has a hit
-#if PCP_BF_SIGN
             uint32_t sg = 0;
 #pragma unroll
             for (int b = 0; b < QB; b++)
@@ -372,7 +280,8 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
                       __float_as_uint(c[b][3]);
             if ((int32_t)sg < 0) {
                 const int tidx = tb + sub * 16 + cls;
-                const float4 p = tile[sub * 16 + cls];
+                const float* g = tf + sub * 64 + cls;
+                const float4 p = make_float4(g[0], g[16], g[32], g[48]);
 #pragma unroll
                 for (int b = 0; b < QB; b++)
 #pragma unroll
@@ -387,29 +296,7 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
                         }
                     }
             }
-#else
-            bool hit = false;
-#pragma unroll
-            for (int b = 0; b < QB; b++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) hit |= c[b][r] < thr[b][r];
-            if (hit) {
-                const int tidx = tb + sub * 16 + cls;
-#pragma unroll
-                for (int b = 0; b < QB; b++)
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const float x = c[b][r];
-                        if (x < thr[b][r]) {
-                            list_insert<L>(ls[b][r], lt[b][r], x, tidx);
-                            thr[b][r] = fminf(ls[b][r][L - 1], thr[b][r]);
-                        }
-                    }
-            }
-#endif
         }
-#endif
-#undef PCP_BF_C
         // refresh theta after tiles 1, 2, 4, 8, ... (rank of each class best in its group)
         if (use_theta && ((tt + 1) & tt) == 0) {
 #pragma unroll
@@ -428,9 +315,7 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
                     for (int o = 1; o < 16; o <<= 1) cand = fminf(cand, __shfl_xor(cand, o, 64));
                     const float t2 = cand + 2.f * ew;
                     if (cand != INFINITY) thr[b][r] = fminf(thr[b][r], t2 + fabsf(t2) * 1e-6f);
-#if PCP_BF_SIGN
                     nthr[b][r] = -thr[b][r];
-#endif
                 }
         }
     }
@@ -571,13 +456,13 @@ int pcp_knn_bruteforce(pcp_ctx* ctx, const double* t, size_t tstride, int64_t nt
     if (nq == 0) return PCP_OK;
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    float4* t4 = nullptr;
+    float* t4 = nullptr;
     double* part = nullptr;
     int32_t* fb = nullptr;
     uint32_t* fbc = nullptr;
     const unsigned npb = grid_for(nt > 0 ? nt : 1, 256, 1024);
     const int64_t ntpad = std::max<int64_t>((nt + kTile - 1) / kTile * kTile, 1);  // whole tiles (LDS-DMA)
-    int rc = dmalloc(ctx, &t4, ntpad);
+    int rc = dmalloc(ctx, &t4, 4 * (size_t)ntpad);
     if (!rc) rc = dmalloc(ctx, &part, 2 * (size_t)npb);
     if (!rc) rc = dmalloc(ctx, &fb, nq);
     if (!rc) rc = dmalloc(ctx, &fbc, 1);
@@ -585,7 +470,7 @@ int pcp_knn_bruteforce(pcp_ctx* ctx, const double* t, size_t tstride, int64_t nt
     if (!rc && nt > 0) {
         hipLaunchKernelGGL(k_bf_targets, dim3(npb), dim3(256), 0, st, t, tstride, nt, t4, part);
         if (ntpad > nt)
-            hipLaunchKernelGGL(k_bf_pad, dim3(1), dim3(256), 0, st, t4 + nt, ntpad - nt);
+            hipLaunchKernelGGL(k_bf_pad, dim3(1), dim3(256), 0, st, t4, nt, ntpad);
         std::vector<double> h(2 * npb);
         hipError_t e = hipMemcpyAsync(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -600,8 +485,8 @@ int pcp_knn_bruteforce(pcp_ctx* ctx, const double* t, size_t tstride, int64_t nt
         a.kk = (int)std::min<double>((double)k, nfin);
         // 32 unit roundoffs of (|p| + |q|)^2: casts to fp32, |p|^2 in fp32 and the 4-term
         // fma chain each contribute a few
-        // (PCP_BF_SIGN: 8 more for the threshold subtraction inside the filter's MFMA)
-        a.E2 = (PCP_BF_SIGN ? 40.0 : 32.0) * std::ldexp(1.0, -24);
+        // (and 8 more for the threshold subtraction inside the filter's MFMA)
+        a.E2 = 40.0 * std::ldexp(1.0, -24);
         a.pmax = std::sqrt(pmax2);
         a.oidx = oidx; a.od2 = od2; a.fb = fb; a.fb_count = fbc;
         if (hipMemsetAsync(fbc, 0, sizeof(uint32_t), st) != hipSuccess) rc = set_error(ctx, PCP_ERR_HIP, "memset");

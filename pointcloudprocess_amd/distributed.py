@@ -242,8 +242,13 @@ class GpuEngine:
 
     def __init__(self, ctx, target_xyz, query_xyz, cell_size=0.0):
         self.target = target_xyz.contiguous()
-        self.index = ops.GridIndex(ctx, self.target, cell_size=cell_size)
-        self.icp = ops.ICP(self.index, query_xyz.contiguous())
+        # the index build and the query sort in one call (their radix sorts overlap on two streams)
+        if hasattr(ctx.lib, "pcp_icp_create_with_target"):
+            self.icp = ops.ICP.with_target(ctx, self.target, query_xyz.contiguous(), cell_size)
+            self.index = self.icp.index
+        else:  # (an A/B build of an older tree, PCP_LIB)
+            self.index = ops.GridIndex(ctx, self.target, cell_size=cell_size)
+            self.icp = ops.ICP(self.index, query_xyz.contiguous())
         self.device = ctx.device
         self.nq = query_xyz.shape[0]
 
@@ -293,6 +298,22 @@ def radius_slab_split(x, world, rank, r):
     x = np.asarray(x)
     own = np.nonzero((x >= lo) & (x < hi))[0]
     halo = np.nonzero(((x >= lo - r) & (x < lo)) | ((x >= hi) & (x < hi + r)))[0]
+    return own, halo
+
+
+def radius_slab_split_dev(x, world, rank, r):
+    """radius_slab_split on a device tensor of x-coordinates (the C5 bench's 200M-point cloud
+    stays in HBM): the same equal-count bounds (sorted x at n * k / world, as slab_bounds, in the
+    values' own precision) and the same owned / halo sets, as int64 index tensors in ascending
+    order."""
+    n = x.numel()
+    xs = torch.sort(x.double()).values
+    b = [-math.inf] + [float(xs[(n * k) // world]) if n else 0.0 for k in range(1, world)] + [math.inf]
+    del xs
+    lo, hi = b[rank], b[rank + 1]
+    xd = x.double()
+    own = torch.nonzero((xd >= lo) & (xd < hi)).flatten()
+    halo = torch.nonzero(((xd >= lo - r) & (xd < lo)) | ((xd >= hi) & (xd < hi + r))).flatten()
     return own, halo
 
 

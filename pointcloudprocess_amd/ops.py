@@ -311,16 +311,40 @@ def normals_rpca(ctx, xyz, knn_idx, pr=0.99, epi=0.5, seed=0):
 class ICP:
     """Device-resident ICP of a query set against an fp32 grid index (the target)."""
 
-    def __init__(self, target_index, q):
+    def __init__(self, target_index, q, _handle=None):
         self.index = target_index
         self.ctx = ctx = target_index.ctx
         self.q = q
         h = C.c_void_p()
-        ctx.check(ctx.lib.pcp_icp_create(ctx.h, target_index.h, _ptr(q), q.stride(0) * q.element_size(),
-                                         q.shape[0], C.byref(h)))
+        if _handle is None:
+            ctx.check(ctx.lib.pcp_icp_create(ctx.h, target_index.h, _ptr(q), q.stride(0) * q.element_size(),
+                                             q.shape[0], C.byref(h)))
+        else:
+            h = _handle
         self.h = h
         self.nq_in = q.shape[0]
         self.acc = torch.zeros(24, dtype=torch.float64, device=ctx.device)
+
+    @classmethod
+    def with_target(cls, ctx, target, q, cell_size):
+        """The fp32 index of `target` and the ICP handle of `q` in one call
+        (pcp_icp_create_with_target: the two pre-iteration sorts overlap).  Returns the ICP; its
+        .index is the GridIndex (close the ICP, then the index)."""
+        hi, hq = C.c_void_p(), C.c_void_p()
+        ctx.check(ctx.lib.pcp_icp_create_with_target(ctx.h, _ptr(target), target.stride(0) * target.element_size(),
+                                                     target.shape[0], float(cell_size), _ptr(q),
+                                                     q.stride(0) * q.element_size(), q.shape[0], C.byref(hi),
+                                                     C.byref(hq)))
+        index = GridIndex.__new__(GridIndex)
+        index.ctx, index.src, index.h, index.f64, index.indices = ctx, target, hi, False, None
+        return cls(index, q, _handle=hq)
+
+    def set_options(self, oct_lanes_first=1, oct_lanes_list=0, ring_lanes=0, ablate=0):
+        """Test / profiling controls (pcp_icp_set_options): lanes per query of the octant pass
+        (first launch, later lists; 0 = by density) and of the fallback pass (0 = by length);
+        `ablate` switches passes off (results are then wrong)."""
+        self.ctx.check(self.ctx.lib.pcp_icp_set_options(self.h, int(oct_lanes_first), int(oct_lanes_list),
+                                                        int(ring_lanes), int(ablate)))
 
     def step(self, T, rmax, corr=False):
         """One iteration at pose T; returns the (device) accumulators (+ correspondences)."""

@@ -164,7 +164,7 @@ def test_frame_selection_walks():
         assert [f[0] for f in frames] == select_frames_reference(line, stamp_file, s, e, vc, 0.1), trial
 
 
-def mul_frame_reference(line, frames_xyz, map_cloud, start, end, valid_count, thr, sep, mul_seg):
+def mul_frame_reference(line, frames_xyz, map_cloud, start, end, valid_count, thr, sep, mul_seg, dense=True):
     """The same composition over the oracle: selection, concatenation, change_cloud_rgb,
     remove_duplicate(0.04), the map cache box (+-30 m) or get_grid_cloud(1.0), get_rot_icp
     (do_scale), and per frame the +-3 m box and a second get_rot_icp."""
@@ -173,7 +173,7 @@ def mul_frame_reference(line, frames_xyz, map_cloud, start, end, valid_count, th
     clouds = [ora.make_cloud(frames_xyz[st]) for st in sel]
     frame = np.concatenate(clouds)
     frame["rgba"] = 0x00FF0000
-    frame = ora.remove_duplicate(frame, 0.04)
+    frame = ora.remove_duplicate(frame, 0.04, is_dense=dense)
     g = ora.Grid()
     g.add_cloud(map_cloud)
     if not mul_seg:
@@ -233,5 +233,50 @@ def test_gpu_do_mul_frame_icp(tmp_path, sep, mul_seg):
     assert sorted(got) == sorted(finals) and len(finals) >= 5
     for st in finals:
         assert np.abs(got[st] - finals[st]).max() <= 1e-5 * np.abs(off).max(), st
+    grid.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_do_mul_frame_icp_plain_tensor_nan(tmp_path):
+    """do_mul_frame_icp with load_cloud returning plain, non-contiguous (n, 48) device tensors,
+    one of them holding a NaN point: the joint frame's is_dense comes from the data's finiteness
+    (False here), so remove_duplicate drops the NaN point as the reference's non-dense VoxelGrid
+    does (point_cloud.h:130-147, voxel_grid.h:880-943); pose within 1e-5 of the oracle composition."""
+    import torch
+    from pointcloudprocess_amd import cloudgrid, ops, pcd, synth
+    ctx = ops.Context(0)
+    T_true = synth.rigid(0.3, 0.1, -0.1, (0.06, -0.04, 0.02))
+    tgt, q = synth.icp_pair(60_000, 60_000, 91, 92, T_true, extent=(40.0, 40.0))
+    off = np.array([3512.25, -1801.5, 40.0])
+    map_cloud = ora.make_cloud(tgt.double().numpy() + off)
+    qx = q.double().numpy() + off
+    order = np.argsort(qx[:, 0], kind="stable")
+    nfr = 10
+    frames_xyz, stamp_file = {}, {}
+    for i in range(nfr):
+        st = 5000 + 10 * i
+        frames_xyz[st] = qx[order[i::nfr][: len(order) // nfr]].copy()
+        stamp_file[st] = st
+    frames_xyz[5050][7] = [np.nan, 1.0, 2.0]  # frame 5 (between start 4 and end 6) holds a NaN point
+
+    def load_cloud(st):  # a column slice of a wider tensor: (n, 48) uint8, not contiguous
+        rec = torch.from_numpy(ora.make_cloud(frames_xyz[st]).view(np.uint8).reshape(-1, 48).copy())
+        wide = torch.zeros((rec.shape[0], 96), dtype=torch.uint8)
+        wide[:, :48] = rec
+        view = wide.to(ctx.device)[:, :48]
+        assert not view.is_contiguous()
+        return view
+
+    errs = [0.05, 0.2, 0.05, 0.05, 0.0, 0.05, 0.3, 0.05, 0.05, 0.05]
+    line = [{"stamp": 5000 + 10 * i, "icperr": errs[i], "matrix": np.eye(4)} for i in range(nfr)]
+    grid = cloudgrid.CloudGrid(ctx)
+    grid.add_cloud_internal(ops.cloud_to_device(map_cloud, ctx.device))
+    dis, rot = callers.do_mul_frame_icp(ctx, line, stamp_file, 4, 6, grid, 2, 0.1, load_cloud=load_cloud)
+    sel, edis, erot, finals = mul_frame_reference(
+        [dict(e) for e in line], frames_xyz, map_cloud, 4, 6, 2, 0.1, False, False, dense=False)
+    assert 5050 in sel
+    assert dis > 0 and edis > 0 and abs(dis - edis) <= 1e-5
+    assert np.abs(rot - erot).max() <= 1e-5 * np.abs(off).max()
     grid.close()
     ctx.close()

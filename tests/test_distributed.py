@@ -152,3 +152,21 @@ def test_radius_slab_halo_two_ranks():
             e, _ = t.radius(xyz[own[k]], 0.2, cap=len(xyz))
             assert set(idx[offs[k]:offs[k + 1]].tolist()) == set(e.tolist())
     assert seen.all()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_radius_slab_split_dev_matches_host(world):
+    """The C5 bench's device split (distributed.radius_slab_split_dev, on a torch tensor) gives the
+    host split's owned / halo sets on every rank; the owned sets partition the cloud."""
+    import torch
+    from pointcloudprocess_amd import distributed as D
+    rng = np.random.default_rng(world)
+    x = rng.uniform(-30, 30, 20_000).astype(np.float32)
+    x[:500] = x[500:1000]  # ties at the bounds
+    seen = np.zeros(len(x), np.int64)
+    for rank in range(world):
+        own, halo = D.radius_slab_split(x, world, rank, 0.2)
+        od, hd = D.radius_slab_split_dev(torch.from_numpy(x), world, rank, 0.2)
+        assert np.array_equal(own, od.numpy()) and np.array_equal(halo, hd.numpy())
+        seen[own] += 1
+    assert (seen == 1).all()

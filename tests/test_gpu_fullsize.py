@@ -12,14 +12,13 @@ path":
   the centroids (calculate_feature.cpp:119-206 over kd_tree.h:814-845 neighbourhoods), every row
   against the oracle to the same 1e-6 tolerance as test_gpu_knn.py::test_normals_vs_oracle;
   the bit-identical row fraction is printed.
-* C5 (configs[4]): 25M points at the 200M-point scene's density (one eighth of it, the
-  per-GPU share at 8 GPUs), radius r = 0.2 over the fp16 cell-relative index; a seeded
-  1M-query sample is checked against the oracle's exact fp64 radiusSearch (kd_tree.h:863-903)
-  with the fp16 band: every row point is closer than r + eps, no row has
-  duplicates, and each row holds exactly as many points closer than r - eps as the oracle finds;
-  rows with no point inside the band have their F1 normals compared with the oracle's fp64 plane
-  of the (then identical) neighbour set (1 - |n.n_oracle| below 1e-6 at p99, 1e-5 at p99.99, 1e-4
-  for the worst-conditioned rows: fp32 accumulation, as the config states).
+* C5 (configs[4]): the bench's 200M-point scene, radius r = 0.2 over the fp16 cell-relative
+  index (~12.8e9 CSR entries, past 2^31): every row is checked on the device (no entry at or past
+  r + eps, its own point once); a 200K-query sample from 20 tiles against the oracle's exact fp64
+  radiusSearch (kd_tree.h:863-903) built on each tile +- 1 m, with the fp16 band:
+  no duplicates, as many points closer than r - eps as the oracle finds; rows with no point
+  inside the band have their F1 normals compared with the oracle's fp64 plane of the (then
+  identical) neighbour set, as an angle.
 """
 import math
 
@@ -80,55 +79,79 @@ def test_c3_fullsize_voxel_and_normals(ctx):
     assert np.all(diff <= 1e-6 * np.maximum(1.0, np.abs(ev)))
 
 
-def test_c5_fullsize_sampled_band(ctx):
+def test_c5_fullsize_200m(ctx):
+    """The C5 bench scene itself (bench_configs.cfg_c5, rank 0): 200M points, ~12.8e9 CSR entries
+    (past 2^31: 64-bit offsets and row positions).  Every row: offsets monotone, each row holds its
+    own point, no entry at or beyond r + eps from its query (exact fp64 distance on the fp32 input).
+    A 200K-query sample from 20 tiles of 4 x 4 m is band-checked against the oracle kd-tree built on
+    each tile +- 1 m, and the band-free rows' normals against the oracle's fp64 planes (as angles)."""
+    from h16_check import EPS, angle_summary, check_against_oracle
     from pointcloudprocess_amd import ops, synth
-    R, EPS = 0.2, 3e-4
-    n = 25_000_000
-    side = math.sqrt(n / 1.5e6) * 40.0                 # bench_configs.cfg_c5's density
+    R = 0.2
+    n = 200_000_000
+    side = math.sqrt(n / 1.5e6) * 40.0                 # bench_configs.cfg_c5's scene
     xyz = synth.street_scene(n, 5001, extent=(side, side), device=ctx.device)
     ix = ops.H16Index(ctx, xyz, cell_size=R)
     offs, idx, nrm = ix.radius_normals(R)
     ix.close()
-    assert int(offs[-1]) == idx.numel() and bool((offs[1:] - offs[:-1] >= 1).all())
-
-    s = torch.from_numpy(np.sort(np.random.default_rng(5201).choice(n, 1_000_000, replace=False))).to(ctx.device)
-    lens = offs[s + 1] - offs[s]
-    row_of = torch.repeat_interleave(torch.arange(s.numel(), device=ctx.device), lens)
-    pos = offs[s][row_of] + (torch.arange(row_of.numel(), device=ctx.device) - (torch.cumsum(lens, 0) - lens)[row_of])
-    rows = idx[pos].long()
-    x64 = xyz.double()
-    d = torch.linalg.norm(x64[rows] - x64[s][row_of], dim=1)
-    far = int((d >= R + EPS).sum())
-    dup = rows.numel() - torch.unique(row_of * n + rows).numel()
-    inner = torch.zeros(s.numel(), dtype=torch.int64, device=ctx.device).index_add_(0, row_of, (d < R - EPS).long())
-
-    xh = xyz.cpu().numpy().astype(np.float64)
-    tree = ora.KdTree(xh)
-    qs = s.cpu().numpy().astype(np.int32)
-    cnt_lo, _ = tree.radius_normals(qs, R - EPS)
-    cnt_hi, _ = tree.radius_normals(qs, R + EPS)
-    cnt_r, planes = tree.radius_normals(qs, R)
-    inner = inner.cpu().numpy()
-    missing = int((inner != cnt_lo).sum())
-    print(f"C5 {n} pts, 1M sampled rows, nbar {idx.numel() / n:.1f}: far {far}, duplicates {dup}, "
-          f"rows missing an inner point {missing}")
-    assert far == 0 and dup == 0 and missing == 0
-
-    # rows with nothing inside the band hold exactly the oracle's r-neighbourhood
-    lens_h = lens.cpu().numpy()
-    clean = (cnt_lo == cnt_hi) & (lens_h == cnt_r) & (cnt_r >= 10)
-    gp = nrm[s].cpu().numpy()
-    ep = np.stack([planes[f] for f in ("normal_x", "normal_y", "normal_z", "min_value", "curvature", "distance")], 1)
-    dots = np.abs((gp[clean, :3] * ep[clean, :3]).sum(1))
-    curv = np.abs(gp[clean, 4] - ep[clean, 4])
-    err = 1 - dots
-    worst = int(np.argmax(err))
-    print(f"C5 normals over {int(clean.sum())} band-free rows: 1-|dot| max {err.max():.3e} (curvature "
-          f"{ep[clean][worst, 4]:.3e}) p99 {np.percentile(err, 99):.3e} p99.99 {np.percentile(err, 99.99):.3e}; "
-          f"curvature err max {curv.max():.3e}")
-    assert clean.sum() > 500_000
-    # fp32 sums of fp16 offsets (the config's precision): the normal's error grows as the plane's
-    # two smallest eigenvalues approach each other (poles, edges), so the bound is on the tail,
-    # with a looser cap on the few worst-conditioned rows
-    assert np.percentile(err, 99) < 1e-6 and np.percentile(err, 99.99) < 1e-5 and err.max() < 1e-4
+    nnz = idx.numel()
+    lens = offs[1:] - offs[:-1]
+    print(f"C5 200M: nnz {nnz} (2^31 = {2 ** 31}), nbar {nnz / n:.1f}, max row {int(lens.max())}")
+    assert nnz > 2 ** 31 and int(offs[0]) == 0 and int(offs[-1]) == nnz and bool((lens >= 1).all())
+    # every row, in chunks of rows: nothing at or beyond r + eps; the query itself present
+    far = 0
+    self_missing = 0
+    chunk = 2_000_000
+    for r0 in range(0, n, chunk):
+        r1 = min(n, r0 + chunk)
+        e0, e1 = int(offs[r0]), int(offs[r1])
+        ent = idx[e0:e1].long()
+        row_of = torch.repeat_interleave(torch.arange(r0, r1, device=ctx.device), lens[r0:r1])
+        d2 = ((xyz[ent].double() - xyz[row_of].double()) ** 2).sum(1)
+        far += int((d2 >= (R + EPS) ** 2).sum())
+        has_self = torch.zeros(r1 - r0, dtype=torch.int32, device=ctx.device).index_add_(
+            0, row_of - r0, (ent == row_of).int())
+        self_missing += int((has_self != 1).sum())
+        del ent, row_of, d2, has_self
+    print(f"C5 200M every row: entries at >= r + eps {far}, rows without exactly one self entry {self_missing}")
+    assert far == 0 and self_missing == 0
+    # sampled rows against the oracle, tile by tile
+    rng = np.random.default_rng(5201)
+    tot, clean, angles, curv = 0, 0, [], []
+    for tile in range(20):
+        cx, cy = rng.uniform(-side / 2 + 5, side / 2 - 5, 2)
+        near = ((xyz[:, 0] - cx).abs() < 3.0) & ((xyz[:, 1] - cy).abs() < 3.0)
+        pts = torch.nonzero(near).flatten()                    # tile +- 1 m
+        inner = ((xyz[pts, 0] - cx).abs() < 2.0) & ((xyz[pts, 1] - cy).abs() < 2.0)
+        loc = torch.nonzero(inner).flatten()
+        if loc.numel() > 10_000:
+            loc = loc[torch.from_numpy(np.sort(rng.choice(loc.numel(), 10_000, replace=False))).to(ctx.device)]
+        tp = xyz[pts].double()
+        tree = ora.KdTree(tp.cpu().numpy())
+        # rows of the tile's queries: local point indices through the tile's inverse map
+        to_loc = torch.full((n,), -1, dtype=torch.int64, device=ctx.device)
+        to_loc[pts] = torch.arange(pts.numel(), device=ctx.device)
+        s_glob = pts[loc]
+        lens_s = lens[s_glob]
+        sub_offs = torch.cat([torch.zeros(1, dtype=torch.int64, device=ctx.device), torch.cumsum(lens_s, 0)])
+        row_of = torch.repeat_interleave(torch.arange(s_glob.numel(), device=ctx.device), lens_s)
+        pos = offs[s_glob][row_of] + (torch.arange(row_of.numel(), device=ctx.device) - sub_offs[:-1][row_of])
+        sub_idx = to_loc[idx[pos].long()]
+        assert bool((sub_idx >= 0).all())       # every neighbour lies inside the tile +- 1 m
+        nrm_loc = torch.zeros((pts.numel(), 6), dtype=nrm.dtype, device=ctx.device)
+        nrm_loc[loc] = nrm[s_glob]
+        res = check_against_oracle(tree, tp, sub_offs, sub_idx, loc, loc.cpu().numpy().astype(np.int32), R,
+                                   nrm=nrm_loc)
+        assert res["far"] == 0 and res["dup"] == 0 and res["missing"] == 0, (tile, {k: v for k, v in res.items()
+                                                                                   if np.isscalar(v)})
+        tot += res["rows"]
+        clean += res["clean"]
+        angles.append(res["angle"])
+        curv.append(res["curv_err"])
+        del to_loc
+    angles, curv = np.concatenate(angles), np.concatenate(curv)
+    print(f"C5 200M sampled: {tot} rows from 20 tiles, {clean} band-free: {angle_summary(angles)}; "
+          f"curvature err max {curv.max():.2e}")
+    assert tot > 150_000 and clean > 100_000
+    assert np.percentile(angles, 99) < 1.5e-3 and np.percentile(angles, 99.99) < 5e-3 and angles.max() < 2e-2
     assert curv.max() < 5e-4

@@ -58,17 +58,21 @@ def test_correspondence_bit_exact(ctx, cell):
         assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * scale)
 
 
-@pytest.mark.parametrize("engine", ["tile", "cache"])
-def test_registration_exact_every_iteration(ctx, engine, monkeypatch):
-    """Both engines over a registration: correspondences bit-exact and accumulators equal to the
-    oracle's direct sums at every iteration (the cached verify / octant / ring passes, the
-    default, and the opt-in LDS-tiled streaming search, PCP_ICP_ENGINE=tile)."""
-    monkeypatch.setenv("PCP_ICP_ENGINE", engine)
+@pytest.mark.parametrize("create", ["separate", "combined"])
+def test_registration_exact_every_iteration(ctx, create):
+    """A registration through both create paths (pcp_index_build_f32 + pcp_icp_create, and
+    pcp_icp_create_with_target, whose query sort runs on a second stream during the target's cell
+    sort): correspondences bit-exact and accumulators equal to the oracle's direct sums at every
+    iteration."""
     from pointcloudprocess_amd import ops, synth
     T_true = synth.rigid()
     tgt, q = _pair(250_000, 41, T_true)
-    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
-    icp = ops.ICP(index, q.to(ctx.device))
+    if create == "separate":
+        index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+        icp = ops.ICP(index, q.to(ctx.device))
+    else:
+        icp = ops.ICP.with_target(ctx, tgt.to(ctx.device), q.to(ctx.device), 0.1)
+        index = icp.index
     oi = ora.F32Index(tgt.numpy())
     T = np.eye(4)
     for it in range(10):
@@ -90,16 +94,15 @@ def test_registration_exact_every_iteration(ctx, engine, monkeypatch):
     index.close()
 
 
-def test_tile_engine_sparse_queries(ctx, monkeypatch):
-    """Few queries spread over many query bricks (nbk far above ceil(nq / 256)): the tile
-    engine's workgroups must stay inside the octant pass's partials region."""
+def test_sparse_queries_over_many_bricks(ctx):
+    """Few queries spread over a large target (query bricks far above ceil(nq / 256)), through
+    the combined create."""
     from pointcloudprocess_amd import ops, synth
-    monkeypatch.setenv("PCP_ICP_ENGINE", "tile")
     T_true = synth.rigid()
     tgt, _ = _pair(400_000, 43, T_true)
     q = synth.apply_inverse(synth.street_scene(5_000, 44, extent=(50.0, 50.0)), T_true)
-    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
-    icp = ops.ICP(index, q.to(ctx.device))
+    icp = ops.ICP.with_target(ctx, tgt.to(ctx.device), q.to(ctx.device), 0.1)
+    index = icp.index
     oi = ora.F32Index(tgt.numpy())
     for T in (np.eye(4), T_true):
         acc, ci, cd = icp.step(T, 0.25, corr=True)
@@ -115,11 +118,10 @@ def test_tile_engine_sparse_queries(ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("cell,per_cell", [(0.5, 40.0), (0.5, 1500.0)])
-def test_tile_engine_dense_cells(ctx, cell, per_cell, monkeypatch):
-    """Crowded cells: octant lists over 256 (the compare-swap top 3), bricks staged per 256-query
-    round, and (1500 per cell) boxes no round can hold, whose queries all take the exact fallback."""
+def test_dense_cells(ctx, cell, per_cell):
+    """Crowded cells: octant lists over 256 (the compare-swap top 3) and (1500 per cell) lists far
+    over it, against the oracle over two poses."""
     from pointcloudprocess_amd import ops
-    monkeypatch.setenv("PCP_ICP_ENGINE", "tile")
     rng = np.random.default_rng(7)
     side = 4.0 if per_cell > 100 else 10.0
     n = int(per_cell * (side / cell) ** 3)
@@ -147,11 +149,10 @@ def _small_motion():
     return synth.rigid(0.2, -0.1, 0.1, (0.03, -0.02, 0.01))
 
 
-def test_verify_pass_exact_over_registration(ctx, monkeypatch):
+def test_verify_pass_exact_over_registration(ctx):
     # The verify pass settles a query from its previous winner and lower bound (triangle
     # inequality); it must return exactly what an exhaustive search returns, at every
     # iteration of a registration, on a repeated pose, and after a jump back to the start.
-    monkeypatch.setenv("PCP_ICP_ENGINE", "cache")
     from pointcloudprocess_amd import ops, synth
     T_true = synth.rigid()
     tgt, q = _pair(200_000, 31, T_true)
@@ -397,13 +398,11 @@ def test_slab_guard_device(ctx):
 
 
 @pytest.mark.parametrize("gs", ["2,2", "4,4", "8,8", "1,0"])
-def test_octant_lane_groups_exact(ctx, gs, monkeypatch):
-    """G lanes per query in the octant pass (PCP_OCT_G="first,list"; 0 = by density): the
-    group merge, the per-group cache write and the > 256-candidate compare-swap path must give
-    the oracle's correspondences over a registration, on lattice ties and a dense cluster."""
+def test_octant_lane_groups_exact(ctx, gs):
+    """G lanes per query in the octant pass (pcp_icp_set_options "first,list"; 0 = by density):
+    the group merge, the per-group cache write and the > 256-candidate compare-swap path must
+    give the oracle's correspondences over a registration, on lattice ties and a dense cluster."""
     from pointcloudprocess_amd import ops, synth
-    monkeypatch.setenv("PCP_OCT_G", gs)
-    monkeypatch.setenv("PCP_ICP_ENGINE", "cache")
     T_true = synth.rigid()
     tgt, q = _pair(120_000, 51, T_true)
     rng = np.random.default_rng(52)
@@ -416,6 +415,8 @@ def test_octant_lane_groups_exact(ctx, gs, monkeypatch):
     q = torch.from_numpy(qn.astype(np.float32))
     index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
     icp = ops.ICP(index, q.to(ctx.device))
+    first, lst = (int(v) for v in gs.split(","))
+    icp.set_options(oct_lanes_first=first, oct_lanes_list=lst)
     oi = ora.F32Index(tgt.numpy())
     T = np.eye(4)
     for it in range(6):
@@ -431,14 +432,13 @@ def test_octant_lane_groups_exact(ctx, gs, monkeypatch):
 
 
 @pytest.mark.parametrize("lanes", ["1", "2", "4", "8"])
-def test_fallback_lane_groups_exact(ctx, lanes, monkeypatch):
-    """G lanes per query in the fallback pass (PCP_RING_LANES; the default picks G from the
+def test_fallback_lane_groups_exact(ctx, lanes):
+    """G lanes per query in the fallback pass (pcp_icp_set_options; the default picks G from the
     list length): the strided row scans, the per-plane group merge and box_search's group-bound
     row cuts must give the oracle's correspondences.  Cells of rmax / 2.5 over a sparse scan send many
     queries through box_search, including "nothing within rmax" boxes; lattice ties and a dense
     cluster exercise the (d2, index) order."""
     from pointcloudprocess_amd import ops, synth
-    monkeypatch.setenv("PCP_RING_LANES", lanes)
     T_true = synth.rigid()
     tgt, q = _pair(60_000, 61, T_true, extent=(30.0, 30.0))  # a dense cell table
     rng = np.random.default_rng(62)
@@ -452,6 +452,7 @@ def test_fallback_lane_groups_exact(ctx, lanes, monkeypatch):
     q = torch.from_numpy(qn.astype(np.float32))
     index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
     icp = ops.ICP(index, q.to(ctx.device))
+    icp.set_options(ring_lanes=int(lanes))
     oi = ora.F32Index(tgt.numpy())
     T = np.eye(4)
     fallbacks = 0

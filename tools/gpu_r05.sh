@@ -1,0 +1,49 @@
+# Round-5 GPU call wrapper: STEPS selects what runs (space separated), each step under its own
+# time limit, the first failure ends the call.
+#   h16tests   the C5 tests (tests/test_gpu_h16.py) and the 200M full-size C5 test
+#   icptests   the ICP tests and the 50M-scale C4 check
+#   bftests    the brute-force kNN tests and the 1M x 1M full-size C2 check
+#   c5ab       interleaved A/B of the C5 bench line: this tree vs variants/$VAR (PCP_LIB)
+#   c5trace    rocprofv3 kernel trace + stats of one C5 bench run
+#   tests      the whole GPU suite + smoke
+#   c4ab       interleaved A/B of the C4 bench line: this tree vs variants/$VAR
+#   c4trace    kernel trace of the C4 bench (per-iteration table)
+#   c2ab       interleaved A/B of the C2 bench line vs variants/$VAR
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/${TAG:-r05}; mkdir -p $O
+for st in ${STEPS}; do
+case $st in
+h16tests)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_h16.py "tests/test_gpu_fullsize.py::test_c5_fullsize_200m" -x -v -s --timeout 500 --timeout-method thread > $O/h16_tests.log 2>&1 ;;
+bftests)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_bruteforce.py "tests/test_gpu_fullsize.py::test_c2_fullsize_bit_exact" -x -v -s --timeout 500 --timeout-method thread > $O/bf_tests.log 2>&1 ;;
+icptests)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_icp.py tests/test_gpu_c4_scale.py -x -v -s --timeout 500 --timeout-method thread > $O/icp_tests.log 2>&1 ;;
+c5ab)
+  for rep in 1 2; do
+    timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_new.jsonl 2>> $O/c5_ab.err
+    PCP_LIB=variants/$VAR/libpcp.so timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_$VAR.jsonl 2>> $O/c5_ab.err
+  done ;;
+c5trace)
+  timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5trace -o run -- python3 bench.py --config C5 --no-cpu --steps 2 --warmup 1 > $O/c5trace.log 2>&1 ;;
+tests)
+  timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $O/gpu_tests.log 2>&1
+  timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
+c4ab)
+  for rep in 1 2 3; do
+    timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 >> $O/c4_ab_new.jsonl 2>> $O/c4_ab.err
+    PCP_LIB=variants/$VAR/libpcp.so timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 >> $O/c4_ab_$VAR.jsonl 2>> $O/c4_ab.err
+  done ;;
+c4trace)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4trace -o run -- python3 bench.py --no-cpu --steps 2 --warmup 1 > $O/c4trace.log 2>&1
+  python3 tools/trace_iters.py $O/c4trace > $O/per_iteration.txt 2>&1 || true ;;
+c2ab)
+  for rep in 1 2; do
+    timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_new.jsonl 2>> $O/c2_ab.err
+    PCP_LIB=variants/$VAR/libpcp.so timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_$VAR.jsonl 2>> $O/c2_ab.err
+  done ;;
+esac
+echo "step $st done" >> $O/steps.log
+done
+echo done

@@ -3,9 +3,11 @@
 
 FETCH_SIZE and WRITE_SIZE are in KB.  gfx950 correction (MI355X_MICROARCH.md, HBM section):
 FETCH_SIZE reports half the bytes of wide (16 B/lane) reads -> x2; WRITE_SIZE is exact.
-  python tools/pmc_summary.py [--src=h16.hip] <fetch_dir> <write_dir> [kernel-name ...]
+  python tools/pmc_summary.py [--src=h16.hip] [--key=name=value ...] <fetch_dir> <write_dir> [kernel-name ...]
 (the sha1 of the named csrc source is recorded, so a bench line only quotes counters measured on
-the kernels it runs)
+the kernels it runs; --key records the workload the counters were taken on -- e.g. --key=n=50000000
+--key=world=1 --key=mode=slab -- and a bench line quotes a record only when every key matches its
+own run)
 """
 import collections
 import csv
@@ -29,8 +31,14 @@ def per_kernel(path, counter):
 def main():
     args = sys.argv[1:]
     src_rel = "icp.hip"
-    if args and args[0].startswith("--src="):  # the source whose kernels are summarised (sha1 recorded)
-        src_rel = args.pop(0)[len("--src="):]
+    workload = {}
+    while args and args[0].startswith("--"):
+        a = args.pop(0)
+        if a.startswith("--src="):  # the source whose kernels are summarised (sha1 recorded)
+            src_rel = a[len("--src="):]
+        elif a.startswith("--key="):  # the workload the counters were measured on
+            k, v = a[len("--key="):].split("=", 1)
+            workload[k] = int(v) if v.lstrip("-").isdigit() else v
     fdir, wdir = args[0], args[1]
     keys = args[2:] or ["k_icp_verify", "k_icp_octant", "k_icp_ring"]
     f, w = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
@@ -48,6 +56,7 @@ def main():
         out["icp_hip_sha1"] = sha
     out["src"] = src_rel
     out["src_sha1"] = sha
+    out["workload"] = workload
     print(json.dumps(out, indent=1))
 
 
