@@ -272,6 +272,9 @@ int pcp_icp_create_with_target(pcp_ctx* ctx, const float* target_dev, size_t tar
 #define PCP_ICP_ABLATE_NO_ACCUM 4
 #define PCP_ICP_ABLATE_NO_FALLBACK 8
 #define PCP_ICP_ABLATE_NO_VERIFY 64
+/* not an ablation: keep 16-byte cache records although the target fits the 12-byte form
+ * (< 2^26 - 2 points); only before the handle's first launch.  Results are identical. */
+#define PCP_ICP_OPT_WIDE_CACHE 128
 int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, int ring_lanes, int ablate);
 int pcp_icp_destroy(pcp_icp* icp);
 /* One iteration at pose T (row-major 4x4 double, cast to fp32 for the kernel):

@@ -36,12 +36,14 @@ struct pcp_icp {
     int64_t nq_in = 0;            // queries passed to pcp_icp_create
     pcp::QXyz* q = nullptr;       // sorted queries, 12-byte xyz (the verify stream reads 12 B, not 16)
     int32_t* qidx = nullptr;      // their original indices (read only for caller-order outputs)
-    uint4* cand = nullptr;        // per sorted query: sorted-target positions of its 3 nearest targets at
-                                  // its last search (~0u = empty slot; the winner is always among them)
-                                  // and (float bits of D) & ~0xff | s, where s = the launch (mod 256) of
-                                  // that search and D a lower bound on the distance from the query, at
-                                  // that launch's pose, to every target NOT cached
-    float* pose_hist = nullptr;   // 256 x 12 floats: the pose of launch t at slot t & 255
+    uint32_t* cand = nullptr;     // per sorted query: its cache record (cache_load / cache_store): the
+                                  // sorted-target positions of its 3 nearest targets at its last search
+                                  // (the winner is always among them), the launch slot s of that search
+                                  // and D, a lower bound on the distance from the query, at that launch's
+                                  // pose, to every target NOT cached.  12 bytes when the target has fewer
+                                  // than 2^26 - 2 points (narrow), else 16
+    bool narrow = false;
+    float* pose_hist = nullptr;   // 256 x 12 floats: the pose of launch t at slot t & hist_mask
     int64_t launches = 0;         // correspondence launches so far (the first has nothing to verify)
     bool last_verified = false;   // the last launch ran the verify pass
     int32_t* sv = nullptr;        // verify pass: per-wave segments of uncertified queries (sv_seg each)
@@ -107,7 +109,11 @@ struct IcpArgs {
     float rho;          // octant half-width in cell units (0.5 - margin)
     float mc;           // cell-unit margin for pruning
     double* partials;
-    uint4* cand;
+    uint32_t* cand;     // cache records (cache_load / cache_store)
+    int narrow;         // 12-byte records
+    uint32_t hist_mask; // pose history slot of a launch: launch & hist_mask (63 narrow, 255 wide)
+    uint32_t max_age;   // older caches are searched again (so their slot is never reused)
+    float dunit, inv_dunit;  // narrow D code unit (cell size / 1024)
     const float* pose_hist;
     uint32_t launch;    // this launch's index (mod 2^32)
     uint32_t ntp;       // target points (tp[ntp] is the far sentinel)
@@ -569,16 +575,80 @@ struct LaneAcc {
 };
 
 // ---- candidate cache (a Verlet-style neighbour list per query)
-// The search that last settled query i left cand[i] = the positions of its kCache nearest
-// targets (or fewer) and D = the dlb word cand[i].w, a lower bound on the distance from the query, at the
-// previous launch's pose q_s, to every target point NOT in cand[i].  With q_t the query at the
+// The search that last settled query i left its record: the positions of its kCache nearest
+// targets (or fewer) and D, a lower bound on the distance from the query, at that launch's pose
+// q_s, to every target point NOT cached.  With q_t the query at the
 // current pose and Delta = |q_t - q_s|, every uncached point p has |q_t - p| >= D - Delta
 // (triangle inequality).  So if the nearest cached point is closer than D - Delta (with
 // relative margins far above the fp32 rounding of d2), it is the exact 1-NN under the
 // contract -- the same (d2, index) winner an exhaustive search returns, cached ties included
 // -- and the query is settled without a search; the bound moves to D - Delta.
-// kCache = 3: cand = {3 positions, dlb word} (one 16-byte record per query)
 constexpr int kCache = 3;
+
+// The record (per sorted query; the verify pass streams it every launch):
+//   wide   (16 B): {c0, c1, c2, dlb}, dlb = bits(D) & ~0xff | (launch & 255) -- D rounded down to
+//                  15 mantissa bits (still a lower bound), the slot of the pose history;
+//   narrow (12 B, targets < 2^26 - 2): c0 | x0 << 26, c1 | x1 << 26, c2 | x2 << 26 with the 18-bit
+//                  word x = (launch & 63) | code(D) << 6, code(D) = D in units of cell / 1024 as a
+//                  4-bit exponent and 8-bit mantissa, rounded down (0: D < 1 unit; 0xfff caps D at
+//                  ~32 cells).  An empty slot is 2^26 - 1 (above every position and the sentinel).
+// A smaller D only sends more queries to the search, so every rounding is down.
+struct CacheRec {
+    uint32_t c0, c1, c2;  // positions, ~0u = empty slot
+    uint32_t slot;        // launch of the search & hist_mask
+    float D;
+};
+constexpr uint32_t kPos26 = (1u << 26) - 1;
+constexpr int kHist = 256;  // pose history slots allocated (narrow records use 64 of them)
+__device__ __forceinline__ uint32_t dcode12(float D, float inv_unit) {
+    const float x = D * inv_unit;
+    if (!(x >= 1.f)) return 0u;
+    const uint32_t b = __float_as_uint(x);
+    const uint32_t e = (b >> 23) - 127u;
+    return e >= 15u ? 0xfffu : ((e + 1u) << 8) | ((b >> 15) & 0xffu);
+}
+__device__ __forceinline__ float ddecode12(uint32_t c, float unit) {
+    return c ? __uint_as_float((((c >> 8) + 126u) << 23) | ((c & 0xffu) << 15)) * unit : 0.f;
+}
+// the raw words of record i (narrow: .w unused)
+__device__ __forceinline__ uint4 cache_raw(const IcpArgs& a, int64_t i) {
+    if (a.narrow) {
+        const uint3 w = *(const uint3*)(a.cand + 3 * i);
+        return make_uint4(w.x, w.y, w.z, 0u);
+    }
+    return ((const uint4*)a.cand)[i];
+}
+__device__ __forceinline__ CacheRec cache_dec(const IcpArgs& a, const uint4 w) {
+    CacheRec r;
+    if (a.narrow) {
+        auto pos = [](uint32_t v) { const uint32_t c = v & kPos26; return c == kPos26 ? ~0u : c; };
+        r.c0 = pos(w.x);
+        r.c1 = pos(w.y);
+        r.c2 = pos(w.z);
+        const uint32_t x = (w.x >> 26) | ((w.y >> 26) << 6) | ((w.z >> 26) << 12);
+        r.slot = x & 63u;
+        r.D = ddecode12(x >> 6, a.dunit);
+    } else {
+        r.c0 = w.x;
+        r.c1 = w.y;
+        r.c2 = w.z;
+        r.slot = w.w & 0xffu;
+        r.D = __uint_as_float(w.w & ~0xffu);
+    }
+    return r;
+}
+__device__ __forceinline__ CacheRec cache_load(const IcpArgs& a, int64_t i) { return cache_dec(a, cache_raw(a, i)); }
+__device__ __forceinline__ void cache_store(const IcpArgs& a, int64_t i, uint32_t c0, uint32_t c1, uint32_t c2, float D,
+                                            uint32_t launch) {
+    if (a.narrow) {
+        auto pos = [](uint32_t c) { return c == ~0u ? kPos26 : c; };
+        const uint32_t x = (launch & 63u) | (dcode12(D, a.inv_dunit) << 6);
+        *(uint3*)(a.cand + 3 * i) =
+            make_uint3(pos(c0) | ((x & 63u) << 26), pos(c1) | (((x >> 6) & 63u) << 26), pos(c2) | ((x >> 12) << 26));
+    } else {
+        ((uint4*)a.cand)[i] = make_uint4(c0, c1, c2, (__float_as_uint(fmaxf(D, 0.f)) & ~0xffu) | (launch & 0xffu));
+    }
+}
 
 // the cached candidates' winner under the current pose, by (d2, target index)
 struct CacheBest {
@@ -587,8 +657,8 @@ struct CacheBest {
     uint32_t bk = ~0u;
     float4 P = make_float4(0.f, 0.f, 0.f, 0.f);
 };
-__device__ __forceinline__ CacheBest cache_best(const float4* tp, const uint4 cd, float qx, float qy, float qz) {
-    const uint32_t c[3] = {cd.x, cd.y, cd.z};  // .w is the dlb word
+__device__ __forceinline__ CacheBest cache_best(const float4* tp, const CacheRec& cd, float qx, float qy, float qz) {
+    const uint32_t c[3] = {cd.c0, cd.c1, cd.c2};
     float4 p[kCache];
 #pragma unroll
     for (int s = 0; s < kCache; s++) p[s] = c[s] != ~0u ? tp[c[s]] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -608,12 +678,6 @@ __device__ __forceinline__ CacheBest cache_best(const float4* tp, const uint4 cd
     return r;
 }
 
-// dlb word: D rounded down to 15 mantissa bits (still a lower bound), launch index in the low byte
-constexpr int kHist = 256;     // pose history slots (launch & 255)
-constexpr uint32_t kMaxAge = 128;  // older caches are searched again (so the slot is never reused)
-__device__ __forceinline__ uint32_t pack_dlb(float D, uint32_t launch) {
-    return (__float_as_uint(fmaxf(D, 0.f)) & ~0xffu) | (launch & 0xffu);
-}
 // 16-byte record of a table by element index.  The byte offset is 32-bit (so the load can use
 // the saddr + 32-bit VGPR offset form): pcp_icp_check_sizes() keeps every table this reads
 // (the fp32 target incl. its far sentinel) below 2^28 records = 4 GB.
@@ -657,7 +721,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
         const int64_t i = (cstart_ + k) * 64 + lane;
         if (k < nsteps && i < a.nq) {
             q = ldq(a, i);
-            cd = a.cand[i];
+            cd = cache_raw(a, i);
         } else {
             q = make_float4(0.f, 0.f, 0.f, 0.f);
             cd = none;
@@ -666,9 +730,10 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     };
     auto gather = [&](const uint4 cd, float4& p0, float4& p1, float4& p2) {
         // an empty slot reads the far sentinel tp[ntp]: d2 = inf
-        p0 = ld16(a.tp, min(cd.x, a.ntp));
-        p1 = ld16(a.tp, min(cd.y, a.ntp));
-        p2 = ld16(a.tp, min(cd.z, a.ntp));
+        const CacheRec r = cache_dec(a, cd);
+        p0 = ld16(a.tp, min(r.c0, a.ntp));
+        p1 = ld16(a.tp, min(r.c1, a.ntp));
+        p2 = ld16(a.tp, min(r.c2, a.ntp));
     };
     float4 q1, q2;
     uint4 c1_, c2_;
@@ -688,7 +753,7 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             const int64_t i = (cstart_ + k) * 64 + lane;
             const bool valid = i < a.nq;
             const float4 qq = q1;
-            const uint32_t Dw = valid ? c1_.w : 0u;
+            const CacheRec rec = cache_dec(a, c1_);
             const float4 p0 = g0, p1 = g1, p2 = g2;
             // issue chunk c+1's gathers and chunk c+2's words before using chunk c's
             gather(c2_, g0, g1, g2);
@@ -714,16 +779,16 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
             take(p1);
             take(p2);
             // the query at the pose of its last search
-            const uint32_t sl = Dw & 0xffu;
+            const uint32_t sl = rec.slot;
             const float4 A = s_pose[sl][0], B = s_pose[sl][1], C = s_pose[sl][2];
             const float ex = qx - __fmaf_rn(A.z, qq.z, __fmaf_rn(A.y, qq.y, __fmaf_rn(A.x, qq.x, C.y)));
             const float ey = qy - __fmaf_rn(B.y, qq.z, __fmaf_rn(B.x, qq.y, __fmaf_rn(A.w, qq.x, C.z)));
             const float ez = qz - __fmaf_rn(C.x, qq.z, __fmaf_rn(B.w, qq.y, __fmaf_rn(B.z, qq.x, C.w)));
             const float delta = sqrtf(__fmaf_rn(ez, ez, __fmaf_rn(ey, ey, ex * ex))) * 1.00001f + 1e-7f;
-            const float lb = __uint_as_float(Dw & ~0xffu) * 0.99998f - delta;  // every uncached point is >= lb
+            const float lb = rec.D * 0.99998f - delta;  // every uncached point is >= lb
             // the nearest cached point is the exact 1-NN (it beats lb), or nothing is within rmax
             const float thr = fminf(m * 1.0003f, r2m);
-            bool ok = valid && ((a.launch - Dw) & 0xffu) < kMaxAge && lb > 0.f && thr + 1e-12f < lb * lb;
+            bool ok = valid && ((a.launch - sl) & a.hist_mask) < a.max_age && lb > 0.f && thr + 1e-12f < lb * lb;
             ok = ok && !(a.dbg & kDbgNoVerify);
             const bool srch = valid && !ok;
             const uint64_t msk = __ballot(srch);
@@ -1057,9 +1122,11 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
             // the cache: the 3 nearest; settled: D bounds every uncached point for the verify
             // pass.  Unsettled: the fallback pass (which overwrites the cache) gets the
             // octant's first uncached d2 instead.
+            // (unsettled: the message is the octant's first uncached distance, rounded down)
             const float D = outside ? dout * 0.9999f
-                                    : (settled ? fminf(sqrtf(o.dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f : o.dnext);
-            if (lead) a.cand[i] = make_uint4(o.c0, o.c1, o.c2, pack_dlb(D, a.launch));
+                                    : (settled ? fminf(sqrtf(o.dnext), (m > 0.f ? m : 0.f) * g.hf) * 0.9999f
+                                               : sqrtf(o.dnext) * 0.99999f);
+            if (lead) cache_store(a, i, o.c0, o.c1, o.c2, D, a.launch);
         }
         // ---- fallback list (ballot + mbcnt, no atomics) and accumulators
         const bool fb = valid && lead && !settled;
@@ -1159,19 +1226,18 @@ __device__ __forceinline__ void ring_run(IcpArgs& a, double (*s_acc)[kAcc], cons
             i = a.ring_all ? j : list[j];
             xform(a, ldq(a, i), qx, qy, qz);
             // provisional: the cache's best (refreshed by the search pass), an upper bound
-            const uint4 cd = a.cand[i];
+            const CacheRec cd = cache_load(a, i);
             const CacheBest cbst = cache_best(a.tp, cd, qx, qy, qz);
             if (cbst.bd <= b.bd) {
                 b.bd = cbst.bd;
                 b.bj = cbst.bj;
                 b.bk = cbst.bk;
             }
-            // the search pass left this launch's octant message: the 4th smallest d2 of its
-            // octant.  Above the cached best, every octant point tied with that best is cached,
-            // so the cached best IS the octant's (d2, index) winner and its cells need no rescan.
-            const uint32_t msg = cd.w;
-            const bool skip_oct = !a.ring_all && ((msg ^ a.launch) & 0xffu) == 0u &&
-                                  __uint_as_float(msg & ~0xffu) > cbst.bd;
+            // the search pass left this launch's octant message: the 4th smallest distance of
+            // its octant (rounded down).  Above the cached best, every octant point tied with
+            // that best is cached, so the cached best IS the octant's (d2, index) winner and its
+            // cells need no rescan.
+            const bool skip_oct = !a.ring_all && cd.slot == (a.launch & a.hist_mask) && cd.D * cd.D > cbst.bd;
             bool done = false;
             if (!a.ring_all) {
                 // stage 2: the 3x3x3 cells around the query (less the octant's when it was
@@ -1221,7 +1287,7 @@ __device__ __forceinline__ void ring_run(IcpArgs& a, double (*s_acc)[kAcc], cons
             const bool ok = b.bj != 0x7fffffff;
             // no bound kept: the next launch searches it again
             if (lead) {
-                a.cand[i] = make_uint4(ok ? b.bk : ~0u, ~0u, ~0u, pack_dlb(0.f, a.launch));
+                cache_store(a, i, ok ? b.bk : ~0u, ~0u, ~0u, 0.f, a.launch);
             }
         }
         const bool acc_ok = valid && lead && b.bj != 0x7fffffff && !(a.dbg & kDbgNoAccum);
@@ -1299,7 +1365,7 @@ __global__ void k_scatter_corr(IcpArgs a, int32_t* idx, float* d2) {
         const int oq = a.qidx[i];
         float x, y, z;
         xform(a, qq, x, y, z);
-        const CacheBest w = cache_best(a.tp, a.cand[i], x, y, z);  // the settled winner is cached
+        const CacheBest w = cache_best(a.tp, cache_load(a, i), x, y, z);  // the settled winner is cached
         const bool ok = w.bd <= a.r2;
         idx[oq] = ok ? w.bj : -1;
         d2[oq] = ok ? w.bd : INFINITY;
@@ -1331,7 +1397,7 @@ __global__ void k_make_keys(IcpArgs a, uint32_t offset, uint64_t* keys) {
         const int oq = a.qidx[i];
         float x, y, z;
         xform(a, qq, x, y, z);
-        const CacheBest w = cache_best(a.tp, a.cand[i], x, y, z);
+        const CacheBest w = cache_best(a.tp, cache_load(a, i), x, y, z);
         keys[oq] = w.bd <= a.r2 ? (((uint64_t)__float_as_uint(w.bd) << 32) | (uint64_t)(uint32_t)((uint32_t)w.bj + offset))
                                 : kNoKey;
     }
@@ -1697,7 +1763,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
         }
     }
     hipLaunchKernelGGL(k_pose_set, dim3(1), dim3(1), 0, ctx->stream, T_dev, hp, icp->pose_dev,
-                       icp->pose_hist + (icp->launches & (kHist - 1)) * 12);
+                       icp->pose_hist + (icp->launches & (icp->narrow ? 63 : kHist - 1)) * 12);
     a.pose = icp->pose_dev;  // every kernel reads the pose (and the previous one) from HBM
     for (int k = 0; k < 9; k++) a.R[k] = hp.R[k];
     for (int k = 0; k < 3; k++) a.t[k] = hp.t[k];
@@ -1709,6 +1775,11 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     const double rr = (0.5 - (double)a.mc) * a.g.h;
     a.cert2 = (float)(rr * rr * (1.0 - 1e-5));
     a.cand = icp->cand;
+    a.narrow = icp->narrow ? 1 : 0;
+    a.hist_mask = icp->narrow ? 63u : (uint32_t)(kHist - 1);
+    a.max_age = icp->narrow ? 32u : 128u;
+    a.dunit = (float)(a.g.h / 1024.0);
+    a.inv_dunit = (float)(1024.0 / a.g.h);
     a.pose_hist = icp->pose_hist;
     a.launch = (uint32_t)icp->launches;
     a.ntp = (uint32_t)tg->n;
@@ -1971,14 +2042,23 @@ int icp_make(pcp_ctx* ctx, const pcp_index* target, QXyz* q3, int32_t* qi, int64
     int rc = dmalloc(ctx, &icp->partials, (size_t)(icp->nb_ver + icp->nb_fast + icp->nb_ring) * kAcc);
     if (!rc) rc = dmalloc(ctx, &icp->acc, kAcc);
     if (!rc) rc = dmalloc(ctx, &icp->pose_dev, 24);
-    if (!rc) rc = dmalloc(ctx, &icp->cand, icp->nq + 1);
+    // 12-byte cache records when every position (and the far sentinel) fits 26 bits
+    icp->narrow = target->n + 1 < (int64_t)kPos26;
+    const int rw = icp->narrow ? 3 : 4;  // words per record
+    if (!rc) rc = dmalloc(ctx, &icp->cand, (size_t)(icp->nq + 1) * rw);
     if (!rc) rc = dmalloc(ctx, &icp->pose_hist, kHist * 12);
     // the first launch over a dense grid (the octant pass over every query) writes every cache
     // record before any pass reads one: only the sentinel record needs its value then (an 800 MB
-    // memset at 50M queries, ~0.1 ms of the pre-iteration span, otherwise)
+    // memset at 50M queries, ~0.1 ms of the pre-iteration span, otherwise).  An empty record has
+    // no positions and D = 0 (wide: NaN), so it is never settled from.
     const bool cand_all = !target->g.dense;
-    if (!rc && (hipMemsetAsync(icp->cand + (cand_all ? 0 : icp->nq), 0xff,
-                               (size_t)(cand_all ? icp->nq + 1 : 1) * sizeof(uint4), ctx->stream) != hipSuccess ||
+    const int64_t r0 = cand_all ? 0 : icp->nq, nr = cand_all ? icp->nq + 1 : 1;
+    hipError_t me = hipSuccess;
+    if (!rc)
+        me = icp->narrow ? hipMemsetD32Async((hipDeviceptr_t)(icp->cand + r0 * rw), (int)kPos26, (size_t)(nr * rw),
+                                             ctx->stream)
+                         : hipMemsetAsync(icp->cand + r0 * rw, 0xff, (size_t)nr * 16, ctx->stream);
+    if (!rc && (me != hipSuccess ||
                 hipMemsetAsync(icp->pose_hist, 0, kHist * 12 * sizeof(float), ctx->stream) != hipSuccess ||
                 hipMemsetAsync(icp->pose_dev, 0, 24 * sizeof(float), ctx->stream) != hipSuccess))
         rc = set_error(ctx, PCP_ERR_HIP, "memset");
@@ -2081,7 +2161,20 @@ int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, i
     icp->oct_g_first = oct_lanes_first ? oct_lanes_first : 1;
     icp->oct_g_list = oct_lanes_list;
     icp->ring_g = ring_lanes;
-    icp->dbg = ablate;
+    if ((ablate & PCP_ICP_OPT_WIDE_CACHE) && icp->narrow) {  // re-create the records in the 16-byte form
+        if (icp->launches > 0) return PCP_ERR_ARG;
+        pcp_ctx* ctx = icp->owner;
+        uint32_t* w = nullptr;
+        if (int rc = pcp::dmalloc(ctx, &w, (size_t)(icp->nq + 1) * 4)) return rc;
+        if (hipMemsetAsync(w, 0xff, (size_t)(icp->nq + 1) * 16, ctx->stream) != hipSuccess) {
+            pcp::dfree(ctx, w);
+            return PCP_ERR_HIP;
+        }
+        pcp::dfree(ctx, icp->cand);
+        icp->cand = w;
+        icp->narrow = false;
+    }
+    icp->dbg = ablate & ~PCP_ICP_OPT_WIDE_CACHE;
     return PCP_OK;
 }
 

@@ -339,12 +339,16 @@ class ICP:
         index.ctx, index.src, index.h, index.f64, index.indices = ctx, target, hi, False, None
         return cls(index, q, _handle=hq)
 
-    def set_options(self, oct_lanes_first=1, oct_lanes_list=0, ring_lanes=0, ablate=0):
+    WIDE_CACHE = 128  # PCP_ICP_OPT_WIDE_CACHE
+
+    def set_options(self, oct_lanes_first=1, oct_lanes_list=0, ring_lanes=0, ablate=0, wide_cache=False):
         """Test / profiling controls (pcp_icp_set_options): lanes per query of the octant pass
         (first launch, later lists; 0 = by density) and of the fallback pass (0 = by length);
-        `ablate` switches passes off (results are then wrong)."""
+        `ablate` switches passes off (results are then wrong); `wide_cache` keeps 16-byte cache
+        records (before the first step; results are identical)."""
+        flags = int(ablate) | (self.WIDE_CACHE if wide_cache else 0)
         self.ctx.check(self.ctx.lib.pcp_icp_set_options(self.h, int(oct_lanes_first), int(oct_lanes_list),
-                                                        int(ring_lanes), int(ablate)))
+                                                        int(ring_lanes), flags))
 
     def step(self, T, rmax, corr=False):
         """One iteration at pose T; returns the (device) accumulators (+ correspondences)."""

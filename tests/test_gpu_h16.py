@@ -18,7 +18,7 @@ import pytest
 import torch
 
 import oracle_ctypes as ora
-from h16_check import EPS, angle_summary, check_against_oracle, row_entries
+from h16_check import EPS, angle_summary, check_against_oracle, plane_angles, row_entries
 
 pytestmark = pytest.mark.gpu
 R = 0.2
@@ -99,7 +99,14 @@ def test_h16_tiny_clouds(ctx, scene, npts):
     cnt, planes = tree.radius_normals(np.arange(npts, dtype=np.int32), R)
     ep = np.stack([planes[f] for f in ("normal_x", "normal_y", "normal_z", "min_value", "curvature", "distance")], 1)
     gp = nrm.cpu().numpy()
-    assert np.allclose(gp[:, :5], ep[:, :5], atol=2e-4, equal_nan=True), (gp, ep)
+    # the MFMA path sums the moments as hi/lo f16 pairs in the query cell's frame: normals within
+    # an angle (a 5-point plane is poorly conditioned), eigenvalue ratios relatively; rows of <= 3
+    # points carry the default plane on both sides
+    small = cnt <= 3
+    assert np.allclose(gp[small, :5], ep[small, :5], atol=0, equal_nan=True), (gp, ep)
+    if (~small).any():
+        assert plane_angles(gp[~small], ep[~small]).max() < 2e-3, (gp, ep)
+        assert np.allclose(gp[~small, 3:5], ep[~small, 3:5], rtol=2e-3, atol=2e-5), (gp, ep)
 
 
 def test_h16_dropped_points(ctx, scene):

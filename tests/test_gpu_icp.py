@@ -149,15 +149,20 @@ def _small_motion():
     return synth.rigid(0.2, -0.1, 0.1, (0.03, -0.02, 0.01))
 
 
-def test_verify_pass_exact_over_registration(ctx):
+@pytest.mark.parametrize("cache", ["narrow", "wide"])
+def test_verify_pass_exact_over_registration(ctx, cache):
     # The verify pass settles a query from its previous winner and lower bound (triangle
     # inequality); it must return exactly what an exhaustive search returns, at every
     # iteration of a registration, on a repeated pose, and after a jump back to the start.
+    # Both cache record forms: 12 bytes (26-bit positions, the bound as a 12-bit code rounded
+    # down; the default below 2^26 - 2 targets) and 16 bytes (PCP_ICP_OPT_WIDE_CACHE).
     from pointcloudprocess_amd import ops, synth
     T_true = synth.rigid()
     tgt, q = _pair(200_000, 31, T_true)
     index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
     icp = ops.ICP(index, q.to(ctx.device))
+    if cache == "wide":
+        icp.set_options(wide_cache=True)
     oi = ora.F32Index(tgt.numpy())
     T = np.eye(4)
     searched = []
@@ -197,6 +202,31 @@ def test_verify_pass_exact_over_registration(ctx):
     _, ci, _ = icp.step(poses[-1], 0.02, corr=True)
     ei, _ = oi.correspond(q.numpy(), R, t, 0.02)
     assert np.array_equal(ci.cpu().numpy(), ei)
+
+
+@pytest.mark.parametrize("cache", ["narrow", "wide"])
+def test_long_registration_history_wrap(ctx, cache):
+    """75 launches of small motions: the caches outlive the pose history (64 slots narrow, 256
+    wide) and age out (32 / 128 launches) -- correspondences stay exact at every checked launch."""
+    from pointcloudprocess_amd import ops, synth
+    T_true = synth.rigid()
+    tgt, q = _pair(100_000, 53, T_true)
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+    icp = ops.ICP(index, q.to(ctx.device))
+    if cache == "wide":
+        icp.set_options(wide_cache=True)
+    oi = ora.F32Index(tgt.numpy())
+    rng = np.random.default_rng(5)
+    for it in range(75):
+        T = synth.rigid(*(rng.normal(0, 0.05, 3)), tuple(rng.normal(0, 0.004, 3))) @ T_true
+        _, ci, cd = icp.step(T, 0.25, corr=True)
+        if it % 5 == 4 or it >= 70:
+            R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+            ei, ed = oi.correspond(q.numpy(), R, t, 0.25)
+            assert np.array_equal(ci.cpu().numpy(), ei), f"launch {it}"
+            assert np.array_equal(cd.cpu().numpy()[ei >= 0], ed[ei >= 0])
+    icp.close()
+    index.close()
 
 
 def test_ties_lattice(ctx):
