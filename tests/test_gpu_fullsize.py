@@ -133,9 +133,14 @@ def test_c5_fullsize_200m(ctx):
         to_loc[pts] = torch.arange(pts.numel(), device=ctx.device)
         s_glob = pts[loc]
         lens_s = lens[s_glob]
-        sub_offs = torch.cat([torch.zeros(1, dtype=torch.int64, device=ctx.device), torch.cumsum(lens_s, 0)])
+        # the sampled rows as a CSR over ALL the tile's points (the others empty; loc ascends), so
+        # that the checks index the offsets and the points with the same local ids
+        lens_all = torch.zeros(pts.numel(), dtype=torch.int64, device=ctx.device)
+        lens_all[loc] = lens_s
+        sub_offs = torch.cat([torch.zeros(1, dtype=torch.int64, device=ctx.device), torch.cumsum(lens_all, 0)])
         row_of = torch.repeat_interleave(torch.arange(s_glob.numel(), device=ctx.device), lens_s)
-        pos = offs[s_glob][row_of] + (torch.arange(row_of.numel(), device=ctx.device) - sub_offs[:-1][row_of])
+        start = torch.cumsum(lens_s, 0) - lens_s
+        pos = offs[s_glob][row_of] + (torch.arange(row_of.numel(), device=ctx.device) - start[row_of])
         sub_idx = to_loc[idx[pos].long()]
         assert bool((sub_idx >= 0).all())       # every neighbour lies inside the tile +- 1 m
         nrm_loc = torch.zeros((pts.numel(), 6), dtype=nrm.dtype, device=ctx.device)

@@ -6,8 +6,10 @@
 #   c5ab       interleaved A/B of the C5 bench line: this tree vs variants/$VAR (PCP_LIB)
 #   c5trace    rocprofv3 kernel trace + stats of one C5 bench run
 #   tests      the whole GPU suite + smoke
-#   c4ab       interleaved A/B of the C4 bench line: this tree vs variants/$VAR
+#   c4ab       interleaved A/B of the C4 bench line: this tree vs variants/$V for V in $VARS (or $VAR)
 #   c4trace    kernel trace of the C4 bench (per-iteration table)
+#   c3ab       interleaved A/B of the C3 bench line vs variants/$V for V in $VARS
+#   knntests   the kNN / normals tests and the full-size C3 check
 #   c2ab       interleaved A/B of the C2 bench line vs variants/$VAR
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
@@ -33,11 +35,22 @@ tests)
 c4ab)
   for rep in 1 2 3; do
     timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 >> $O/c4_ab_new.jsonl 2>> $O/c4_ab.err
-    PCP_LIB=variants/$VAR/libpcp.so timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 >> $O/c4_ab_$VAR.jsonl 2>> $O/c4_ab.err
+    for V in ${VARS:-$VAR}; do
+      PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 >> $O/c4_ab_$V.jsonl 2>> $O/c4_ab.err
+    done
   done ;;
 c4trace)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4trace -o run -- python3 bench.py --no-cpu --steps 2 --warmup 1 > $O/c4trace.log 2>&1
   python3 tools/trace_iters.py $O/c4trace > $O/per_iteration.txt 2>&1 || true ;;
+c3ab)
+  for rep in 1 2 3; do
+    timeout -k 10 300 python3 -u bench.py --config C3 --no-cpu --steps 5 >> $O/c3_ab_new.jsonl 2>> $O/c3_ab.err
+    for V in ${VARS:-$VAR}; do
+      PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C3 --no-cpu --steps 5 >> $O/c3_ab_$V.jsonl 2>> $O/c3_ab.err
+    done
+  done ;;
+knntests)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_knn.py "tests/test_gpu_fullsize.py::test_c3_fullsize_voxel_and_normals" -x -v -s --timeout 500 --timeout-method thread > $O/knn_tests.log 2>&1 ;;
 c2ab)
   for rep in 1 2; do
     timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_new.jsonl 2>> $O/c2_ab.err
