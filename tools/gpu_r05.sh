@@ -25,7 +25,9 @@ icptests)
 c5ab)
   for rep in 1 2; do
     timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_new.jsonl 2>> $O/c5_ab.err
-    PCP_LIB=variants/$VAR/libpcp.so timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_$VAR.jsonl 2>> $O/c5_ab.err
+    for V in ${VARS:-$VAR}; do
+      PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_$V.jsonl 2>> $O/c5_ab.err
+    done
   done ;;
 c5trace)
   timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5trace -o run -- python3 bench.py --config C5 --no-cpu --steps 2 --warmup 1 > $O/c5trace.log 2>&1 ;;
@@ -56,6 +58,18 @@ c2ab)
     timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_new.jsonl 2>> $O/c2_ab.err
     PCP_LIB=variants/$VAR/libpcp.so timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_$VAR.jsonl 2>> $O/c2_ab.err
   done ;;
+c5pmc)
+  sq1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_VALU"
+  sq2="SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
+  sq3="SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"
+  mkdir -p $O/c5pmc
+  timeout -k 10 60 rocprofv3 -L > $O/c5pmc/counters_list.txt 2>&1
+  i=0
+  for c in "$sq1" "$sq2" "$sq3" "WRITE_SIZE" "FETCH_SIZE"; do
+    timeout -s KILL 200 rocprofv3 --pmc $c --output-format csv -d $O/c5pmc/p$i -o run -- python3 bench.py --config C5 --no-cpu --steps 1 --warmup 0 --c5-points ${C5N:-50000000} > $O/c5pmc/p$i.log 2>&1
+    i=$((i+1))
+  done
+  python3 tools/pmc_table.py $O/c5pmc k_h16 > $O/c5pmc/table.txt 2>&1 ;;
 esac
 echo "step $st done" >> $O/steps.log
 done

@@ -14,7 +14,7 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(out, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         m = re.search(r"(\w+)(<[^(]*>)?\(", r["Kernel_Name"].replace("(anonymous namespace)", "anon"))
-        name = m.group(1) if m else r["Kernel_Name"]
+        name = (m.group(1) + (m.group(2) or "")) if m else r["Kernel_Name"]
         if any(k in name for k in keys):
             vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in vals.items():
