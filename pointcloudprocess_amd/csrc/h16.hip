@@ -133,8 +133,8 @@ __global__ void k_h16_plane_default(pcp_plane* out, int64_t n) {
 // FMAs on every lane and the sums' 36-value reduce-scatter).
 constexpr int kMxSteps = 4;              // candidate steps per block (4 x 64)
 constexpr int kMxC = kMxSteps * 64;      // candidates per block
-constexpr int kMxF = 18;                 // moment feature rows: hi, lo f16 of x y z xx xy xz yy yz zz
-constexpr int kMxFS = kMxC + 4;          // feature row stride (halves): 8-byte fragment reads spread over the banks
+constexpr int kMxF = 9;                  // moment feature rows: x y z xx xy xz yy yz zz, each word = (hi, lo) f16
+constexpr int kMxFS = kMxC + 4;          // feature row stride (words)
 constexpr int kMxPS = kMxC + 16;         // P row stride (floats)
 constexpr float kMxFar = 1e30f;          // |P|^2 of a padding candidate, C of a non-query: never a hit
 constexpr int kMxWaves = 3;              // waves per SIMD (LDS-bound: ~13.9 KB per fill wave)
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
     __shared__ uint4 s_row[9];   // per neighbour row: kk = j + off, the query column [b1, b2)
     __shared__ float2 s_rdz[9];  // per neighbour row: its dy h, dz h
     __shared__ float s_p[FILL ? 4 : 1][FILL ? kMxPS : 1];                          // P x y z, |P|^2
-    __shared__ __attribute__((aligned(16))) _Float16 s_f[FILL ? kMxF : 1][FILL ? kMxFS : 1];  // moments
+    __shared__ __attribute__((aligned(16))) uint32_t s_f[FILL ? kMxF : 1][FILL ? kMxFS : 1];  // moments
     const GridDesc& g = a.g;
     const int lane = threadIdx.x;
     const float hf = a.hf, hh = 0.5f * a.hf, r2 = a.r2;
@@ -267,8 +267,9 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
 #pragma unroll
                         for (int k = 0; k < 9; k++) {
                             const _Float16 hi = (_Float16)mo[k];
-                            s_f[2 * k][c] = hi;
-                            s_f[2 * k + 1][c] = (_Float16)(mo[k] - (float)hi);
+                            const _Float16 lo = (_Float16)(mo[k] - (float)hi);
+                            s_f[k][c] = (uint32_t)__builtin_bit_cast(uint16_t, hi) |
+                                        ((uint32_t)__builtin_bit_cast(uint16_t, lo) << 16);
                         }
                     }
                 }
@@ -300,7 +301,7 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
                 const float b16 = kq == 0 ? ax : (kq == 1 ? ay : (kq == 2 ? az : 1.f));
                 const mx_f4 c16 = {qc, qc, qc, qc};
                 int32_t cntv = 0;  // lane t: query t's row length so far
-                mx_f4 acc1 = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+                mx_f4 acc1 = {0.f, 0.f, 0.f, 0.f};
                 // rows of query group G (queries 4G .. 4G + 3) over the block's steps: the group's
                 // row starts and lengths live in scalar registers for the pass
                 auto group_rows = [&](auto gtag, const mx_f4& Cg, uint32_t mb) {
@@ -328,14 +329,14 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
                         const mx_f4 D = Ds[s];
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
-                            if (!((ownm >> (4 * G + i)) & 1u)) continue;
+                            // (a query outside the tile has C = far: never a hit)
                             const bool hit = D[i] < 0.f;
                             const uint64_t m = __ballot(hit);
                             if constexpr (FILL) {
                                 if (hit) {  // the row entries of this step: one contiguous run
-                                    const uint32_t pos = rc[i] + __builtin_amdgcn_mbcnt_hi(
-                                                                     (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                                    out_idx[rb[i] + pos] = cidv[s];
+                                    int32_t* row = out_idx + (rb[i] + (int64_t)rc[i]);  // uniform
+                                    row[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = cidv[s];
                                 }
                             }
                             rc[i] += (uint32_t)__popcll(m);
@@ -359,45 +360,37 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
 #pragma unroll
                         for (int s = 0; s < kMxSteps; s++) {
                             if (64u * s >= mb) break;
-                            // sums: the hit matrix in the transposed layout, then moments x hits
+                            // sums: the hit matrix in the transposed layout, then moments x hits,
+                            // 16 candidates per product: K = 32 runs over (candidate, hi / lo)
+                            // pairs, so each moment's two f16 halves meet the same hit and add
 #pragma unroll
-                            for (int ch = 0; ch < 2; ch++) {
-                                if (64u * s + 32u * ch >= mb) break;
-                                const int c0 = 64 * s + 32 * ch;
-                                const mx_f4 S0 = __builtin_amdgcn_mfma_f32_16x16x4f32(s_p[kq][c0 + t], b16, c16, 0, 0, 0);
-                                const mx_f4 S1 = __builtin_amdgcn_mfma_f32_16x16x4f32(s_p[kq][c0 + 16 + t], b16, c16, 0, 0, 0);
+                            for (int ch = 0; ch < 4; ch++) {
+                                if (64u * s + 16u * ch >= mb) break;
+                                const int c0 = 64 * s + 16 * ch;
+                                const mx_f4 S = __builtin_amdgcn_mfma_f32_16x16x4f32(s_p[kq][c0 + t], b16, c16, 0, 0, 0);
                                 mx_h8 mk;
 #pragma unroll
                                 for (int i = 0; i < 4; i++) {
-                                    mk[i] = (_Float16)mx_hit(S0[i]);
-                                    mk[4 + i] = (_Float16)mx_hit(S1[i]);
+                                    const _Float16 h = (_Float16)mx_hit(S[i]);
+                                    mk[2 * i] = h;
+                                    mk[2 * i + 1] = h;
                                 }
-                                // A: moment row t (tile 1) / 16 + t (tile 2: zz only) of candidates
-                                // c0 + 4 kq + 0..3 and c0 + 16 + 4 kq + 0..3
-                                const uint2 f1a = *(const uint2*)&s_f[t][c0 + 4 * kq];
-                                const uint2 f1b = *(const uint2*)&s_f[t][c0 + 16 + 4 * kq];
-                                const mx_h8 fa1 = __builtin_bit_cast(mx_h8, make_uint4(f1a.x, f1a.y, f1b.x, f1b.y));
-                                uint4 f2 = make_uint4(0u, 0u, 0u, 0u);
-                                if (t < kMxF - 16) {
-                                    const uint2 f2a = *(const uint2*)&s_f[16 + t][c0 + 4 * kq];
-                                    const uint2 f2b = *(const uint2*)&s_f[16 + t][c0 + 16 + 4 * kq];
-                                    f2 = make_uint4(f2a.x, f2a.y, f2b.x, f2b.y);
-                                }
-                                const mx_h8 fa2 = __builtin_bit_cast(mx_h8, f2);
-                                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa1, mk, acc1, 0, 0, 0);
-                                acc2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa2, mk, acc2, 0, 0, 0);
+                                // A: moment t (rows past the 9 moments repeat the last; their
+                                // sums are never read) of candidates c0 + 4 kq + 0..3, (hi, lo) each
+                                const mx_h8 fa = __builtin_bit_cast(mx_h8, *(const uint4*)&s_f[min(t, kMxF - 1)][c0 + 4 * kq]);
+                                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa, mk, acc1, 0, 0, 0);
                             }
                         }
                     }
                 }
                 if constexpr (!FILL) {
                     if (own && lane < 16) count[caller] = cntv;
-                } else if (sums && own) {
-                    // lane l: moment rows 4 kq + i of query t = moments 2 kq (i = 0, 1: hi + lo) and
-                    // 2 kq + 1 (i = 2, 3); tile 2's lanes kq = 0: zz
+                } else if (sums) {
+                    // lane l: moments 4 kq + i of query t (kq = 2: the ninth, zz, and the count)
+                    const int32_t n_t = __shfl(cntv, t, 64);
                     float* o = sums[qs + t].S;
-                    *(float2*)(o + 2 * kq) = make_float2(acc1[0] + acc1[1], acc1[2] + acc1[3]);
-                    if (kq == 0) *(float2*)(o + 8) = make_float2(acc2[0] + acc2[1], __int_as_float(cntv));
+                    if (own && kq < 2) *(float4*)(o + 4 * kq) = make_float4(acc1[0], acc1[1], acc1[2], acc1[3]);
+                    if (own && kq == 2) *(float4*)(o + 8) = make_float4(acc1[0], __int_as_float(n_t), 0.f, 0.f);
                 }
             }
             wave_sync();  // s_row and the block's LDS are rewritten by the next cell
