@@ -131,13 +131,19 @@ __global__ void k_h16_plane_default(pcp_plane* out, int64_t n) {
 // Per query and 64-candidate step this is ~8 VALU ops (compare, row-store addressing, the mask
 // conversion) against ~34 for the per-lane-FMA form it replaces (round 4: the test, the 9 sum
 // FMAs on every lane and the sums' 36-value reduce-scatter).
-constexpr int kMxSteps = 4;              // candidate steps per block (4 x 64)
+// candidate steps per block (2 x 64): a smaller block is more blocks per neighbourhood but less
+// LDS per wave -- 5 waves/SIMD at 128 candidates against 3 at 256 (measured: 256 / 192 / 128 / 64
+// candidates 2030 / 2165 / 2240 / 2257 Mpts/s, profiles/r05_c5/)
+#ifndef PCP_MX_STEPS
+#define PCP_MX_STEPS 2
+#endif
+constexpr int kMxSteps = PCP_MX_STEPS;
 constexpr int kMxC = kMxSteps * 64;      // candidates per block
 constexpr int kMxF = 9;                  // moment feature rows: x y z xx xy xz yy yz zz, each word = (hi, lo) f16
 constexpr int kMxFS = kMxC + 4;          // feature row stride (words)
 constexpr int kMxPS = kMxC + 16;         // P row stride (floats)
 constexpr float kMxFar = 1e30f;          // |P|^2 of a padding candidate, C of a non-query: never a hit
-constexpr int kMxWaves = 3;              // waves per SIMD (LDS-bound: ~13.9 KB per fill wave)
+constexpr int kMxWaves = 5;              // waves per SIMD (~7.3 KB of LDS per fill wave)
 
 typedef float mx_f4 __attribute__((ext_vector_type(4)));
 typedef _Float16 mx_h8 __attribute__((ext_vector_type(8)));
