@@ -78,6 +78,10 @@ def parse():
     ap.add_argument("--c5-check", type=int, default=0,
                     help="--config C5 at N > 1: after timing, compare this many sampled rows per rank with the "
                          "single-process rows (rehearsal check)")
+    ap.add_argument("--c5-order", choices=("native", "tiles", "cells"), default="native",
+                    help="--config C5 diagnostic: 'tiles' feeds the scene in 1 m tile order (a scan-coherent "
+                         "caller order), 'cells' in the index's own cell order, instead of the generator's random "
+                         "order; the headline is 'native'")
     ap.add_argument("--config", choices=("C1", "C2", "C3", "C4", "C5"), default="C4")
     return ap.parse_args()
 

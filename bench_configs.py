@@ -300,6 +300,16 @@ def cfg_c5(ctx, args, rank, timer):
     n = int(args.c5_points)
     side = math.sqrt(n / 1.5e6) * 40.0  # the C5 test density (1.5M pts on 40 x 40 m)
     xyz = synth.street_scene(n, 5001, extent=(side, side), device=ctx.device)
+    order = getattr(args, "c5_order", "native")
+    if order == "tiles":  # diagnostic: caller order = 1 m tiles, row-major
+        t = torch.floor(xyz[:, :2] + side).long()
+        xyz = xyz[torch.argsort(t[:, 1] * 100_000 + t[:, 0])].contiguous()
+        del t
+    elif order == "cells":  # diagnostic: caller order = the index's cell order (z, y, x cells of r)
+        c = torch.floor((xyz - xyz.min(0).values) / R).long()
+        m = c.max(0).values + 1
+        xyz = xyz[torch.argsort((c[:, 2] * m[1] + c[:, 1]) * m[0] + c[:, 0])].contiguous()
+        del c
     own = halo = gid = None
     if world > 1:
         own, halo = D.radius_slab_split_dev(xyz[:, 0].contiguous(), world, rank, R)
@@ -331,7 +341,8 @@ def cfg_c5(ctx, args, rank, timer):
             "pmc_key": {"n": n, "world": world},
             "workload": f"C5: radiusSearch r=0.2 + normals over the fp16 cell-relative index, the {n}-pt street "
                         f"scene ({side:.0f} x {side:.0f} m)" + (f", split into {world} x-slabs with an r halo"
-                                                               if world > 1 else " on one GPU")}
+                                                               if world > 1 else " on one GPU")
+                        + ("" if order == "native" else f" [diagnostic: caller order = {order}]")}
 
     def per_rank():
         return {"owned_points": n_owned, "halo_points": 0 if halo is None else int(halo.numel()),

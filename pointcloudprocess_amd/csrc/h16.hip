@@ -148,12 +148,16 @@ constexpr int kMxWaves = 5;              // waves per SIMD (~7.3 KB of LDS per f
 typedef float mx_f4 __attribute__((ext_vector_type(4)));
 typedef _Float16 mx_h8 __attribute__((ext_vector_type(8)));
 
-// one query's F1 sums for k_h16_mx_planes (sorted order): S P (3), S P P^T (xx xy xz yy yz zz),
-// the hit count; P relative to the query cell's centre
-struct alignas(16) MxSums {
+// one query's F1 sums for k_h16_mx_planes, by caller index: S P (3), S P P^T (xx xy xz yy yz zz),
+// the hit count and the query's cell (P relative to its centre).  64 bytes: the fill writes each
+// record whole with one store instruction (a 64-byte-aligned random write, no partial line), so
+// the planes pass reads the sums and writes the planes both in caller order -- a plane written at
+// a random caller position (24 B, straddling lines) cost ~8 ms of the 200M step (profiles/r05_c5).
+struct alignas(64) MxSums {
     float S[9];
     int32_t n;
-    float pad0, pad1;
+    uint32_t cell;
+    float pad[5];
 };
 
 // D[query 4G + i][candidate lane] += the K = 3 + 1 product of the step (C: the group's |Q|^2 - r^2)
@@ -392,11 +396,13 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
                 if constexpr (!FILL) {
                     if (own && lane < 16) count[caller] = cntv;
                 } else if (sums) {
-                    // lane l: moments 4 kq + i of query t (kq = 2: the ninth, zz, and the count)
+                    // lane l: 16 bytes of query t's record -- moments 4 kq + i (kq = 2: the ninth, zz,
+                    // the count and the cell; kq = 3: padding), the four lanes one whole record
                     const int32_t n_t = __shfl(cntv, t, 64);
-                    float* o = sums[qs + t].S;
-                    if (own && kq < 2) *(float4*)(o + 4 * kq) = make_float4(acc1[0], acc1[1], acc1[2], acc1[3]);
-                    if (own && kq == 2) *(float4*)(o + 8) = make_float4(acc1[0], __int_as_float(n_t), 0.f, 0.f);
+                    float4 v = make_float4(acc1[0], acc1[1], acc1[2], acc1[3]);
+                    if (kq == 2) v = make_float4(acc1[0], __int_as_float(n_t), __uint_as_float(cid), 0.f);
+                    if (kq == 3) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (own) *((float4*)(sums + caller) + kq) = v;
                 }
             }
             wave_sync();  // s_row and the block's LDS are rewritten by the next cell
@@ -464,11 +470,11 @@ __device__ inline bool h16_plane(const double C[9], double xa, double ya, double
 
 // the fp64 covariance S P P^T - n mu mu^T and the absolute mean (the query cell's centre + mu) of
 // sorted point s from its sums
-__device__ inline void mx_cov(const H16Args& a, int64_t s, const MxSums& q, double C[9], double& xa, double& ya,
+__device__ inline void mx_cov(const H16Args& a, uint32_t cid, const MxSums& q, double C[9], double& xa, double& ya,
                               double& za) {
     const GridDesc& g = a.g;
     int cx, cy, cz;
-    cell_xyz(g, a, a.cell[s], cx, cy, cz);
+    cell_xyz(g, a, cid, cx, cy, cz);
     const double nn = (double)q.n;
     const double m0 = q.S[0] / nn, m1 = q.S[1] / nn, m2 = q.S[2] / nn;
     C[0] = q.S[3] - nn * m0 * m0; C[1] = q.S[4] - nn * m0 * m1; C[2] = q.S[5] - nn * m0 * m2;
@@ -480,39 +486,45 @@ __device__ inline void mx_cov(const H16Args& a, int64_t s, const MxSums& q, doub
     za = g.o[2] + (double)cz * g.h + hh + m2;
 }
 
-// the rows h16_plane left to the Jacobi core
+// the rows h16_plane left to the Jacobi core (caller indices)
 __global__ __launch_bounds__(kB) void k_h16_mx_planes_fb(H16Args a, const MxSums* __restrict__ sums,
                                                          const int64_t* __restrict__ list,
                                                          const uint32_t* __restrict__ nlist, pcp_plane* __restrict__ out_nrm) {
     const uint32_t m = *nlist;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        const int64_t s = list[i];
+        const int64_t c = list[i];
+        const MxSums q = sums[c];
         double C[9], xa, ya, za;
-        mx_cov(a, s, sums[s], C, xa, ya, za);
+        mx_cov(a, q.cell, q, C, xa, ya, za);
         pcp_plane pl;
         plane_from_cov(C, xa, ya, za, pl);
-        out_nrm[a.mapping[s]] = pl;
+        out_nrm[c] = pl;
     }
 }
 
-// the planes of k_h16_mx's sums (sorted order)
+// the planes of k_h16_mx's sums, in caller order (sequential reads and writes)
 __global__ __launch_bounds__(kB) void k_h16_mx_planes(H16Args a, const MxSums* __restrict__ sums,
+                                                      const int64_t* __restrict__ offsets,
                                                       pcp_plane* __restrict__ out_nrm, int64_t* __restrict__ fb,
                                                       uint32_t* __restrict__ nfb) {
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < a.n; s += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t caller = a.mapping[s];
-        if (caller >= a.n_owned) continue;
-        const MxSums q = sums[s];
+    for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < a.n_owned;
+         c += (int64_t)gridDim.x * blockDim.x) {
+        // the reads issued together (one memory round trip per point; the compiler otherwise sinks
+        // the record's loads into the branch below)
+        const int64_t o0 = offsets[c], o1 = offsets[c + 1];
+        const MxSums q = sums[c];
+        asm volatile("" ::"v"(o0), "v"(o1), "v"(q.n));
+        if (o1 == o0) continue;  // a point the build dropped: no record, the default plane is set
         pcp_plane pl{0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
         if (q.n > 3) {  // rows of 3 points or fewer keep the default plane (the F1 guard, N > 3)
             double C[9], xa, ya, za;
-            mx_cov(a, s, q, C, xa, ya, za);
+            mx_cov(a, q.cell, q, C, xa, ya, za);
             if (!h16_plane(C, xa, ya, za, pl)) {
-                fb[atomicAdd(nfb, 1u)] = s;
+                fb[atomicAdd(nfb, 1u)] = c;
                 continue;
             }
         }
-        out_nrm[caller] = pl;
+        out_nrm[c] = pl;
     }
 }
 
@@ -621,7 +633,7 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
         pcp_ctx* c; int32_t** a; MxSums** b; int64_t** d;
         ~Free() { dfree(c, *a); dfree(c, *b); dfree(c, *d); }
     } fr{ctx, &ids, &sm, &fb};
-    if (normals_dev) PCP_TRY(dmalloc(ctx, &sm, (size_t)ix->n));
+    if (normals_dev) PCP_TRY(dmalloc(ctx, &sm, (size_t)n_owned));
     // the reported ids: the caller indices (the index's own mapping), or their global ids
     const int32_t* rep_ids = ix->mapping;
     if (global_id_dev) {
@@ -633,11 +645,11 @@ int pcp_h16_radius_fill(pcp_ctx* ctx, const pcp_index* ix, float radius, int64_t
     hipLaunchKernelGGL(k_h16_mx<true>, dim3(mx_blocks(ix->n)), dim3(64), 0, ctx->stream, a, (int32_t*)nullptr,
                        offsets_dev, rep_ids, idx_dev, sm);
     if (normals_dev) {
-        PCP_TRY(dmalloc(ctx, &fb, (size_t)ix->n + 1));
-        uint32_t* nfb = (uint32_t*)(fb + ix->n);
+        PCP_TRY(dmalloc(ctx, &fb, (size_t)n_owned + 1));
+        uint32_t* nfb = (uint32_t*)(fb + n_owned);
         PCP_HIP(ctx, hipMemsetAsync(nfb, 0, sizeof(uint32_t), ctx->stream));
-        hipLaunchKernelGGL(k_h16_mx_planes, dim3(grid_for(ix->n, kB)), dim3(kB), 0, ctx->stream, a, (const MxSums*)sm,
-                           normals_dev, fb, nfb);
+        hipLaunchKernelGGL(k_h16_mx_planes, dim3(grid_for(n_owned, kB)), dim3(kB), 0, ctx->stream, a,
+                           (const MxSums*)sm, offsets_dev, normals_dev, fb, nfb);
         hipLaunchKernelGGL(k_h16_mx_planes_fb, dim3(256), dim3(kB), 0, ctx->stream, a, (const MxSums*)sm,
                            (const int64_t*)fb, (const uint32_t*)nfb, normals_dev);
     }

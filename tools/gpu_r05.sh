@@ -70,6 +70,11 @@ c5pmc)
     i=$((i+1))
   done
   python3 tools/pmc_table.py $O/c5pmc k_h16 > $O/c5pmc/table.txt 2>&1 ;;
+c5order)
+  for rep in 1 2; do
+    timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_native.jsonl 2>> $O/c5_ab.err
+    timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 --c5-order cells >> $O/c5_ab_cells.jsonl 2>> $O/c5_ab.err
+  done ;;
 esac
 echo "step $st done" >> $O/steps.log
 done
