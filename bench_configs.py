@@ -336,6 +336,8 @@ def cfg_c5(ctx, args, rank, timer):
            f"(halo) and writes its owned points' rows (global ids) and planes; no collective") if world > 1 else \
         "x1"
     info = {"unit": "Mpoints/s", "units_per_step": n_owned, "units_all_ranks_per_step": n,
+            "data": "synthetic street scene (seeded)" + ("; one scene split into x-slabs across the ranks"
+                                                         if world > 1 else ""),
             "scaling": "strong" if world > 1 else "weak", "parallelism": par,
             "dtype": "fp16 coords / f32 accum",
             "pmc_key": {"n": n, "world": world},
@@ -472,7 +474,7 @@ def main(args):
         "scaling": info.get("scaling", "weak"),
         "vs_baseline": None,
         "dtype": info["dtype"],
-        "data": "synthetic (seeded); every rank its own batch",
+        "data": info.get("data", "synthetic (seeded)" + ("; every rank its own batch" if world > 1 else "")),
         "config": {"workload": info["workload"],
                    "parallelism": info.get("parallelism", f"x{world} independent batches, no collective")},
         "per_rank": per_rank,

@@ -75,6 +75,11 @@ c5order)
     timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_native.jsonl 2>> $O/c5_ab.err
     timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 --c5-order cells >> $O/c5_ab_cells.jsonl 2>> $O/c5_ab.err
   done ;;
+rehearsal)
+  # N = 2 on ONE GPU over gloo (the driver owns the 8-GPU runs): the C4 line and a 50M C5 line
+  # with the slab-vs-single-process row check
+  PCP_BENCH_DEVICE=0 PCP_BENCH_BACKEND=gloo timeout -k 10 600 python3 -u bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu > $O/rehearsal_c4_2rank.json 2> $O/rehearsal_c4.err
+  PCP_BENCH_DEVICE=0 PCP_BENCH_BACKEND=gloo timeout -k 10 600 python3 -u bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu --config C5 --c5-points 50000000 --c5-check 20000 > $O/rehearsal_c5_2rank.json 2> $O/rehearsal_c5.err ;;
 esac
 echo "step $st done" >> $O/steps.log
 done
