@@ -128,7 +128,7 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_
  * features with fp32 accumulation): pairs within 3e-4 m of the radius may differ from an exact
  * search (the fp16 offsets' quantisation).  n_owned must not exceed the indexed
  * cloud's size (PCP_ERR_ARG).
- * Memory: the fill takes ~48 B per indexed point of scratch for the plane sums (with normals),
+ * Memory: the fill takes 64 B per owned point of scratch for the plane sums (with normals),
  * released when it returns; neither call keeps state in the index between calls, so calls on
  * one index from different threads only need the context's usual serialisation. */
 int pcp_index_build_h16(pcp_ctx* ctx, const float* xyz_dev, size_t stride_bytes, int64_t n,

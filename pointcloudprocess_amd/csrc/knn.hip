@@ -21,6 +21,9 @@
 #include "topk.hpp"
 #include "pca.hpp"
 
+#ifndef PCP_NORMALS_STATS
+#define PCP_NORMALS_STATS 0  // profiling builds: per-phase counters of pcp_normals_knn on stderr
+#endif
 namespace pcp {
 namespace {
 
@@ -97,6 +100,9 @@ __device__ __forceinline__ const double* qptr(const double* q, size_t stride, in
 struct FarList {
     int32_t* list;
     uint32_t* count;
+    // optional, per entry: an upper bound on the query's exact k-th d2 (the k-th exact d2 of a
+    // set of k points the earlier pass already holds), so the next pass prunes from the start
+    double* ub = nullptr;
 };
 
 // Deferred queries are few but each is expensive, so the far pass gives every one its own
@@ -110,7 +116,11 @@ template <bool FAR>
 __device__ __forceinline__ int64_t work_item(const FarList& f, int64_t w) {
     return (FAR && f.list) ? (int64_t)f.list[w >> 6] : w;
 }
-__device__ __forceinline__ void defer(const FarList& f, int64_t i) { f.list[atomicAdd(f.count, 1u)] = (int32_t)i; }
+__device__ __forceinline__ void defer(const FarList& f, int64_t i, double ub = INFINITY) {
+    const uint32_t at = atomicAdd(f.count, 1u);
+    f.list[at] = (int32_t)i;
+    if (f.ub) f.ub[at] = ub;
+}
 
 // K3: batch nearestKSearch.  Rows ascending by (d2, internal j), indices mapped through
 // index_mapping_ (kd_tree.h:837-842); entries past min(k, size) are -1 / +inf.
@@ -265,7 +275,7 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     uint32_t t = 0;  // the wave's cell / brick counter: item t belongs to lane t % 64
     for (int s = 0; s <= smax + 1; s++) {
         if (s > 0) {
-            v.shared = PCP_COOP_KTH_BISECT ? fmin(v.shared, kth_bound<K>(v.top, kk)) : global_kth<K>(v.top, kk, lane);
+            v.shared = fmin(v.shared, PCP_COOP_KTH_BISECT ? kth_bound<K>(v.top, kk) : global_kth<K>(v.top, kk, lane));
             const double rmin = (double)(s - 1) + dmin - mc;
             if (rmin > 0 && rmin * rmin * h2 > v.ubound()) return;
         }
@@ -314,7 +324,7 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     for (int sb = farb; sb <= sbmax; sb++) {
         if (shells) (*shells)++;
         const long long c0 = tk ? (long long)clock64() : 0;
-        v.shared = PCP_COOP_KTH_BISECT ? fmin(v.shared, kth_bound<K>(v.top, kk)) : global_kth<K>(v.top, kk, lane);
+        v.shared = fmin(v.shared, PCP_COOP_KTH_BISECT ? kth_bound<K>(v.top, kk) : global_kth<K>(v.top, kk, lane));
         if (tk) tk[1] += (long long)clock64() - c0;
         if (sb > 0) {
             const double rmin = (double)(4 * (sb - 1)) + bdmin - mc;
@@ -568,6 +578,7 @@ __global__ __launch_bounds__(kB) void k_normals_coop(GridDesc g, const double4* 
         v.pts = pts;
         v.qx = qp.x; v.qy = qp.y; v.qz = qp.z;
         v.top.init(kk);
+        if (far.ub) v.shared = far.ub[w];  // the earlier passes' k-th: pruning from the first ring
         int shells = 0;
         const long long t0 = dbg ? (long long)clock64() : 0;
         long long tk[5] = {t0, 0, 0, 0, 0};
@@ -834,7 +845,8 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
                               ? row_window_search<KnnVisitor<K>>(g, v.qx, v.qy, v.qz, mc, v)
                               : ring_search<double, KnnVisitor<K>, FAR>(g, v.qx, v.qy, v.qz, mc, v);
         if (!done) {
-            defer(far, s);
+            // the tile's bound or the window's own k-th, whichever is smaller
+            defer(far, s, fmin((!FAR && in.ub) ? in.ub[w] : INFINITY, v.top.kth()));
             continue;
         }
         const int jq = (int)qp.w;
@@ -1290,7 +1302,7 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                 if (i == kk - 1) dk = D[i];
             if (!valid) continue;
             if (!(dk < lb && dk < b2)) {
-                defer(far, s);
+                defer(far, s, dk);  // dk: the k-th exact d2 of the kept points, an upper bound
                 if (stats) atomicAdd(stats + (dk < lb ? 2 : 0), 1ull);
                 continue;
             }
@@ -1507,11 +1519,12 @@ int centroid_aos48_dev(pcp_ctx* ctx, const void* in, int64_t n, int is_dense, do
 struct FarBuf {
     FarList f{nullptr, nullptr};
     pcp_ctx* ctx = nullptr;
-    ~FarBuf() { dfree(ctx, f.list); dfree(ctx, f.count); }
-    int alloc(pcp_ctx* c, int64_t n) {
+    ~FarBuf() { dfree(ctx, f.list); dfree(ctx, f.count); dfree(ctx, f.ub); }
+    int alloc(pcp_ctx* c, int64_t n, bool with_ub = false) {
         ctx = c;
         PCP_TRY(dmalloc(ctx, &f.list, n));
         PCP_TRY(dmalloc(ctx, &f.count, 1));
+        if (with_ub) PCP_TRY(dmalloc(ctx, &f.ub, n));
         PCP_HIP(ctx, hipMemsetAsync(f.count, 0, sizeof(uint32_t), ctx->stream));
         return PCP_OK;
     }
@@ -1633,10 +1646,14 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
     const double mc = cell_margin64(ix->g);
     const double4* pts = (const double4*)ix->pts;
     FarBuf fb;
-    PCP_TRY(fb.alloc(ctx, ix->n));
+    PCP_TRY(fb.alloc(ctx, ix->n, true));
     const int tile_R = kk <= 8 ? 1 : 2;  // the tile's window half-width in cells
     if (ix->g.dense) {
-        unsigned long long* st = nullptr;  // (per-phase counters of profiling builds)
+        unsigned long long* st = nullptr;  // per-phase counters of profiling builds (PCP_NORMALS_STATS)
+#if PCP_NORMALS_STATS
+        PCP_TRY(dmalloc(ctx, &st, 24));
+        PCP_HIP(ctx, hipMemsetAsync(st, 0, 24 * sizeof(unsigned long long), ctx->stream));
+#endif
         const unsigned nbt = (unsigned)std::min<int64_t>((ix->n + 63) / 64, 1 << 20);
         // brick order of the queries: (brick key, sorted position) radix-sorted
         uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *order = nullptr;
@@ -1666,7 +1683,7 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         PCP_TRY(dmalloc(ctx, (char**)&tmp, tb));
         PCP_HIP(ctx, rocprim::radix_sort_pairs(tmp, tb, k0, k1, v0, order, (size_t)ix->n, 0u, bits, ctx->stream));
         FarBuf fb2;  // the near pass's own deferred queries
-        PCP_TRY(fb2.alloc(ctx, ix->n));
+        PCP_TRY(fb2.alloc(ctx, ix->n, true));
         // the tile's uncertified queries: the lane-per-query near pass (cell rings), its own
         // deferrals then the wave-per-query pass (PCP_NORMALS_NEAR_DEFAULT; 0: all of them straight
         // to the wave-per-query pass, measured slower)
@@ -1690,6 +1707,24 @@ int pcp_normals_knn(pcp_ctx* ctx, const pcp_index* ix, int k, pcp_plane* out, in
         }
 #undef LAUNCH_TILE
         PCP_LAUNCH_CHECK(ctx);
+#if PCP_NORMALS_STATS
+        {
+            unsigned long long h[24];
+            unsigned c1 = 0, c2 = 0;
+            PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            PCP_HIP(ctx, hipMemcpy(h, st, sizeof(h), hipMemcpyDeviceToHost));
+            PCP_HIP(ctx, hipMemcpy(&c1, fb.f.count, 4, hipMemcpyDeviceToHost));
+            PCP_HIP(ctx, hipMemcpy(&c2, fb2.f.count, 4, hipMemcpyDeviceToHost));
+            const unsigned long long* d = h + 4;
+            fprintf(stderr, "normals stats: n=%lld k=%d tile deferred %u (list bound %llu, box %llu, oversize %llu), "
+                    "near deferred %u; far pass: %llu queries, shells mean %.1f max %llu, cycles mean %.0f max %llu "
+                    "(slowest: ring %llu, kth %llu, bricks %llu, rows+points %llu, mid-shell %llu; at %.2f %.2f %.2f)\n",
+                    (long long)ix->n, k, c1, h[0], h[2], h[1], c2, d[0], d[0] ? (double)d[1] / d[0] : 0.0, d[2],
+                    d[0] ? (double)d[3] / d[0] : 0.0, d[4], d[11], d[12], d[13], d[14], d[15],
+                    __builtin_bit_cast(double, d[5]), __builtin_bit_cast(double, d[6]), __builtin_bit_cast(double, d[7]));
+            dfree(ctx, st);
+        }
+#endif
         return PCP_OK;
     }
 #define LAUNCH_NRM(KV)                                                                                              \

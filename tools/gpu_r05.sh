@@ -75,6 +75,21 @@ c5order)
     timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_native.jsonl 2>> $O/c5_ab.err
     timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 --c5-order cells >> $O/c5_ab_cells.jsonl 2>> $O/c5_ab.err
   done ;;
+pmc)
+  # SQ / traffic counters of one bench config: CFG (C2, C3, C5 ...), KEYS = kernel substrings
+  sq1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_VALU"
+  sq2="SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
+  sq3="SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_LDS_IDX_ACTIVE"
+  P=$O/pmc_$CFG; mkdir -p $P
+  i=0
+  for c in "$sq1" "$sq2" "$sq3" "WRITE_SIZE" "FETCH_SIZE"; do
+    timeout -s KILL 200 rocprofv3 --pmc $c --output-format csv -d $P/p$i -o run -- python3 bench.py --config $CFG --no-cpu --steps 1 --warmup 0 $ARGS > $P/p$i.log 2>&1
+    i=$((i+1))
+  done
+  python3 tools/pmc_table.py $P $KEYS > $P/table.txt 2>&1 ;;
+trace)
+  # kernel trace + stats of one bench config: CFG, ARGS
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$CFG -o run -- python3 bench.py --config $CFG --no-cpu --steps 3 --warmup 1 $ARGS > $O/trace_$CFG.log 2>&1 ;;
 rehearsal)
   # N = 2 on ONE GPU over gloo (the driver owns the 8-GPU runs): the C4 line and a 50M C5 line
   # with the slab-vs-single-process row check
