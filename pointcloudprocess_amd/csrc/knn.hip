@@ -172,6 +172,12 @@ struct CoopVisitor {
     TopK<K> top;
     __device__ double bound() const { return fmin(top.kth(), shared) * (1.0 + 1e-12); }
     __device__ double ubound() const { return shared * (1.0 + 1e-12); }
+    // a point beyond the wave's shared bound (an upper bound on the global k-th) cannot be in
+    // the result: only the cheap compare, not the K-slot insertion (which a lane's own list,
+    // empty until it has seen k points, would otherwise take for every point)
+    __device__ __forceinline__ void take(double d, int j) {
+        if (d <= shared * (1.0 + 1e-12)) top.push(d, j);
+    }
     __device__ void visit(uint32_t s, uint32_t e) {
         constexpr int U = PCP_COOP_VISIT_BATCH;
         uint32_t t = s;
@@ -181,12 +187,12 @@ struct CoopVisitor {
 #pragma unroll
                 for (int u = 0; u < U; u++) p[u] = pts[t + u];
 #pragma unroll
-                for (int u = 0; u < U; u++) top.push(l2_simple(qx, qy, qz, p[u]), (int)p[u].w);
+                for (int u = 0; u < U; u++) take(l2_simple(qx, qy, qz, p[u]), (int)p[u].w);
             }
         }
         for (; t < e; t++) {
             const double4 p = pts[t];
-            top.push(l2_simple(qx, qy, qz, p), (int)p.w);
+            take(l2_simple(qx, qy, qz, p), (int)p.w);
         }
     }
 };
@@ -318,6 +324,12 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     __shared__ uint16_t s_rows[kB / 64][64 * 8 * 16];  // per wave: their non-empty rows (brick << 4 | row)
     int4* const flat = s_flat[threadIdx.x >> 6];
     uint16_t* const rows = s_rows[threadIdx.x >> 6];
+    __shared__ uint32_t s_fr[kB / 64][4][64];  // per wave: a row chunk's point-range prefix, starts, lengths
+    uint32_t* const f_pre = s_fr[threadIdx.x >> 6][0];
+    uint32_t* const f_s1 = s_fr[threadIdx.x >> 6][1];
+    uint32_t* const f_l1 = s_fr[threadIdx.x >> 6][2];
+    uint32_t* const f_s2 = s_fr[threadIdx.x >> 6][3];
+    constexpr int kFlatU = 4;  // points per lane in flight
 #endif
     // rings closer than `farb` lie wholly outside the grid (a query far away from it)
     if (tk) tk[0] = clock64();
@@ -438,31 +450,79 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (uint32_t ir = (uint32_t)lane; ir < nrow; ir += 64) {
-                const uint32_t it = rows[ir];
-                const int4 bk = flat[it >> 4];
-                const int y = 4 * bk.y + (int)(it & 3), z = 4 * bk.z + (int)((it >> 2) & 3);
-                if (y >= g.n[1] || z >= g.n[2]) continue;
-                const double cyz2 = sq_gap(axis_gap<double>(z, cz, lz), mc) + sq_gap(axis_gap<double>(y, cy, ly), mc);
-                if (cyz2 * h2 > v.bound()) continue;
-                const bool yzin = abs(z - cz) <= kCellRings && abs(y - cy) <= kCellRings;
-                int xa = 4 * bk.x, xe = min(4 * bk.x + 3, g.n[0] - 1);
-                while (xa <= xe && (cyz2 + sq_gap(axis_gap<double>(xa, cx, lx), mc)) * h2 > v.bound()) xa++;
-                while (xe >= xa && (cyz2 + sq_gap(axis_gap<double>(xe, cx, lx), mc)) * h2 > v.bound()) xe--;
-                if (xa > xe) continue;
-                const int64_t r0 = g.dense ? dense_id(g, 0, y, z) : (int64_t)bk.w * 64 + local_of(0, y, z);
-                auto run = [&](int x0, int x1) {  // cells [x0, x1] of this row
-                    if (x0 > x1) return;
-                    const int64_t c0 = g.dense ? r0 + x0 : r0 + (x0 & 3);
-                    const uint32_t st = g.cstart[c0], en = g.cstart[c0 + (x1 - x0) + 1];
-                    if (en > st) v.visit(st, en);
-                };
-                if (yzin) {
-                    run(xa, min(xe, cx - kCellRings - 1));
-                    run(max(xa, cx + kCellRings + 1), xe);
-                } else {
-                    run(xa, xe);
+            // Rows in chunks of 64, one per lane: the lane resolves its row to at most two point
+            // ranges (one cstart round trip for the whole chunk), then the chunk's points are
+            // dealt flat over the lanes -- point p to lane p % 64, its range found by a binary
+            // search of the ranges' prefix in LDS -- so a long row no longer runs as one lane's
+            // serial chain of loads while the others wait.
+            for (uint32_t r0 = 0; r0 < nrow; r0 += 64) {
+                const uint32_t ir = r0 + (uint32_t)lane;
+                uint32_t s1 = 0, l1 = 0, s2 = 0, l2 = 0;
+                do {
+                    if (ir >= nrow) break;
+                    const uint32_t it = rows[ir];
+                    const int4 bk = flat[it >> 4];
+                    const int y = 4 * bk.y + (int)(it & 3), z = 4 * bk.z + (int)((it >> 2) & 3);
+                    if (y >= g.n[1] || z >= g.n[2]) break;
+                    const double cyz2 = sq_gap(axis_gap<double>(z, cz, lz), mc) + sq_gap(axis_gap<double>(y, cy, ly), mc);
+                    if (cyz2 * h2 > v.bound()) break;
+                    const bool yzin = abs(z - cz) <= kCellRings && abs(y - cy) <= kCellRings;
+                    int xa = 4 * bk.x, xe = min(4 * bk.x + 3, g.n[0] - 1);
+                    while (xa <= xe && (cyz2 + sq_gap(axis_gap<double>(xa, cx, lx), mc)) * h2 > v.bound()) xa++;
+                    while (xe >= xa && (cyz2 + sq_gap(axis_gap<double>(xe, cx, lx), mc)) * h2 > v.bound()) xe--;
+                    if (xa > xe) break;
+                    const int64_t rb = g.dense ? dense_id(g, 0, y, z) : (int64_t)bk.w * 64 + local_of(0, y, z);
+                    auto range = [&](int x0, int x1, uint32_t& st, uint32_t& len) {  // cells [x0, x1]
+                        if (x0 > x1) return;
+                        const int64_t c0 = g.dense ? rb + x0 : rb + (x0 & 3);
+                        st = g.cstart[c0];
+                        len = g.cstart[c0 + (x1 - x0) + 1] - st;
+                    };
+                    if (yzin) {
+                        range(xa, min(xe, cx - kCellRings - 1), s1, l1);
+                        range(max(xa, cx + kCellRings + 1), xe, s2, l2);
+                    } else {
+                        range(xa, xe, s1, l1);
+                    }
+                } while (false);
+                const uint32_t cnt = l1 + l2;
+                uint32_t inc = cnt;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t tv = (uint32_t)__shfl_up((int)inc, o, 64);
+                    if (lane >= o) inc += tv;
                 }
+                const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+                f_pre[lane] = inc - cnt;
+                f_s1[lane] = s1;
+                f_l1[lane] = l1;
+                f_s2[lane] = s2;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (uint32_t p0 = 0; p0 < tot; p0 += 64u * kFlatU) {  // wave-uniform
+                    uint32_t idx[kFlatU];
+#pragma unroll
+                    for (int u = 0; u < kFlatU; u++) {
+                        const uint32_t pp = p0 + (uint32_t)lane + 64u * u;
+                        // the owner: the last lane whose prefix is <= pp (an empty lane shares its
+                        // prefix with the next, so the last one is the non-empty owner)
+                        int o = 0;
+#pragma unroll
+                        for (int b = 32; b >= 1; b >>= 1) o += f_pre[o + b] <= pp ? b : 0;
+                        const uint32_t off = pp - f_pre[o], a1 = f_l1[o];
+                        idx[u] = pp < tot ? (off < a1 ? f_s1[o] + off : f_s2[o] + (off - a1)) : ~0u;
+                    }
+                    double4 q4[kFlatU];
+#pragma unroll
+                    for (int u = 0; u < kFlatU; u++) q4[u] = v.pts[idx[u] != ~0u ? idx[u] : 0u];
+#pragma unroll
+                    for (int u = 0; u < kFlatU; u++)
+                        if (idx[u] != ~0u) v.take(l2_simple(v.qx, v.qy, v.qz, q4[u]), (int)q4[u].w);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next chunk rewrites f_*
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next batch rewrites flat[]
             __builtin_amdgcn_wave_barrier();
