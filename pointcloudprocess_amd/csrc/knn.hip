@@ -71,8 +71,13 @@ struct KnnVisitor {
     const double4* pts;
     double qx, qy, qz;
     TopK<K> top;
+    // a known upper bound on the query's k-th d2 (the tile's: k points it already holds), or inf
+    double cap = INFINITY;
     // pruning radius^2 (1e-12 covers the rounding of the cell-box bound and of d2)
-    __device__ double bound() const { return top.kth() * (1.0 + 1e-12); }
+    __device__ double bound() const { return fmin(top.kth(), cap) * (1.0 + 1e-12); }
+    __device__ __forceinline__ void take(double d, int j) {
+        if (d <= cap * (1.0 + 1e-12)) top.push(d, j);
+    }
     __device__ void visit(uint32_t s, uint32_t e) {
         uint32_t t = s;
         for (; t + U <= e; t += U) {
@@ -80,11 +85,11 @@ struct KnnVisitor {
 #pragma unroll
             for (int u = 0; u < U; u++) p[u] = pts[t + u];
 #pragma unroll
-            for (int u = 0; u < U; u++) top.push(l2_simple(qx, qy, qz, p[u]), (int)p[u].w);
+            for (int u = 0; u < U; u++) take(l2_simple(qx, qy, qz, p[u]), (int)p[u].w);
         }
         for (; t < e; t++) {
             const double4 p = pts[t];
-            top.push(l2_simple(qx, qy, qz, p), (int)p.w);
+            take(l2_simple(qx, qy, qz, p), (int)p.w);
         }
     }
 };
@@ -896,6 +901,9 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
         v.pts = pts;
         v.qx = qp.x; v.qy = qp.y; v.qz = qp.z;
         v.top.init(kk);
+        // the tile's k-th: its kk points lie within its window (+-2 cells), inside this pass's
+        // window, so the walk below still finds kk points under the cap
+        if (ROWS && !FAR && in.ub) v.cap = in.ub[w];
         // the near pass over the tiled kernel's uncertified queries, on dense grids, walks the
         // window by rows (the queries are indexed points, so they lie inside the grid).  Not for
         // every point: a large k over a dense neighbourhood fills its list faster cell by cell
