@@ -269,6 +269,10 @@ __device__ double wave_kth_of_bests(const TopK<K>& top, int kk, int lane) {
     return __shfl(x, kk - 1, 64);
 }
 
+// bricks per lane per batch of the far pass's shells (8 spilled the K = 32 lists to scratch:
+// ~700 bytes per lane, every list update a round trip to memory)
+constexpr int kCoopBB = 4;
+
 template <int K>
 __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int lane, int kk,
                             int* shells = nullptr, long long* tk = nullptr) {
@@ -283,7 +287,59 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     far = max(far, max(cz - (g.n[2] - 1), -cz));
     const int rmax = far + max(g.n[0], max(g.n[1], g.n[2]));
     const int smax = min(rmax, kCellRings);
+    // Point ranges gathered one per lane (a cell, or a row's one or two runs), then their points
+    // dealt flat over the lanes -- point p to lane p % 64, its range found by a binary search of
+    // the ranges' prefix in LDS -- so no lane runs a long range as a serial chain of loads while
+    // the others wait.  Wave-uniform call.
+    __shared__ uint32_t s_fr[kB / 64][4][64];  // per wave: the ranges' prefix, starts, lengths
+    uint32_t* const f_pre = s_fr[threadIdx.x >> 6][0];
+    uint32_t* const f_s1 = s_fr[threadIdx.x >> 6][1];
+    uint32_t* const f_l1 = s_fr[threadIdx.x >> 6][2];
+    uint32_t* const f_s2 = s_fr[threadIdx.x >> 6][3];
+    constexpr int kFlatU = 2;  // points per lane in flight (4 spilled the K = 32 lists to scratch)
+    auto flat_visit = [&](uint32_t s1, uint32_t l1, uint32_t s2, uint32_t l2) {
+        const uint32_t cnt = l1 + l2;
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t tv = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane >= o) inc += tv;
+        }
+        const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+        if (tot == 0) return;
+        f_pre[lane] = inc - cnt;
+        f_s1[lane] = s1;
+        f_l1[lane] = l1;
+        f_s2[lane] = s2;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t p0 = 0; p0 < tot; p0 += 64u * kFlatU) {  // wave-uniform
+            uint32_t idx[kFlatU];
+#pragma unroll
+            for (int u = 0; u < kFlatU; u++) {
+                const uint32_t pp = p0 + (uint32_t)lane + 64u * u;
+                // the owner: the last lane whose prefix is <= pp (an empty lane shares its prefix
+                // with the next, so the last one is the non-empty owner)
+                int o = 0;
+#pragma unroll
+                for (int b = 32; b >= 1; b >>= 1) o += f_pre[o + b] <= pp ? b : 0;
+                const uint32_t off = pp - f_pre[o], a1 = f_l1[o];
+                idx[u] = pp < tot ? (off < a1 ? f_s1[o] + off : f_s2[o] + (off - a1)) : ~0u;
+            }
+            double4 q4[kFlatU];
+#pragma unroll
+            for (int u = 0; u < kFlatU; u++) q4[u] = v.pts[idx[u] != ~0u ? idx[u] : 0u];
+#pragma unroll
+            for (int u = 0; u < kFlatU; u++)
+                if (idx[u] != ~0u) v.take(l2_simple(v.qx, v.qy, v.qz, q4[u]), (int)q4[u].w);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next call rewrites f_*
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     uint32_t t = 0;  // the wave's cell / brick counter: item t belongs to lane t % 64
+    uint32_t rs = 0, rl = 0;  // this lane's pending cell range (flushed every 64 items)
     for (int s = 0; s <= smax + 1; s++) {
         if (s > 0) {
             v.shared = fmin(v.shared, PCP_COOP_KTH_BISECT ? kth_bound<K>(v.top, kk) : global_kth<K>(v.top, kk, lane));
@@ -306,13 +362,24 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
                 const int step = yface ? 1 : 2 * s;
                 for (int x = yface ? x0 : cx - s; x <= x1; x += (step > 0 ? step : 1)) {
                     if (x < x0) continue;
-                    if ((t++ & 63u) != (uint32_t)lane) continue;
-                    if ((gyz2 + sq_gap(axis_gap<double>(x, cx, lx), mc)) * h2 > v.bound()) continue;
-                    uint32_t st, en;
-                    if (cell_range(g, x, y, z, st, en)) v.visit(st, en);
+                    const bool mine = (t & 63u) == (uint32_t)lane;
+                    t++;
+                    if (mine && (gyz2 + sq_gap(axis_gap<double>(x, cx, lx), mc)) * h2 <= v.bound()) {
+                        uint32_t st, en;
+                        if (cell_range(g, x, y, z, st, en)) {
+                            rs = st;
+                            rl = en - st;
+                        }
+                    }
+                    if ((t & 63u) == 0u) {  // (uniform) a chunk of 64 cells: its points, flat
+                        flat_visit(rs, rl, 0u, 0u);
+                        rl = 0u;
+                    }
                 }
             }
         }
+        flat_visit(rs, rl, 0u, 0u);  // the ring's last partial chunk
+        rl = 0u;
     }
     if (rmax <= kCellRings) return;
     // bricks of 4x4x4 cells, rings outward, the cells phase 1 covered skipped
@@ -325,16 +392,10 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
     farb = max(farb, max(bz - (g.nb[2] - 1), -bz));
     const int sbmax = farb + max(g.nb[0], max(g.nb[1], g.nb[2]));
 #if PCP_COOP_FLAT
-    __shared__ int4 s_flat[kB / 64][64 * 8];  // per wave: a batch's occupied bricks {x, y, z, word}
-    __shared__ uint16_t s_rows[kB / 64][64 * 8 * 16];  // per wave: their non-empty rows (brick << 4 | row)
+    __shared__ int4 s_flat[kB / 64][64 * kCoopBB];  // per wave: a batch's occupied bricks {x, y, z, word}
+    __shared__ uint16_t s_rows[kB / 64][64 * kCoopBB * 16];  // per wave: their non-empty rows (brick << 4 | row)
     int4* const flat = s_flat[threadIdx.x >> 6];
     uint16_t* const rows = s_rows[threadIdx.x >> 6];
-    __shared__ uint32_t s_fr[kB / 64][4][64];  // per wave: a row chunk's point-range prefix, starts, lengths
-    uint32_t* const f_pre = s_fr[threadIdx.x >> 6][0];
-    uint32_t* const f_s1 = s_fr[threadIdx.x >> 6][1];
-    uint32_t* const f_l1 = s_fr[threadIdx.x >> 6][2];
-    uint32_t* const f_s2 = s_fr[threadIdx.x >> 6][3];
-    constexpr int kFlatU = 4;  // points per lane in flight
 #endif
     // rings closer than `farb` lie wholly outside the grid (a query far away from it)
     if (tk) tk[0] = clock64();
@@ -375,8 +436,7 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
         const int64_t total = area[0] + area[1] + area[2] + area[3] + area[4] + area[5];
         // bricks t = lane + 64 u: the occupancy words of a batch are loaded together (mostly
         // empty bricks around isolated queries: one dependent load each would serialise)
-        constexpr int kBB = 8;
-        static_assert(kBB == 8, "s_flat holds 64 * 8 bricks per wave");
+        constexpr int kBB = kCoopBB;
         for (int64_t base = 0; base < total; base += 64 * kBB) {  // wave-uniform trip count
             const long long cb0 = tk ? (long long)clock64() : 0;
             const int64_t t0 = base + lane;
@@ -490,44 +550,7 @@ __device__ void coop_search(const GridDesc& g, double mc, CoopVisitor<K>& v, int
                         range(xa, xe, s1, l1);
                     }
                 } while (false);
-                const uint32_t cnt = l1 + l2;
-                uint32_t inc = cnt;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t tv = (uint32_t)__shfl_up((int)inc, o, 64);
-                    if (lane >= o) inc += tv;
-                }
-                const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
-                f_pre[lane] = inc - cnt;
-                f_s1[lane] = s1;
-                f_l1[lane] = l1;
-                f_s2[lane] = s2;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (uint32_t p0 = 0; p0 < tot; p0 += 64u * kFlatU) {  // wave-uniform
-                    uint32_t idx[kFlatU];
-#pragma unroll
-                    for (int u = 0; u < kFlatU; u++) {
-                        const uint32_t pp = p0 + (uint32_t)lane + 64u * u;
-                        // the owner: the last lane whose prefix is <= pp (an empty lane shares its
-                        // prefix with the next, so the last one is the non-empty owner)
-                        int o = 0;
-#pragma unroll
-                        for (int b = 32; b >= 1; b >>= 1) o += f_pre[o + b] <= pp ? b : 0;
-                        const uint32_t off = pp - f_pre[o], a1 = f_l1[o];
-                        idx[u] = pp < tot ? (off < a1 ? f_s1[o] + off : f_s2[o] + (off - a1)) : ~0u;
-                    }
-                    double4 q4[kFlatU];
-#pragma unroll
-                    for (int u = 0; u < kFlatU; u++) q4[u] = v.pts[idx[u] != ~0u ? idx[u] : 0u];
-#pragma unroll
-                    for (int u = 0; u < kFlatU; u++)
-                        if (idx[u] != ~0u) v.take(l2_simple(v.qx, v.qy, v.qz, q4[u]), (int)q4[u].w);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next chunk rewrites f_*
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                flat_visit(s1, l1, s2, l2);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next batch rewrites flat[]
             __builtin_amdgcn_wave_barrier();

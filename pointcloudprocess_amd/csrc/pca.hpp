@@ -46,18 +46,22 @@ __device__ inline void eigen_sym3(const double Ain[9], double ev[3], double E[9]
             }
         }
     }
-    const double d[3] = {A[0], A[4], A[8]};
-    int ord[3] = {0, 1, 2};
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int jj = i + 1; jj < 3; jj++)
-            if (d[ord[jj]] > d[ord[i]]) { const int t = ord[i]; ord[i] = ord[jj]; ord[jj] = t; }
+    // eigenvalues descending (a 3-element exchange sort, swapping only on strictly greater), the
+    // eigenvectors as rows -- written with selects on the order, not with indices computed at run
+    // time (a runtime index puts the arrays in scratch memory)
+    const double d0 = A[0], d1 = A[4], d2 = A[8];
+    auto dsel = [&](int o) { return o == 0 ? d0 : (o == 1 ? d1 : d2); };
+    int o0 = 0, o1 = 1, o2 = 2;
+    if (dsel(o1) > dsel(o0)) { const int t = o0; o0 = o1; o1 = t; }
+    if (dsel(o2) > dsel(o0)) { const int t = o0; o0 = o2; o2 = t; }
+    if (dsel(o2) > dsel(o1)) { const int t = o1; o1 = o2; o2 = t; }
+    const int ord[3] = {o0, o1, o2};
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        ev[i] = d[ord[i]];
+        ev[i] = dsel(ord[i]);
 #pragma unroll
-        for (int r = 0; r < 3; r++) E[3 * i + r] = V[3 * r + ord[i]];
+        for (int r = 0; r < 3; r++)
+            E[3 * i + r] = ord[i] == 0 ? V[3 * r] : (ord[i] == 1 ? V[3 * r + 1] : V[3 * r + 2]);
     }
 }
 
@@ -66,17 +70,22 @@ __device__ inline void plane_from_cov(const double C[9], double xa, double ya, d
     eigen_sym3(C, ev, E);
     int nummin = 0, nummax = 0;  // calculate_feature.cpp:168-179
     double vmin = ev[0], vmax = ev[0];
+#pragma unroll
     for (int i = 0; i < 3; i++) {
         if (vmin > ev[i]) { vmin = ev[i]; nummin = i; }
         if (vmax < ev[i]) { vmax = ev[i]; nummax = i; }
     }
     double l1 = 0, l2 = 0, l3 = 0;  // :180-192
+#pragma unroll
     for (int i = 0; i < 3; i++) {
-        if (i == nummin) l3 = ev[nummin];
-        else if (i == nummax) l1 = ev[nummax];
+        if (i == nummin) l3 = ev[i];
+        else if (i == nummax) l1 = ev[i];
         else l2 = ev[i];
     }
-    double n[3] = {E[3 * nummin], E[3 * nummin + 1], E[3 * nummin + 2]};
+    // the eigenvector row of the smallest eigenvalue (selects, no runtime index)
+    double n[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) n[r] = nummin == 0 ? E[r] : (nummin == 1 ? E[3 + r] : E[6 + r]);
     int big = 0;
     for (int a = 1; a < 3; a++)
         if (fabs(n[a]) > fabs(n[big])) big = a;
