@@ -50,6 +50,12 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_TILE_MORTON  // tiled normals: queries in Morton order inside each brick (1) or index order (0)
 #define PCP_TILE_MORTON 1
 #endif
+#ifndef PCP_T_RB  // fp64 records per gather batch of the tiled normals' re-rank and PCA
+#define PCP_T_RB 8
+#endif
+#ifndef PCP_T_WB  // window rows per batch of cell-start loads (tiled normals)
+#define PCP_T_WB 5
+#endif
 #ifndef PCP_TILE_ROWTAB  // tiled normals: per-point row bytes in LDS (1) or binary searches of the row table (0)
 #define PCP_TILE_ROWTAB 1
 #endif
@@ -1018,6 +1024,10 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// keeps a loaded value live on every lane: a load whose result is only used under a per-lane
+// condition is otherwise sunk into a branch with its own wait, one round trip per load
+__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(double& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ int quant14(double v, double inv) {
     const double t = rint(v * inv);
     return (int)(t < 0.0 ? 0.0 : (t > (double)kTileQ ? (double)kTileQ : t));
@@ -1040,15 +1050,28 @@ __device__ __forceinline__ TileBox tile_box(const GridDesc& g, int cx, int cy, i
     b.total = 0xffffffffu;
     const int ext = max(max(b.x1 - b.x0, b.y1 - b.y0), b.z1 - b.z0) + 1;
     if (b.nrow > kTileRows || ext > kTileExt) return b;
+    // every row's cell starts first (unconditional loads of a clamped row: one round trip for
+    // the whole box), then the prefix sums
+    constexpr int kRowIt = kTileRows / 64;
+    uint32_t st_[kRowIt], en_[kRowIt];
+#pragma unroll
+    for (int it = 0; it < kRowIt; it++) {
+        const int r = it * 64 + lane;
+        const int rc = r < b.nrow ? r : 0;
+        const int y = b.y0 + rc % b.ny, z = b.z0 + rc / b.ny;
+        st_[it] = g.cstart[dense_id(g, b.x0, y, z)];
+        en_[it] = g.cstart[dense_id(g, b.x1, y, z) + 1];
+    }
+#pragma unroll
+    for (int it = 0; it < kRowIt; it++) pin(st_[it]), pin(en_[it]);
     uint32_t carry = 0;
-    for (int r0 = 0; r0 < b.nrow; r0 += 64) {
+#pragma unroll
+    for (int it = 0; it < kRowIt; it++) {
+        const int r0 = it * 64;
+        if (r0 >= b.nrow) break;
         const int r = r0 + lane;
-        uint32_t st = 0, cnt = 0;
-        if (r < b.nrow) {
-            const int y = b.y0 + r % b.ny, z = b.z0 + r / b.ny;
-            st = g.cstart[dense_id(g, b.x0, y, z)];
-            cnt = g.cstart[dense_id(g, b.x1, y, z) + 1] - st;
-        }
+        const uint32_t st = r < b.nrow ? st_[it] : 0u;
+        const uint32_t cnt = r < b.nrow ? en_[it] - st_[it] : 0u;
         uint32_t inc = cnt;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1105,7 +1128,7 @@ __global__ void k_brick_keys(GridDesc g, const double4* pts, int64_t n, int lb, 
 }
 
 template <int K>
-__global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* pts, const int32_t* mapping,
+__global__ __launch_bounds__(64, 2) void k_normals_tile(GridDesc g, const double4* pts, const int32_t* mapping,
                                                      int identity, int64_t n, int kk, int R, double mc,
                                                      pcp_plane* out, int64_t n_out, FarList far,
                                                      unsigned long long* stats, const uint32_t* order,
@@ -1130,7 +1153,11 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
         // does not fit even then takes the exact search.
         int grp = 0, G = 1;
         bool over = false;  // this lane's group does not fit: deferred
-        if (tile_box(g, cx, cy, cz, valid, R, lane, s_rs, s_rb, false).total > (uint32_t)kTileCap) {
+        // the whole wave's box, listed at once (the common case: no second pass of row starts)
+        wave_lds_fence();  // the previous chunk's readers are done with the lists
+        const TileBox bw = tile_box(g, cx, cy, cz, valid, R, lane, s_rs, s_rb, true);
+        const bool whole = bw.total <= (uint32_t)kTileCap;
+        if (!whole) {
             const int nbx = (g.n[0] + 7) >> kTileBrick, nby = (g.n[1] + 7) >> kTileBrick;
             const int bxq = clampi(cx, 0, g.n[0] - 1) >> kTileBrick, byq = clampi(cy, 0, g.n[1] - 1) >> kTileBrick,
                       bzq = clampi(cz, 0, g.n[2] - 1) >> kTileBrick;
@@ -1166,8 +1193,11 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
         for (int gi = 0; gi < G; gi++) {
             const bool mine = grp == gi && !over;
             if (!__ballot(mine && valid)) continue;  // an empty or deferred group
-            wave_lds_fence();  // the previous group's readers are done with the lists
-            const TileBox b = tile_box(g, cx, cy, cz, mine && valid, R, lane, s_rs, s_rb, true);
+            TileBox b = bw;
+            if (!whole) {
+                wave_lds_fence();  // the previous group's readers are done with the lists
+                b = tile_box(g, cx, cy, cz, mine && valid, R, lane, s_rs, s_rb, true);
+            }
             const uint32_t total = b.total;
             wave_lds_fence();
             // 14-bit fixed point relative to the box corner, one step for all three axes
@@ -1188,21 +1218,49 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
 #if PCP_TILE_ROWTAB
             // e advances by 64 per step, so each lane's row only moves forward: a short walk
             // instead of a binary search, and the row of every staged point is kept (one byte)
-            // for the re-rank's list index -> position lookups
+            // for the re-rank's list index -> position lookups.  kSB entries per lane per step:
+            // their rows first, then kSB unconditional loads (a lane past the list reads position
+            // 0), so a step waits on one round trip, not kSB
             int rw = 0;
-            for (uint32_t e = lane; e < total; e += 64) {
-                while (s_rb[rw + 1] <= e) rw++;
-                const int r = rw;
-                s_row[e] = (uint8_t)r;
-                const double4 p = pts[s_rs[r] + (e - s_rb[r])];
+            constexpr int kSB = 4;
+            for (uint32_t e0 = lane; e0 < total; e0 += 64 * kSB) {
+                uint32_t pi[kSB];
+#pragma unroll
+                for (int u = 0; u < kSB; u++) {
+                    const uint32_t e = e0 + 64u * u;
+                    const bool on = e < total;
+                    while (on && s_rb[rw + 1] <= e) rw++;
+                    if (on) s_row[e] = (uint8_t)rw;
+                    pi[u] = on ? s_rs[rw] + (e - s_rb[rw]) : 0u;
+                }
+                double px[kSB], py[kSB], pz[kSB];
+#pragma unroll
+                for (int u = 0; u < kSB; u++) {
+                    const double4* pp = pts + pi[u];
+                    px[u] = pp->x;
+                    py[u] = pp->y;
+                    pz[u] = pp->z;
+                }
+#pragma unroll
+                for (int u = 0; u < kSB; u++) {
+                    pin(px[u]), pin(py[u]), pin(pz[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kSB; u++) {
+                    const uint32_t e = e0 + 64u * u;
+                    if (e < total)
+                        s_u[e] = make_uint2((uint32_t)quant14(px[u] - ox, inv) | ((uint32_t)quant14(py[u] - oy, inv) << 16),
+                                            (uint32_t)quant14(pz[u] - oz, inv));
+                }
+            }
 #else
             for (uint32_t e = lane; e < total; e += 64) {
                 const int r = row_of(e);
                 const double4 p = pts[s_rs[r] + (e - s_rb[r])];
-#endif
                 s_u[e] = make_uint2((uint32_t)quant14(p.x - ox, inv) | ((uint32_t)quant14(p.y - oy, inv) << 16),
                                     (uint32_t)quant14(p.z - oz, inv));
             }
+#endif
             wave_lds_fence();
             const uint32_t qxy = (uint32_t)quant14(q.x - ox, inv) | ((uint32_t)quant14(q.y - oy, inv) << 16);
             const int qz = quant14(q.z - oz, inv);
@@ -1234,41 +1292,56 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
             if (lane_mode && R <= kLaneR) {
                 constexpr int kW = (2 * kLaneR + 1) * (2 * kLaneR + 1);
                 const int nwin = R >= 2 ? 25 : (R == 1 ? 9 : 1);
-                // the LDS run [a, b) of window row i, or a == b (empty / outside the box)
-                auto row_run = [&](int i, uint32_t& a, uint32_t& e2) {
-                    int y, z;
-                    window_row(i, y, z);
-                    y += cy;
-                    z += cz;
-                    a = e2 = 0;
-                    if (act && i < nwin && y >= b.y0 && y <= b.y1 && z >= b.z0 && z <= b.z1) {
-                        const int r = (y - b.y0) + (z - b.z0) * b.ny;
-                        const uint32_t ca = g.cstart[dense_id(g, wx0, y, z)];
-                        const uint32_t cb = g.cstart[dense_id(g, wx1, y, z) + 1];
-                        a = s_rb[r] + (ca - s_rs[r]);
-                        e2 = a + (cb - ca);
+                // the LDS run [a, e) of every window row as a | e << 16 (0: empty / outside the
+                // box).  The cell-start loads of all kW rows are unconditional (cell 0 for a row
+                // outside) and issued before any is used: one round trip, not one per row
+                // row (dy, dz) of the window: cell (wx0, cy + dy, cz + dz) = the lane's base cell
+                // plus a uniform offset (scalar: dy, dz are constants of the unrolled loop)
+                const int64_t cbase = act ? dense_id(g, wx0, cy, cz) : 0;
+                const int64_t sy = g.n[0], sz = (int64_t)g.n[0] * g.n[1];
+                const uint32_t xw = (uint32_t)(wx1 - wx0 + 1);
+                const int rbase = (cy - b.y0) + (cz - b.z0) * b.ny;
+                uint32_t run[kW];
+                constexpr int kWB = PCP_T_WB;  // rows per batch of cell-start loads
+#pragma unroll
+                for (int i0 = 0; i0 < kW; i0 += kWB) {
+                    uint32_t ca[kWB], cb[kWB], okm = 0;
+#pragma unroll
+                    for (int u = 0; u < kWB && i0 + u < kW; u++) {
+                        int dy, dz;
+                        window_row(i0 + u, dy, dz);
+                        const int y = cy + dy, z = cz + dz;
+                        const bool ok = act && i0 + u < nwin && y >= b.y0 && y <= b.y1 && z >= b.z0 && z <= b.z1;
+                        okm |= ok ? 1u << u : 0u;
+                        const int64_t c0 = ok ? cbase + dy * sy + dz * sz : 0;
+                        ca[u] = g.cstart[c0];
+                        cb[u] = g.cstart[ok ? c0 + xw : 0];
                     }
-                };
+#pragma unroll
+                    for (int u = 0; u < kWB && i0 + u < kW; u++) pin(ca[u]), pin(cb[u]);
+#pragma unroll
+                    for (int u = 0; u < kWB && i0 + u < kW; u++) {
+                        int dy, dz;
+                        window_row(i0 + u, dy, dz);
+                        const bool ok = (okm >> u) & 1u;
+                        const int r = ok ? rbase + dy + dz * b.ny : 0;
+                        const uint32_t a0 = s_rb[r] + (ca[u] - s_rs[r]);
+                        run[i0 + u] = ok && cb[u] > ca[u] ? a0 | ((a0 + (cb[u] - ca[u])) << 16) : 0u;
+                    }
+                }
                 uint32_t* s_w = reinterpret_cast<uint32_t*>(s_u);
                 int nr = 0, excl = 0;
                 if (2 * total + 64u * kW <= 2u * kTileCap) {
                     // room for a fixed kW-word region per lane at the end of the list (odd stride:
-                    // the lanes' reads of one slot fall in distinct banks): one pass of cell starts
+                    // the lanes' reads of one slot fall in distinct banks)
                     lane_path = true;
                     excl = 2 * kTileCap - 64 * kW + lane * kW;
-#pragma unroll 5
-                    for (int i = 0; i < kW; i++) {
-                        uint32_t a, e2;
-                        row_run(i, a, e2);
-                        if (e2 > a) s_w[excl + nr++] = a | (e2 << 16);
-                    }
+#pragma unroll
+                    for (int i = 0; i < kW; i++)
+                        if (run[i]) s_w[excl + nr++] = run[i];
                 } else {
-#pragma unroll 5
-                    for (int i = 0; i < kW; i++) {  // pass 1: this lane's non-empty rows
-                        uint32_t a, e2;
-                        row_run(i, a, e2);
-                        nr += e2 > a ? 1 : 0;
-                    }
+#pragma unroll
+                    for (int i = 0; i < kW; i++) nr += run[i] ? 1 : 0;  // this lane's non-empty rows
                     excl = nr;
 #pragma unroll
                     for (int o = 1; o < 64; o <<= 1) {
@@ -1280,13 +1353,10 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                     lane_path = 2 * total + (uint32_t)tot_rows <= 2u * kTileCap;
                     if (lane_path) {  // compacted after the staged points
                         excl += 2 * (int)total;
-                        int j = excl;  // pass 2 (the cell starts again, now from the caches): write them
-#pragma unroll 5
-                        for (int i = 0; i < kW; i++) {
-                            uint32_t a, e2;
-                            row_run(i, a, e2);
-                            if (e2 > a) s_w[j++] = a | (e2 << 16);
-                        }
+                        int j = excl;
+#pragma unroll
+                        for (int i = 0; i < kW; i++)
+                            if (run[i]) s_w[j++] = run[i];
                     }
                 }
                 if (lane_path) {
@@ -1343,7 +1413,11 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
             if (fz1 < g.n[2] - 1) bd = fmin(bd, g.o[2] + (double)(fz1 + 1) * g.h - q.z);
             bd -= mc * g.h + 1e-12 * (fabs(q.x) + fabs(q.y) + fabs(q.z) + 1.0);
             const double b2 = bd > 0.0 ? bd * bd * (1.0 - 1e-12) : (bd == INFINITY ? INFINITY : 0.0);
-            // exact FLANN re-rank of the kept candidates
+            // exact FLANN re-rank of the kept candidates.  The fp64 records are gathered in
+            // batches of kRB unconditional loads (a slot without a candidate reads position 0 and
+            // is discarded), so a wave waits on M / kRB round trips instead of one per candidate
+            // (a load under a per-lane condition is a branch with its own wait).
+            constexpr int kRB = PCP_T_RB;
             double D[M];
             uint32_t P[M];
 #pragma unroll
@@ -1356,7 +1430,25 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
                 const int r = row_of(has ? ei : 0u);
 #endif
                 P[i] = has ? s_rs[r] + (ei - s_rb[r]) : 0u;
-                D[i] = has ? l2_simple(q.x, q.y, q.z, pts[P[i]]) : INFINITY;
+            }
+#pragma unroll
+            for (int i0 = 0; i0 < M; i0 += kRB) {
+                double px[kRB], py[kRB], pz[kRB];
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < M; u++) {
+                    const double4* pp = pts + P[i0 + u];
+                    px[u] = pp->x;
+                    py[u] = pp->y;
+                    pz[u] = pp->z;
+                }
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < M; u++) {
+                    pin(px[u]), pin(py[u]), pin(pz[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < M; u++)
+                    D[i0 + u] = t[i0 + u] != kMax ? l2_simple(q.x, q.y, q.z, make_double4(px[u], py[u], pz[u], 0.0))
+                                                  : INFINITY;
             }
             // every list point not kept: its quantised distance is >= sqrt(float(t[M] & ~2047))
             // steps (the int -> float rounding is covered by the 2^-20), and quantisation moves
@@ -1400,24 +1492,53 @@ __global__ __launch_bounds__(64) void k_normals_tile(GridDesc g, const double4* 
             const int jq = (int)q.w;
             const int64_t oi = identity ? jq : mapping[jq];
             if (oi >= n_out) continue;
-            // mean, sequential in kNN order (calculate_feature.cpp:131-142)
+            // mean, sequential in kNN order (calculate_feature.cpp:131-142); the records again in
+            // batches of unconditional loads (P[i] is a valid position for every i)
             double xa = 0, ya = 0, za = 0;
 #pragma unroll
-            for (int i = 0; i < K; i++) {
-                if (i < kk) {
-                    const double4 p = pts[P[i]];
-                    xa += p.x; ya += p.y; za += p.z;
+            for (int i0 = 0; i0 < K; i0 += kRB) {
+                double px[kRB], py[kRB], pz[kRB];
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < K; u++) {
+                    const double4* pp = pts + P[i0 + u];
+                    px[u] = pp->x;
+                    py[u] = pp->y;
+                    pz[u] = pp->z;
+                }
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < K; u++) {
+                    pin(px[u]), pin(py[u]), pin(pz[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < K; u++) {
+                    if (i0 + u < kk) {
+                        xa += px[u]; ya += py[u]; za += pz[u];
+                    }
                 }
             }
             xa /= kk; ya /= kk; za /= kk;
             double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
 #pragma unroll
-            for (int i = 0; i < K; i++) {
-                if (i < kk) {
-                    const double4 p = pts[P[i]];
-                    const double a0 = p.x - xa, a1 = p.y - ya, a2 = p.z - za;
-                    c00 += a0 * a0; c01 += a0 * a1; c02 += a0 * a2;
-                    c11 += a1 * a1; c12 += a1 * a2; c22 += a2 * a2;
+            for (int i0 = 0; i0 < K; i0 += kRB) {
+                double px[kRB], py[kRB], pz[kRB];
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < K; u++) {
+                    const double4* pp = pts + P[i0 + u];
+                    px[u] = pp->x;
+                    py[u] = pp->y;
+                    pz[u] = pp->z;
+                }
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < K; u++) {
+                    pin(px[u]), pin(py[u]), pin(pz[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kRB && i0 + u < K; u++) {
+                    if (i0 + u < kk) {
+                        const double a0 = px[u] - xa, a1 = py[u] - ya, a2 = pz[u] - za;
+                        c00 += a0 * a0; c01 += a0 * a1; c02 += a0 * a2;
+                        c11 += a1 * a1; c12 += a1 * a2; c22 += a2 * a2;
+                    }
                 }
             }
             const double C[9] = {c00, c01, c02, c01, c11, c12, c02, c12, c22};
