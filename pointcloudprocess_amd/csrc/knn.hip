@@ -50,6 +50,9 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_TILE_MORTON  // tiled normals: queries in Morton order inside each brick (1) or index order (0)
 #define PCP_TILE_MORTON 1
 #endif
+#ifndef PCP_T_SB  // staged points per lane per load batch (tiled normals)
+#define PCP_T_SB 4
+#endif
 #ifndef PCP_T_RB  // fp64 records per gather batch of the tiled normals' re-rank and PCA
 #define PCP_T_RB 8
 #endif
@@ -983,7 +986,7 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
 // (points outside the box).  Uncertified lanes go to the exact two-level search (the far pass
 // of k_normals), so the output is that of the exact path bit for bit.
 constexpr int kTileCap = 2048;   // union points per wave (11-bit list index)
-constexpr int kTileRows = 256;   // (y, z) rows per wave
+constexpr int kTileRows = 255;   // (y, z) rows per wave (255: the wave's LDS fits 8 waves per CU)
 constexpr int kTileQ = 16383;    // 14-bit fixed-point coordinates: squared distances fit in int32
 constexpr int kTileExt = 96;     // box extent (cells) cap: keeps the fixed-point step fine
 constexpr int kLaneR = 2;        // largest window half-width of the per-lane window scan
@@ -1052,7 +1055,7 @@ __device__ __forceinline__ TileBox tile_box(const GridDesc& g, int cx, int cy, i
     if (b.nrow > kTileRows || ext > kTileExt) return b;
     // every row's cell starts first (unconditional loads of a clamped row: one round trip for
     // the whole box), then the prefix sums
-    constexpr int kRowIt = kTileRows / 64;
+    constexpr int kRowIt = (kTileRows + 63) / 64;
     uint32_t st_[kRowIt], en_[kRowIt];
 #pragma unroll
     for (int it = 0; it < kRowIt; it++) {
@@ -1210,7 +1213,7 @@ __global__ __launch_bounds__(64, 2) void k_normals_tile(GridDesc g, const double
             auto row_of = [&](uint32_t e) {
                 int r = 0;
 #pragma unroll
-                for (int stp = kTileRows / 2; stp > 0; stp >>= 1)
+                for (int stp = (kTileRows + 1) / 2; stp > 0; stp >>= 1)
                     r = (r + stp < nrow && s_rb[r + stp] <= e) ? r + stp : r;
                 return r;
             };
@@ -1222,7 +1225,7 @@ __global__ __launch_bounds__(64, 2) void k_normals_tile(GridDesc g, const double
             // their rows first, then kSB unconditional loads (a lane past the list reads position
             // 0), so a step waits on one round trip, not kSB
             int rw = 0;
-            constexpr int kSB = 4;
+            constexpr int kSB = PCP_T_SB;
             for (uint32_t e0 = lane; e0 < total; e0 += 64 * kSB) {
                 uint32_t pi[kSB];
 #pragma unroll
