@@ -662,7 +662,7 @@ __global__ __launch_bounds__(kB) void k_knn_coop(GridDesc g, const double4* pts,
 }
 
 template <int K>
-__global__ __launch_bounds__(kB) void k_normals_coop(GridDesc g, const double4* pts, const int32_t* mapping,
+__global__ __launch_bounds__(kB, 2) void k_normals_coop(GridDesc g, const double4* pts, const int32_t* mapping,
                                                      int identity, const int32_t* pos_of_j, int kk, double mc,
                                                      pcp_plane* out, int64_t n_out, FarList far,
                                                      unsigned long long* dbg = nullptr) {
