@@ -240,6 +240,10 @@ def shard_range(n, world, rank):
 class GpuEngine:
     """libpcp engine: fp32 grid index over the local target (tile or shard) + the queries."""
 
+    # profiling only (bench.py --oct-lanes-list ...): (oct_lanes_first, oct_lanes_list, ring_lanes)
+    # passed to ICP.set_options on every new handle; None = the library's own choices
+    lane_options = None
+
     def __init__(self, ctx, target_xyz, query_xyz, cell_size=0.0):
         self.target = target_xyz.contiguous()
         # the index build and the query sort in one call (their radix sorts overlap on two streams)
@@ -249,6 +253,8 @@ class GpuEngine:
         else:  # (an A/B build of an older tree, PCP_LIB)
             self.index = ops.GridIndex(ctx, self.target, cell_size=cell_size)
             self.icp = ops.ICP(self.index, query_xyz.contiguous())
+        if GpuEngine.lane_options is not None:
+            self.icp.set_options(*GpuEngine.lane_options)
         self.device = ctx.device
         self.nq = query_xyz.shape[0]
 

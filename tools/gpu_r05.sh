@@ -11,6 +11,7 @@
 #   c3ab       interleaved A/B of the C3 bench line vs variants/$V for V in $VARS
 #   knntests   the kNN / normals tests and the full-size C3 check
 #   c2ab       interleaved A/B of the C2 bench line vs variants/$VAR
+#   octg       per-launch octant times at fixed search-list lanes per query (kernel traces)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-r05}; mkdir -p $O
@@ -90,6 +91,13 @@ pmc)
 trace)
   # kernel trace + stats of one bench config: CFG, ARGS
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$CFG -o run -- python3 bench.py --config $CFG --no-cpu --steps 3 --warmup 1 $ARGS > $O/trace_$CFG.log 2>&1 ;;
+octg)
+  # per-launch octant times with fixed lanes per query on the search lists (G = 1 2 4 8) and the
+  # default density rule (0): one registration each under a kernel trace
+  for G in 0 1 2 4 8; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/octg$G -o run -- python3 bench.py --no-cpu --steps 1 --warmup 0 --icp-lanes 0,$G,0 > $O/octg$G.log 2>&1
+    python3 tools/trace_iters.py $O/octg$G > $O/octg$G.txt 2>&1 || true
+  done ;;
 rehearsal)
   # N = 2 on ONE GPU over gloo (the driver owns the 8-GPU runs): the C4 line and a 50M C5 line
   # with the slab-vs-single-process row check
