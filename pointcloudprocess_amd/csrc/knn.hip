@@ -50,6 +50,9 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_TILE_MORTON  // tiled normals: queries in Morton order inside each brick (1) or index order (0)
 #define PCP_TILE_MORTON 1
 #endif
+#ifndef PCP_T_PF  // tiled normals: the next chunk's positions loaded a chunk ahead
+#define PCP_T_PF 1
+#endif
 #ifndef PCP_T_SB  // staged points per lane per load batch (tiled normals)
 #define PCP_T_SB 4
 #endif
@@ -1144,9 +1147,22 @@ __global__ __launch_bounds__(64, 2) void k_normals_tile(GridDesc g, const double
     __shared__ uint8_t s_row[kTileCap];  // the (y, z) row of each staged point
 #endif
     const int lane = threadIdx.x;
+#if PCP_T_PF
+    // the next chunk's sorted positions are loaded a chunk ahead (the chain order -> point ->
+    // cells -> rows -> staging starts one round trip shorter)
+    uint32_t s_next = blockIdx.x * 64 < n ? order[min((int64_t)blockIdx.x * 64 + lane, n - 1)] : 0u;
+#endif
     for (int64_t c = blockIdx.x; c * 64 < n; c += gridDim.x) {
         const bool valid = c * 64 + lane < n;
+#if PCP_T_PF
+        const int64_t s = s_next;  // a sorted position
+        {
+            const int64_t cn = c + gridDim.x;
+            if (cn * 64 < n) s_next = order[min(cn * 64 + lane, n - 1)];
+        }
+#else
         const int64_t s = order[valid ? c * 64 + lane : c * 64];  // a sorted position
+#endif
         const double4 q = pts[s];
         const int cx = cell_i<double>(g, q.x, 0), cy = cell_i<double>(g, q.y, 1), cz = cell_i<double>(g, q.z, 2);
         // Groups of lanes, each staged and scanned on its own: the whole wave when its box fits
