@@ -50,6 +50,9 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_TILE_MORTON  // tiled normals: queries in Morton order inside each brick (1) or index order (0)
 #define PCP_TILE_MORTON 1
 #endif
+#ifndef PCP_T_MX  // tiled normals: keys kept per lane beyond k (the re-rank's slack)
+#define PCP_T_MX 1
+#endif
 #ifndef PCP_T_PF  // tiled normals: the next chunk's positions loaded a chunk ahead
 #define PCP_T_PF 1
 #endif
@@ -980,7 +983,7 @@ __global__ __launch_bounds__(kB) void k_normals(GridDesc g, const double4* pts, 
 // The wave copies the union of its queries' neighbourhoods -- the box of their cells grown by
 // R cells, one contiguous point run per (y, z) row -- into LDS as fp32 coordinates relative to
 // the box corner plus the sorted position.  Every lane then scans the whole list (uniform trip
-// count, broadcast LDS reads, no divergence) keeping its M = K + 4 smallest packed keys
+// count, broadcast LDS reads, no divergence) keeping its M = K + PCP_T_MX (1) smallest packed keys
 // (bits(fp32 d2) & ~1023 | list index) and the (M+1)-th as a bound with a v_med3_u32 network
 // (M + 1 VALU ops per candidate instead of the fp64 register top-k's divergent shifts).  The
 // kept candidates are re-ranked by the exact FLANN fp64 (d2, j) and sorted; the lane's result
@@ -1139,7 +1142,7 @@ __global__ __launch_bounds__(64, 2) void k_normals_tile(GridDesc g, const double
                                                      pcp_plane* out, int64_t n_out, FarList far,
                                                      unsigned long long* stats, const uint32_t* order,
                                                      int lane_mode) {
-    constexpr int M = K + 4;
+    constexpr int M = K + PCP_T_MX;
     constexpr uint32_t kMax = 0xffffffffu;
     __shared__ uint2 s_u[kTileCap];
     __shared__ uint32_t s_rs[kTileRows], s_rb[kTileRows + 1];
