@@ -57,7 +57,9 @@ knntests)
 c2ab)
   for rep in 1 2; do
     timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_new.jsonl 2>> $O/c2_ab.err
-    PCP_LIB=variants/$VAR/libpcp.so timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_$VAR.jsonl 2>> $O/c2_ab.err
+    for V in ${VARS:-$VAR}; do
+      PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_$V.jsonl 2>> $O/c2_ab.err
+    done
   done ;;
 c5pmc)
   sq1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_VALU"
