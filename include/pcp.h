@@ -116,8 +116,8 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_
             int64_t nq, int k, int32_t* out_idx_dev, double* out_d2_dev);
 
 /* C5 (BASELINE configs[4]): fp16 cell-relative index + radius search with fused normals.
- * pcp_index_build_h16 sorts the cloud (fp32 xyz) into cells of `cell_size` (0 < h <= 0.5 m,
- * dense table) and stores each point as fp16 offsets from its cell origin (8 B) + its cell id.
+ * pcp_index_build_h16 sorts the cloud (fp32 xyz) into cells of `cell_size` (1 mm <= h <= 0.5 m:
+ * below 1 mm the metre offsets would reach fp16's subnormal range; PCP_ERR_UNSUPPORTED; dense table) and stores each point as fp16 offsets from its cell origin (8 B) + its cell id.
  * Queries are the indexed points whose caller index is < n_owned (the rest are a multi-GPU
  * slab's halo).  pcp_h16_radius_count: per owned point the number of points with d2 < r^2
  * (itself included), r <= cell size; pcp_scan_counts -> offsets; pcp_h16_radius_fill: the
@@ -125,7 +125,7 @@ int pcp_knn(pcp_ctx* ctx, const pcp_index* index, const double* q_dev, size_t q_
  * as global_id_dev[caller] (or the caller index when NULL), and optionally one F1 plane per
  * row (calculate_plan_parameter(cloud, radius), calculate_feature.h:15) from fp32 sums.
  * The hit test and the plane sums run on the matrix cores (fp32 d^2 - r^2 expansion, f16 moment
- * features with fp32 accumulation): pairs within 3e-4 m of the radius may differ from an exact
+ * features in cell units with fp32 accumulation): pairs within 3e-4 m of the radius may differ from an exact
  * search (the fp16 offsets' quantisation).  n_owned must not exceed the indexed
  * cloud's size (PCP_ERR_ARG).
  * Memory: the fill takes 64 B per owned point of scratch for the plane sums (with normals),
@@ -262,11 +262,12 @@ int pcp_icp_create_with_target(pcp_ctx* ctx, const float* target_dev, size_t tar
                                size_t q_stride_bytes, int64_t nq, pcp_index** index_out,
                                pcp_icp** icp_out);
 /* Test / profiling controls of an ICP handle (not needed by callers):
- *   oct_lanes_first, oct_lanes_list: lanes per query of the octant search pass at the first
- *     launch and over the later search lists (1, 2, 4, 8; 0 = by the list's density);
+ *   oct_lanes_first: lanes per query of the octant search pass at the first launch (1, 2, 4, 8;
+ *     0 = 1 lane); oct_lanes_list: the same over the later search lists (0 = by the list's density);
  *   ring_lanes: lanes per query of the fallback pass (1, 2, 4, 8; 0 = by the list's length);
  *   ablate: PCP_ICP_ABLATE_* flags that switch passes off for profiling -- results are WRONG
  *     while any is set.
+ * A failed call (PCP_ERR_ARG with the reason in pcp_last_error) leaves the handle unchanged.
  * Results are identical for every lane choice. */
 #define PCP_ICP_ABLATE_NO_SCAN 1
 #define PCP_ICP_ABLATE_NO_ACCUM 4

@@ -7,7 +7,10 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PCP_LIB") or os.path.join(HERE, "libpcp.so")  # PCP_LIB: A/B builds
+# A/B measurements only: PCP_LIB names another build of the library, and is honoured only together
+# with PCP_AB=1 (tools/*_ab.sh set both); the product and the tests always load the in-tree build
+_AB = os.environ.get("PCP_AB") == "1" and bool(os.environ.get("PCP_LIB"))
+LIB_PATH = os.environ["PCP_LIB"] if _AB else os.path.join(HERE, "libpcp.so")
 
 PCP_OK = 0
 _STATUS = {
@@ -124,14 +127,18 @@ def load(path=LIB_PATH, bind_all=True):
             f"libpcp.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; "
             "g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
     lib = C.CDLL(path)
-    ab_build = bool(os.environ.get("PCP_LIB"))  # an A/B build of an older tree may lack newer symbols
     if bind_all:
+        skipped = []
         for name, res, args in SIGNATURES:
-            if ab_build and not hasattr(lib, name):
+            if _AB and path == LIB_PATH and not hasattr(lib, name):  # an A/B build of an older tree
+                skipped.append(name)
                 continue
             fn = getattr(lib, name)  # AttributeError if the ABI symbol is missing
             fn.restype = res
             fn.argtypes = args
+        if skipped:
+            import sys
+            print(f"_lib: A/B build {path} lacks {len(skipped)} ABI symbols: {', '.join(skipped)}", file=sys.stderr)
     if path == LIB_PATH:
         _lib = lib
     return lib

@@ -19,7 +19,8 @@
 //     gives a query's hit mask over the wave in candidate = row order);
 //   * the F1 sums (S P, S P P^T of the hits) are the product of the 0/1 hit matrix with the
 //     candidates' moment features, on f16 MFMA with fp32 accumulation
-//     (v_mfma_f32_16x16x32_f16; each moment as an f16 hi + lo pair, 22 significant bits).  The hit
+//     (v_mfma_f32_16x16x32_f16; each moment, in cell units, as an f16 hi + lo pair, ~22
+//     significant bits at any cell size).  The hit
 //     matrix comes from the same contraction evaluated in the transposed layout
 //     (v_mfma_f32_16x16x4_f32: rows = candidates, columns = queries), which is the f16 MFMA's B
 //     operand with no lane movement; both layouts run the same k-ordered fp32 fma chain on the
@@ -148,7 +149,7 @@ constexpr int kMxWaves = 5;              // waves per SIMD (~7.3 KB of LDS per f
 typedef float mx_f4 __attribute__((ext_vector_type(4)));
 typedef _Float16 mx_h8 __attribute__((ext_vector_type(8)));
 
-// one query's F1 sums for k_h16_mx_planes, by caller index: S P (3), S P P^T (xx xy xz yy yz zz),
+// one query's F1 sums for k_h16_mx_planes, by caller index: S P (3), S P P^T (xx xy xz yy yz zz) in cell units,
 // the hit count and the query's cell (P relative to its centre).  64 bytes: the fill writes each
 // record whole with one store instruction (a 64-byte-aligned random write, no partial line), so
 // the planes pass reads the sums and writes the planes both in caller order -- a plane written at
@@ -273,7 +274,11 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
                         s_p[1][c] = py;
                         s_p[2][c] = pz;
                         s_p[3][c] = p2;
-                        const float mo[9] = {px, py, pz, px * px, px * py, px * pz, py * py, py * pz, pz * pz};
+                        // the moments in cell units (|u| <= 1.5), not metres: split into f16 (hi, lo)
+                        // pairs they keep ~22 significant bits at any cell size, where metre-sized
+                        // moments of a mm-scale cell would fall into f16's subnormal range
+                        const float ux = px * g.inv_hf, uy = py * g.inv_hf, uz = pz * g.inv_hf;
+                        const float mo[9] = {ux, uy, uz, ux * ux, ux * uy, ux * uz, uy * uy, uy * uz, uz * uz};
 #pragma unroll
                         for (int k = 0; k < 9; k++) {
                             const _Float16 hi = (_Float16)mo[k];
@@ -475,11 +480,12 @@ __device__ inline void mx_cov(const H16Args& a, uint32_t cid, const MxSums& q, d
     const GridDesc& g = a.g;
     int cx, cy, cz;
     cell_xyz(g, a, cid, cx, cy, cz);
-    const double nn = (double)q.n;
-    const double m0 = q.S[0] / nn, m1 = q.S[1] / nn, m2 = q.S[2] / nn;
-    C[0] = q.S[3] - nn * m0 * m0; C[1] = q.S[4] - nn * m0 * m1; C[2] = q.S[5] - nn * m0 * m2;
-    C[3] = C[1];                  C[4] = q.S[6] - nn * m1 * m1; C[5] = q.S[7] - nn * m1 * m2;
-    C[6] = C[2];                  C[7] = C[5];                  C[8] = q.S[8] - nn * m2 * m2;
+    // the sums are in cell units (k_h16_mx): back to metres with the kernel's fp32 cell size
+    const double nn = (double)q.n, hd = (double)a.hf, hd2 = hd * hd;
+    const double m0 = q.S[0] * hd / nn, m1 = q.S[1] * hd / nn, m2 = q.S[2] * hd / nn;
+    C[0] = q.S[3] * hd2 - nn * m0 * m0; C[1] = q.S[4] * hd2 - nn * m0 * m1; C[2] = q.S[5] * hd2 - nn * m0 * m2;
+    C[3] = C[1];                        C[4] = q.S[6] * hd2 - nn * m1 * m1; C[5] = q.S[7] * hd2 - nn * m1 * m2;
+    C[6] = C[2];                        C[7] = C[5];                        C[8] = q.S[8] * hd2 - nn * m2 * m2;
     const double hh = (double)(0.5f * a.hf);  // the kernel's fp32 half cell
     xa = g.o[0] + (double)cx * g.h + hh + m0;
     ya = g.o[1] + (double)cy * g.h + hh + m1;
@@ -569,6 +575,8 @@ extern "C" {
 int pcp_index_build_h16(pcp_ctx* ctx, const float* xyz, size_t stride, int64_t n, double cell_size, pcp_index** out) {
     if (!ctx || !out || !(cell_size > 0)) return set_error(ctx, PCP_ERR_ARG, "pcp_index_build_h16: bad arguments");
     if (cell_size > 0.5) return set_error(ctx, PCP_ERR_UNSUPPORTED, "h16 cells > 0.5 m lose fp16 offset precision");
+    if (cell_size < 1e-3)  // offsets below ~6e-5 m are f16 subnormals (absolute spacing 6e-8 m)
+        return set_error(ctx, PCP_ERR_UNSUPPORTED, "h16 cells < 1 mm put the fp16 offsets in the subnormal range");
     pcp_index* ix = nullptr;
     PCP_TRY(pcp_index_build_f32(ctx, xyz, stride, n, cell_size, &ix));
     if (!ix->g.dense) {

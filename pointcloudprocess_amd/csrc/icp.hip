@@ -1971,6 +1971,16 @@ int qsort_launch(pcp_ctx* ctx, hipStream_t st, const GridDesc& g, const float* q
         (rc = dmalloc(ctx, &s.qs, nq + 1)) || (rc = dmalloc(ctx, &s.d_cnt, 1)))
         return rc;
     PCP_HIP(ctx, event_get(ctx, &s.done));
+    unsigned bits = 1;  // keys are in [0, query_key_end]
+    while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)query_key_end(g)) bits++;
+    size_t tb = 0;
+    if (nq > 0) {
+        PCP_HIP(ctx, rocprim::radix_sort_pairs<RecSortConfig>(nullptr, tb, s.k0, s.k1, s.r0, s.qs, (size_t)nq, 0u, bits, st));
+        if ((rc = dmalloc(ctx, (char**)&s.tmp, tb))) return rc;
+    }
+    // Every block the side stream uses is allocated above, before `go` is recorded: a block the
+    // context cache hands out after that point could still be in use by main-stream work the side
+    // stream does not wait for.
     if (st != ctx->stream) {  // the side stream starts after the main stream's work so far
         hipEvent_t go = nullptr;
         PCP_HIP(ctx, event_get(ctx, &go));
@@ -1981,13 +1991,8 @@ int qsort_launch(pcp_ctx* ctx, hipStream_t st, const GridDesc& g, const float* q
     }
     PCP_HIP(ctx, hipMemsetAsync(s.d_cnt, 0, sizeof(unsigned long long), st));
     if (nq > 0) {
-        unsigned bits = 1;  // keys are in [0, query_key_end]
-        while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)query_key_end(g)) bits++;
-        size_t tb = 0;
         hipLaunchKernelGGL(k_query_keys, dim3(grid_for(nq, 256)), dim3(256), 0, st, g, q, q_stride / sizeof(float), nq,
                            s.k0, s.r0);
-        PCP_HIP(ctx, rocprim::radix_sort_pairs<RecSortConfig>(nullptr, tb, s.k0, s.k1, s.r0, s.qs, (size_t)nq, 0u, bits, st));
-        if ((rc = dmalloc(ctx, (char**)&s.tmp, tb))) return rc;
         PCP_HIP(ctx, rocprim::radix_sort_pairs<RecSortConfig>(s.tmp, tb, s.k0, s.k1, s.r0, s.qs, (size_t)nq, 0u, bits, st));
         hipLaunchKernelGGL(k_first_at_least, dim3(1), dim3(1), 0, st, s.k1, nq, query_key_end(g), s.d_cnt);
     }
@@ -2157,23 +2162,27 @@ int pcp_icp_create_with_target(pcp_ctx* ctx, const float* target_xyz, size_t t_s
 int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, int ring_lanes, int ablate) {
     if (!icp) return PCP_ERR_ARG;
     auto lanes = [](int v) { return v == 0 || v == 1 || v == 2 || v == 4 || v == 8; };
-    if (!lanes(oct_lanes_first) || !lanes(oct_lanes_list) || !lanes(ring_lanes) || ablate < 0) return PCP_ERR_ARG;
-    icp->oct_g_first = oct_lanes_first ? oct_lanes_first : 1;
-    icp->oct_g_list = oct_lanes_list;
-    icp->ring_g = ring_lanes;
-    if ((ablate & PCP_ICP_OPT_WIDE_CACHE) && icp->narrow) {  // re-create the records in the 16-byte form
-        if (icp->launches > 0) return PCP_ERR_ARG;
-        pcp_ctx* ctx = icp->owner;
+    pcp_ctx* ctx = icp->owner;
+    // every check and allocation first: a failed call leaves the handle as it was
+    if (!lanes(oct_lanes_first) || !lanes(oct_lanes_list) || !lanes(ring_lanes) || ablate < 0)
+        return pcp::set_error(ctx, PCP_ERR_ARG, "pcp_icp_set_options: lanes must be 0, 1, 2, 4 or 8; ablate >= 0");
+    const bool widen = (ablate & PCP_ICP_OPT_WIDE_CACHE) && icp->narrow;
+    if (widen && icp->launches > 0)
+        return pcp::set_error(ctx, PCP_ERR_ARG, "PCP_ICP_OPT_WIDE_CACHE only before the handle's first launch");
+    if (widen) {  // re-create the records in the 16-byte form
         uint32_t* w = nullptr;
         if (int rc = pcp::dmalloc(ctx, &w, (size_t)(icp->nq + 1) * 4)) return rc;
         if (hipMemsetAsync(w, 0xff, (size_t)(icp->nq + 1) * 16, ctx->stream) != hipSuccess) {
             pcp::dfree(ctx, w);
-            return PCP_ERR_HIP;
+            return pcp::set_error(ctx, PCP_ERR_HIP, "pcp_icp_set_options: memset");
         }
         pcp::dfree(ctx, icp->cand);
         icp->cand = w;
         icp->narrow = false;
     }
+    icp->oct_g_first = oct_lanes_first ? oct_lanes_first : 1;
+    icp->oct_g_list = oct_lanes_list;
+    icp->ring_g = ring_lanes;
     icp->dbg = ablate & ~PCP_ICP_OPT_WIDE_CACHE;
     return PCP_OK;
 }

@@ -158,5 +158,7 @@ def test_c5_fullsize_200m(ctx):
     print(f"C5 200M sampled: {tot} rows from 20 tiles, {clean} band-free: {angle_summary(angles)}; "
           f"curvature err max {curv.max():.2e}")
     assert tot > 150_000 and clean > 100_000
-    assert np.percentile(angles, 99) < 1.5e-3 and np.percentile(angles, 99.99) < 5e-3 and angles.max() < 2e-2
+    # the gate sits ~1.5-2x above the measured error (round 5: p99 3.2e-4, max 1.1e-3 rad), so a
+    # regression that makes the fp16 normals a few times worse fails here
+    assert np.percentile(angles, 99) < 5e-4 and angles.max() < 2.5e-3, angle_summary(angles)
     assert curv.max() < 5e-4

@@ -36,20 +36,20 @@ def scene():
     return synth.street_scene(1_500_000, 5101, extent=(40.0, 40.0)).numpy()  # C5 density
 
 
-def _rows(ctx, xyz, r=R, n_owned=None, gid=None, normals=True):
+def _rows(ctx, xyz, r=R, n_owned=None, gid=None, normals=True, cell=R):
     from pointcloudprocess_amd import ops
-    ix = ops.H16Index(ctx, torch.from_numpy(np.ascontiguousarray(xyz)).to(ctx.device), cell_size=R)
+    ix = ops.H16Index(ctx, torch.from_numpy(np.ascontiguousarray(xyz)).to(ctx.device), cell_size=cell)
     offs, idx, nrm = ix.radius_normals(r, n_owned=n_owned, global_id=gid, normals=normals)
     ix.close()
     return offs, idx, nrm
 
 
-def _check(ctx, xyz, offs, idx, nrm, qs, r=R, id_to_point=None, min_rows=10):
+def _check(ctx, xyz, offs, idx, nrm, qs, r=R, id_to_point=None, min_rows=10, eps=EPS):
     tree = ora.KdTree(xyz.astype(np.float64))
     x64 = torch.from_numpy(xyz.astype(np.float64)).to(ctx.device)
     s = torch.from_numpy(np.asarray(qs, dtype=np.int64)).to(ctx.device)
     return check_against_oracle(tree, x64, offs, idx, s, np.asarray(qs, dtype=np.int32), r, nrm, id_to_point,
-                                min_rows=min_rows)
+                                min_rows=min_rows, eps=eps)
 
 
 def test_h16_radius_rows_and_normals(ctx, scene):
@@ -81,6 +81,36 @@ def test_h16_radius_below_cell(ctx, scene, r):
           f"{res['missing']}; {angle_summary(res['angle'])}")
     assert res["far"] == 0 and res["dup"] == 0 and res["missing"] == 0
     assert np.percentile(res["angle"], 99) < 1.5e-3
+
+
+@pytest.mark.parametrize("r", [0.005, 0.02])
+def test_h16_small_radius_normals(ctx, r):
+    """mm-scale cells and radii (moments in metres fell into f16's subnormal range below
+    ~1 cm): a 1 x 1 m wavy surface with 400K points (~30 points per 5 mm ball), cell = r, rows and
+    band-free planes against the oracle's exact fp64 search.  The band is the fp16 offset bound at
+    this cell size (h * 2^-10, per axis); the angle gate is the r = 0.2 test's."""
+    rng = np.random.default_rng(11)
+    n = 400_000
+    u, v = rng.uniform(0.0, 1.0, n), rng.uniform(0.0, 1.0, n)
+    w = 0.05 * np.sin(3.0 * u) * np.cos(2.0 * v) + rng.normal(0.0, 2e-4, n)
+    xyz = np.ascontiguousarray(np.stack([u + 12.0, v - 3.0, w + 1.5], 1).astype(np.float32))
+    offs, idx, nrm = _rows(ctx, xyz, r=r, cell=r)
+    qs = np.sort(rng.choice(n, 20_000, replace=False))
+    res = _check(ctx, xyz, offs, idx, nrm, qs, r=r, eps=2.0 * r * 2.0 ** -10)
+    a = res["angle"]
+    print(f"r={r}: {res['rows']} rows nbar {res['nbar']:.1f}: far {res['far']} dup {res['dup']} missing "
+          f"{res['missing']}; {res['clean']} band-free: {angle_summary(a)}; curvature err max "
+          f"{res['curv_err'].max():.2e}")
+    assert res["far"] == 0 and res["dup"] == 0 and res["missing"] == 0
+    assert res["clean"] > 10_000
+    assert np.percentile(a, 99) < 1.5e-3 and a.max() < 2e-2
+    assert res["curv_err"].max() < 5e-4
+
+
+def test_h16_cell_below_1mm_rejected(ctx, scene):
+    from pointcloudprocess_amd import _lib, ops
+    with pytest.raises(_lib.PcpError):
+        ops.H16Index(ctx, torch.from_numpy(np.ascontiguousarray(scene[:1000])).to(ctx.device), cell_size=5e-4)
 
 
 @pytest.mark.parametrize("npts", [1, 2, 5])

@@ -1,4 +1,4 @@
-# Round-5 GPU call wrapper: STEPS selects what runs (space separated), each step under its own
+# Round-6 GPU call wrapper: STEPS selects what runs (space separated), each step under its own
 # time limit, the first failure ends the call.
 #   h16tests   the C5 tests (tests/test_gpu_h16.py) and the 200M full-size C5 test
 #   icptests   the ICP tests and the 50M-scale C4 check
@@ -14,9 +14,15 @@
 #   octg       per-launch octant times at fixed search-list lanes per query (kernel traces)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/${TAG:-r05}; mkdir -p $O
+O=gpurun_out/${TAG:-r06}; mkdir -p $O
 for st in ${STEPS}; do
 case $st in
+micro)
+  timeout -k 10 120 tools/sort_micro > $O/sort_micro.log 2>&1 ;;
+c4bench)
+  timeout -k 10 300 python3 -u bench.py --no-cpu --steps ${NSTEPS:-5} --warmup 2 >> $O/c4_bench.jsonl 2>> $O/c4_bench.err ;;
+c5bench)
+  timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_bench.jsonl 2>> $O/c5_bench.err ;;
 h16tests)
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_h16.py "tests/test_gpu_fullsize.py::test_c5_fullsize_200m" -x -v -s --timeout 500 --timeout-method thread > $O/h16_tests.log 2>&1 ;;
 bftests)
@@ -27,7 +33,7 @@ c5ab)
   for rep in 1 2; do
     timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_new.jsonl 2>> $O/c5_ab.err
     for V in ${VARS:-$VAR}; do
-      PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_$V.jsonl 2>> $O/c5_ab.err
+      PCP_AB=1 PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C5 --no-cpu --steps 3 >> $O/c5_ab_$V.jsonl 2>> $O/c5_ab.err
     done
   done ;;
 c5trace)
@@ -39,7 +45,7 @@ c4ab)
   for rep in 1 2 3; do
     timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 >> $O/c4_ab_new.jsonl 2>> $O/c4_ab.err
     for V in ${VARS:-$VAR}; do
-      PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 >> $O/c4_ab_$V.jsonl 2>> $O/c4_ab.err
+      PCP_AB=1 PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 >> $O/c4_ab_$V.jsonl 2>> $O/c4_ab.err
     done
   done ;;
 c4trace)
@@ -49,7 +55,7 @@ c3ab)
   for rep in 1 2 3; do
     timeout -k 10 300 python3 -u bench.py --config C3 --no-cpu --steps 5 >> $O/c3_ab_new.jsonl 2>> $O/c3_ab.err
     for V in ${VARS:-$VAR}; do
-      PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C3 --no-cpu --steps 5 >> $O/c3_ab_$V.jsonl 2>> $O/c3_ab.err
+      PCP_AB=1 PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C3 --no-cpu --steps 5 >> $O/c3_ab_$V.jsonl 2>> $O/c3_ab.err
     done
   done ;;
 knntests)
@@ -58,7 +64,7 @@ c2ab)
   for rep in 1 2; do
     timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_new.jsonl 2>> $O/c2_ab.err
     for V in ${VARS:-$VAR}; do
-      PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_$V.jsonl 2>> $O/c2_ab.err
+      PCP_AB=1 PCP_LIB=variants/$V/libpcp.so timeout -k 10 300 python3 -u bench.py --config C2 --no-cpu --steps 3 >> $O/c2_ab_$V.jsonl 2>> $O/c2_ab.err
     done
   done ;;
 c5pmc)

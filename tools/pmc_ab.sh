@@ -9,7 +9,7 @@ passes=(
   "WRITE_SIZE TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum"
 )
 for v in ${VARIANTS:-default}; do
-  if [ $v = default ]; then export PCP_LIB=""; else export PCP_LIB=$GRAFT_REPO_ROOT/variants/$v/libpcp.so; fi
+  if [ $v = default ]; then export PCP_LIB=""; else export PCP_AB=1 PCP_LIB=$GRAFT_REPO_ROOT/variants/$v/libpcp.so; fi
   mkdir -p $O/$v; i=0
   for p in "${passes[@]}"; do
     timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d $O/$v/p$i -o run -- python3 tools/icp_micro.py --reps 1 --iters ${ITERS:-8} > $O/$v/p$i.log 2>&1
