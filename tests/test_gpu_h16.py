@@ -65,8 +65,10 @@ def test_h16_radius_rows_and_normals(ctx, scene):
           f"{res['missing']}; {res['clean']} band-free: {angle_summary(a)}; curvature err max {res['curv_err'].max():.2e}")
     assert res["far"] == 0 and res["dup"] == 0 and res["missing"] == 0
     assert res["clean"] > 120_000  # ~72 % of the rows have no point inside the band
-    # fp16 offsets (~6e-5 m) + fp32 accumulation: angles grow as the two smallest eigenvalues meet
-    assert np.percentile(a, 99) < 1.5e-3 and np.percentile(a, 99.99) < 5e-3 and a.max() < 2e-2
+    # fp16 offsets (~6e-5 m) + fp32 accumulation: angles grow as the two smallest eigenvalues meet.
+    # Gate ~1.5-2x above the measured error (p99 3.3e-4, p99.99 9.2e-4, max 4.9e-3 rad: near-degenerate
+    # rows), so a regression that makes the normals a few times worse fails
+    assert np.percentile(a, 99) < 5e-4 and np.percentile(a, 99.99) < 1.5e-3 and a.max() < 1e-2
     assert res["curv_err"].max() < 5e-4
 
 
@@ -86,23 +88,23 @@ def test_h16_radius_below_cell(ctx, scene, r):
 @pytest.mark.parametrize("r", [0.005, 0.02])
 def test_h16_small_radius_normals(ctx, r):
     """mm-scale cells and radii (moments in metres fell into f16's subnormal range below
-    ~1 cm): a 1 x 1 m wavy surface with 400K points (~30 points per 5 mm ball), cell = r, rows and
-    band-free planes against the oracle's exact fp64 search.  The band is the fp16 offset bound at
-    this cell size (h * 2^-10, per axis); the angle gate is the r = 0.2 test's."""
+    ~1 cm): a 1 x 1 m wavy surface with ~30 points per r-ball (400K points at r = 5 mm), cell = r,
+    rows and band-free planes against the oracle's exact fp64 search.  The band is the fp16 offset
+    bound at this cell size (2 h 2^-10 per pair); the angle gate is the r = 0.2 test's."""
     rng = np.random.default_rng(11)
-    n = 400_000
+    n = int(400_000 * (0.005 / r) ** 2)
     u, v = rng.uniform(0.0, 1.0, n), rng.uniform(0.0, 1.0, n)
     w = 0.05 * np.sin(3.0 * u) * np.cos(2.0 * v) + rng.normal(0.0, 2e-4, n)
     xyz = np.ascontiguousarray(np.stack([u + 12.0, v - 3.0, w + 1.5], 1).astype(np.float32))
     offs, idx, nrm = _rows(ctx, xyz, r=r, cell=r)
-    qs = np.sort(rng.choice(n, 20_000, replace=False))
+    qs = np.sort(rng.choice(n, min(n, 20_000), replace=False))
     res = _check(ctx, xyz, offs, idx, nrm, qs, r=r, eps=2.0 * r * 2.0 ** -10)
     a = res["angle"]
     print(f"r={r}: {res['rows']} rows nbar {res['nbar']:.1f}: far {res['far']} dup {res['dup']} missing "
           f"{res['missing']}; {res['clean']} band-free: {angle_summary(a)}; curvature err max "
           f"{res['curv_err'].max():.2e}")
     assert res["far"] == 0 and res["dup"] == 0 and res["missing"] == 0
-    assert res["clean"] > 10_000
+    assert res["clean"] > 0.5 * res["rows"]
     assert np.percentile(a, 99) < 1.5e-3 and a.max() < 2e-2
     assert res["curv_err"].max() < 5e-4
 

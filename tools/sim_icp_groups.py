@@ -15,6 +15,17 @@ real pose sequence and the engine's cache certificate (as tools/sim_icp_cache.py
 
 The inflation is (scores per searched query) / (octant candidates per searched query).  The
 verdict's criterion: build the block-MFMA search only if it is <= 3x.
+
+Round 6 (verdict item 1(a)): the C5 cell-wave form, counted in WAVE PASSES (one wave-wide step
+that evaluates one 64-lane slice of candidates against one query set) per listed query:
+  lanes    the current form: chunks of 64 / G consecutive listed queries (list order = sorted
+           order), G lanes per query by the device density rule (G = 1 above 36 %, 2 above 8 %,
+           else 4), each chunk ceil(Lw / G) steps with Lw the chunk's longest octant list;
+  cellwave one wave per 2x2x2 query brick (bricks of octant-block origins) holding >= 1 listed
+           query: its 3x3x3-cell neighbourhood loaded once (ceil(C / 64) coalesced steps), then
+           per listed query (wave-uniform) ceil(C / 64) evaluation steps plus the wave-wide
+           top-3 merge of 6 butterfly stages (counted as 6 / 4 = 1.5 passes: ~4 DPP ops per
+           stage against ~16 VALU ops of a candidate step) and a per-brick set-up of 1 pass.
   python tools/sim_icp_groups.py [n_points]
 """
 import math
@@ -87,7 +98,8 @@ D = np.zeros(n)
 cache = np.zeros((n, K), np.int64)
 print(f"{n} pts, tile {side:.1f} m")
 print("launch  searched  octant/q  group m*C/q  infl  tiled/q  infl  cw64-tiled/q  infl")
-tot = {"oct": 0.0, "grp": 0.0, "til": 0.0, "cw": 0.0, "q": 0}
+tot = {"oct": 0.0, "grp": 0.0, "til": 0.0, "cw": 0.0, "q": 0, "wl": 0.0, "wc": 0.0}
+wave_rows = []
 for it, T in enumerate(poses):
     qt = q64 @ T[:3, :3].T + T[:3, 3]
     if it == 0:
@@ -111,6 +123,25 @@ for it, T in enumerate(poses):
     cell = np.floor(f).astype(np.int64) + 4
     cw = grouped(cell // 2, lambda g: box_count(g * 2 - 1, 4), True)
     nq_ = len(idx)
+    # wave passes: the current lanes form over the list in sorted order (queries are sorted by the
+    # brick-major key of their octant block, so sort the listed queries by it)
+    G = 1 if nq_ * 100 > n * 36 else (2 if nq_ * 100 > n * 8 else 4)
+    L = box_count(b, 2)
+    ordk = np.lexsort((b[:, 0] % 8, b[:, 1] % 8, b[:, 2] % 8, b[:, 0] // 8, b[:, 1] // 8, b[:, 2] // 8))
+    Ls = L[ordk]
+    qpc = 64 // G
+    nch = -(-nq_ // qpc)
+    Lp = np.zeros(nch * qpc, np.int64)
+    Lp[:nq_] = Ls
+    Lw = Lp.reshape(nch, qpc).max(1)
+    w_lanes = float(np.ceil(Lw / G).sum())
+    gb, ginv, gm = np.unique(b // 2, axis=0, return_inverse=True, return_counts=True)
+    C = box_count(gb * 2, 3)
+    steps = np.ceil(C / 64)
+    w_cell = float((steps + 1.0 + gm * (steps + 1.5)).sum())
+    tot["wl"] += w_lanes
+    tot["wc"] += w_cell
+    wave_rows.append((it, nq_ / n, G, w_lanes / nq_, len(gb), nq_ / len(gb), float(C.mean()), w_cell / nq_))
     tot["oct"] += oct_c
     tot["grp"] += grp
     tot["til"] += til
@@ -118,5 +149,11 @@ for it, T in enumerate(poses):
     tot["q"] += nq_
     print(f"{it:6d}  {nq_ / n:8.3f}  {oct_c / nq_:8.1f}  {grp / nq_:11.1f}  {grp / oct_c:4.1f}  {til / nq_:7.1f}  "
           f"{til / oct_c:4.1f}  {cw / nq_:12.1f}  {cw / oct_c:4.1f}")
+print("\nwave passes per listed query (verdict r5 item 1(a))")
+print("launch  searched  G  lanes/q  bricks  q/brick  C/brick  cellwave/q  ratio")
+for (it, fr, G, wl, nb, qb, cb, wc) in wave_rows:
+    print(f"{it:6d}  {fr:8.3f}  {G}  {wl:7.3f}  {nb:6d}  {qb:7.2f}  {cb:7.1f}  {wc:10.3f}  {wc / wl:5.1f}")
+print(f"launches 1-19: lanes {sum(r[3] * r[1] for r in wave_rows[1:]) / sum(r[1] for r in wave_rows[1:]):.3f}, "
+      f"cellwave {sum(r[7] * r[1] for r in wave_rows[1:]) / sum(r[1] for r in wave_rows[1:]):.3f} wave passes per listed query")
 print(f"all launches: octant {tot['oct'] / tot['q']:.1f} candidates per searched query; group m*C x{tot['grp'] / tot['oct']:.2f}, "
       f"16x16-tiled x{tot['til'] / tot['oct']:.2f}, cw64 tiled x{tot['cw'] / tot['oct']:.2f}")
