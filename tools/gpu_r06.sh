@@ -89,9 +89,10 @@ pmc)
   sq1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_VALU"
   sq2="SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
   sq3="SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_LDS_IDX_ACTIVE"
+  ta1="TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"
   P=$O/pmc_$CFG; mkdir -p $P
   i=0
-  for c in "$sq1" "$sq2" "$sq3" "WRITE_SIZE" "FETCH_SIZE"; do
+  for c in "$sq1" "$sq2" "$sq3" "$ta1" "WRITE_SIZE" "FETCH_SIZE"; do
     timeout -s KILL 200 rocprofv3 --pmc $c --output-format csv -d $P/p$i -o run -- python3 bench.py --config $CFG --no-cpu --steps 1 --warmup 0 $ARGS > $P/p$i.log 2>&1
     i=$((i+1))
   done
