@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""CPU model (round 6): a candidate cache whose winner is exact and whose other K - 1 points are
+QUANTISED offsets from it, against the current exact 3-point cache.
+
+The engine's verify pass gathers every cached point (3 x 16 B per query per launch, ~31 B of
+effective traffic) to re-rank them exactly.  The variant stores the search-time winner's position
+(one gather) and the other cached points as offsets from the winner quantised to e (error <= e per
+point), so the record can hold more points for about the same bytes.  Certificate at pose t
+(q_t, the search pose q_s, D the bound on every uncached point at q_s):
+
+  exact K    (the current engine's):  min over the K cached of |q_t - p| < D - |q_t - q_s|
+  quant K    |q_t - w| < D - |q_t - q_s|  and  |q_t - w| < min_i |q_t - o~_i| - e - margin
+             (the winner must still beat every other cached point: a switch of the nearest
+             cached point, which the exact cache settles, is sent to the search instead)
+
+It replays both over the registration's real pose sequence on a tile of the C4 bench scene at the
+bench density (as tools/sim_icp_cache.py) and prints the searched fraction per launch.
+  python tools/sim_icp_qcache.py [n_points]
+"""
+import math
+import os
+import sys
+
+import numpy as np
+from scipy.spatial import cKDTree
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import oracle_ctypes as ora  # noqa: E402  (test infrastructure: the reference ICP poses)
+from pointcloudprocess_amd import synth  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 2_000_000
+side = 200.0 * math.sqrt(n / 50e6)
+T_true = synth.rigid()
+tgt, q = synth.icp_pair(n, n, 4001, 4002, T_true, extent=(side, side))
+tgt, q = tgt.numpy(), q.numpy()
+rmax, iters, h, mc = 0.25, 20, 0.12, 1e-3
+eps = float(os.environ.get("SIM_EPS", str(h / 512.0)))  # quantisation error bound per point
+
+oi = ora.F32Index(tgt)
+poses, T = [], np.eye(4)
+for it in range(iters):
+    poses.append(T.copy())
+    R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+    ei, ed = oi.correspond(q, R, t, rmax)
+    acc = ora.icp_accumulate(tgt, q, R, t, ei, ed)
+    rc, dT = ora.icp_solve(acc)
+    T = dT @ T
+print(f"{n} pts, tile {side:.1f} m; quantisation error bound {eps * 1e3:.3f} mm")
+tree = cKDTree(tgt.astype(np.float64))
+o = tgt.min(0).astype(np.float64)
+q64 = q.astype(np.float64)
+t64 = tgt.astype(np.float64)
+
+
+def cert(qt):
+    f = (qt - o) / h
+    b = np.floor(f - 0.5)
+    m = np.minimum(f - b, b + 2 - f).min(1)
+    return (m - mc) * h
+
+
+def run(K, quant):
+    qs = np.zeros((n, 3))
+    D = np.zeros(n)
+    cache = np.zeros((n, K), np.int64)   # [:, 0] = the search-time winner
+    off = np.zeros((n, K - 1, 3))        # quantised others relative to the winner
+    searched, switched = [], []
+    for it, T in enumerate(poses):
+        qt = q64 @ T[:3, :3].T + T[:3, 3]
+        if it == 0:
+            need = np.ones(n, bool)
+        else:
+            delta = np.linalg.norm(qt - qs, axis=1)
+            if quant:
+                w = t64[cache[:, 0]]
+                dw = np.linalg.norm(w - qt, axis=1)
+                do = np.linalg.norm(w[:, None, :] + off - qt[:, None, :], axis=2) - eps
+                beat = dw < do.min(1) * (1 - 1e-6) - 1e-7
+                need = ~((dw < D - delta) & beat)
+                dall = np.linalg.norm(t64[cache] - qt[:, None, :], axis=2)
+                exact_ok = dall.min(1) < D - delta
+                switched.append(float((exact_ok & ~beat).sum()) / n)
+            else:
+                dall = np.linalg.norm(t64[cache] - qt[:, None, :], axis=2)
+                need = ~(dall.min(1) < D - delta)
+        idx = np.nonzero(need)[0]
+        dd, ii = tree.query(qt[idx], k=K + 1, workers=8)
+        c = cert(qt[idx])
+        ok = dd[:, 0] <= c
+        cache[idx] = ii[:, :K]
+        if quant:
+            rel = t64[ii[:, 1:K]] - t64[ii[:, :1]]
+            off[idx] = np.round(rel / (2 * eps / math.sqrt(3))) * (2 * eps / math.sqrt(3))
+        D[idx] = np.where(ok, np.minimum(dd[:, K], c), 0.0)
+        qs[idx] = qt[idx]
+        searched.append(len(idx) / n)
+    tot = sum(searched)
+    tag = f"{'quant' if quant else 'exact'} K={K}"
+    print(f"{tag}: searched per launch " + " ".join(f"{s:.3f}" for s in searched))
+    if quant:
+        print(f"   settled by the exact cache but sent to search by a winner switch (per launch): " +
+              " ".join(f"{s:.3f}" for s in switched))
+    print(f"   later searches {tot - searched[0]:.3f} x n")
+    return tot - searched[0]
+
+
+base = run(3, False)
+for K in (3, 5, 7, 9):
+    r = run(K, True)
+    print(f"   quant K={K}: {r / base:.3f} of the current engine's later searches")
+r = run(5, False)
+print(f"   exact K=5: {r / base:.3f}")
