@@ -523,7 +523,9 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             hooked = true;                                  // work that needs only it (overlaps the sort)
             if ((rc = (*on_geom)(g))) break;
         }
-        if ((rc = dmalloc(ctx, &count, ncells + 1))) break;
+        // + 1 pad entry: the ICP octant pass loads a row's starts as one 3-word vector at the row's
+        // first cell, whose third word lies one past the table for a 1-cell row at the last cell
+        if ((rc = dmalloc(ctx, &count, ncells + 2))) break;
         // ---- stable radix sort by cell id.  fp32: the payload is the point record itself, so
         // the sort output is the cell-ordered point array (no gather).  fp64: the payload is the
         // internal j (FLANN tie order), gathered below.

@@ -993,7 +993,68 @@ __device__ __forceinline__ void take_exact(OctResult& o, const float4 p, uint32_
     o.wz = t ? p.z : o.wz;
 }
 
-// packed-key scan (every lane's list < 256 candidates); G lanes per query share its list
+// v of lane (group base + src) of this lane's G-lane group (groups of G consecutive lanes; G = 2
+// and 4 by DPP quad permutes, inside the quad, no LDS)
+template <int G>
+__device__ __forceinline__ uint32_t grp_bcast(uint32_t v, int src) {
+    if constexpr (G == 1) return v;
+    if constexpr (G == 2) {  // quad_perm [s, s, 2 + s, 2 + s]
+        return src == 0 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0 | 0 << 2 | 2 << 4 | 2 << 6, 0xf, 0xf, false)
+                        : (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 1 | 1 << 2 | 3 << 4 | 3 << 6, 0xf, 0xf, false);
+    }
+    if constexpr (G == 4) {  // quad_perm [s, s, s, s]
+        switch (src) {
+            case 0: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xf, 0xf, false);
+            case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x55, 0xf, 0xf, false);
+            case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xf, 0xf, false);
+            default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xf, 0xf, false);
+        }
+    }
+    const int lane = (int)(threadIdx.x & 63);
+    return (uint32_t)__shfl((int)v, (lane & ~(G - 1)) | src, 64);
+}
+template <int G>
+__device__ __forceinline__ uint32_t grp_xor(uint32_t v, int s) {
+    if (s == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // [1,0,3,2]
+    if (s == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+    return (uint32_t)__shfl_xor((int)v, s, 64);
+}
+
+// The octant's 4 x-rows (y = by + (r & 1), z = bz + (r >> 1), cells [xa, xb], xb - xa + 1 = 1 or
+// 2): each row's point range [rs, rs + rn) from the cell starts.  A row's start and end are two
+// of the three consecutive words at its first cell, loaded as one 12-byte vector (the cell table
+// carries a pad word past its end for that).  With G lanes per query the group's lanes load
+// different rows (lane sub: rows sub, sub + G, ...) and exchange them inside the group, so a wave
+// issues 4 / G row loads instead of 8 (the loads of a sparse search list each touch a line per
+// query: what bounds those launches, TA busy ~75 %).
+template <int G>
+__device__ __forceinline__ void octant_rows(const GridDesc& g, bool scanq, int bx, int by, int bz, uint32_t sub,
+                                            uint32_t (&rs)[4], uint32_t (&rn)[4]) {
+    const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
+    constexpr int PER = G >= 4 ? 1 : 4 / G;  // rows this lane loads
+    uint32_t ls[PER], le[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int r = (int)sub + k * G;
+        const int y = by + (r & 1), z = bz + (r >> 1);
+        const bool in = scanq && r < 4 && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
+        uint3 t = make_uint3(0u, 0u, 0u);
+        if (in) t = *(const uint3*)(g.cstart + dense_id(g, xa, y, z));
+        ls[k] = t.x;
+        le[k] = xb > xa ? t.z : t.y;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t s0 = G == 1 ? ls[r] : grp_bcast<G>(ls[(r / G) % PER], r % G);
+        const uint32_t e0 = G == 1 ? le[r] : grp_bcast<G>(le[(r / G) % PER], r % G);
+        rs[r] = s0;
+        rn[r] = e0 - s0;
+    }
+}
+
+// packed-key scan (every lane's list < 256 candidates); G lanes per query share its list.  The
+// exact re-rank of the 3 kept points: with G > 1 the group's lanes gather different kept points
+// and reduce the exact (d2, index) winner inside the group (1 or 2 gathers per lane, not 3).
 template <int G>
 __device__ __forceinline__ OctResult octant_packed(const IcpArgs& a, const uint32_t (&rs)[4], const uint32_t (&rn)[4],
                                                    uint32_t Lw, float qx, float qy, float qz, uint32_t sub) {
@@ -1006,11 +1067,39 @@ __device__ __forceinline__ OctResult octant_packed(const IcpArgs& a, const uint3
     o.c0 = k.t0 != kKeyMax ? cat_addr_l(k.t0 & 0xffu, c1, c2, c3, L, o0, o1, o2, o3, a.ntp) : ~0u;
     o.c1 = k.t1 != kKeyMax ? cat_addr_l(k.t1 & 0xffu, c1, c2, c3, L, o0, o1, o2, o3, a.ntp) : ~0u;
     o.c2 = k.t2 != kKeyMax ? cat_addr_l(k.t2 & 0xffu, c1, c2, c3, L, o0, o1, o2, o3, a.ntp) : ~0u;
-    const float4 p0 = ld16(a.tp, min(o.c0, a.ntp)), p1 = ld16(a.tp, min(o.c1, a.ntp)), p2 = ld16(a.tp, min(o.c2, a.ntp));
     int wj = 0x7fffffff;
-    take_exact(o, p0, o.c0, qx, qy, qz, wj);
-    take_exact(o, p1, o.c1, qx, qy, qz, wj);
-    take_exact(o, p2, o.c2, qx, qy, qz, wj);
+    if constexpr (G == 1) {
+        const float4 p0 = ld16(a.tp, min(o.c0, a.ntp)), p1 = ld16(a.tp, min(o.c1, a.ntp)),
+                     p2 = ld16(a.tp, min(o.c2, a.ntp));
+        take_exact(o, p0, o.c0, qx, qy, qz, wj);
+        take_exact(o, p1, o.c1, qx, qy, qz, wj);
+        take_exact(o, p2, o.c2, qx, qy, qz, wj);
+    } else {
+        constexpr int PER = G >= 3 ? 1 : 2;  // kept points per lane: G = 2: lane 0 {c0, c2}, lane 1 {c1}
+#pragma unroll
+        for (int s = 0; s < PER; s++) {
+            const uint32_t kslot = sub + (uint32_t)(s * G);
+            const uint32_t c = kslot == 0 ? o.c0 : (kslot == 1 ? o.c1 : (kslot == 2 ? o.c2 : ~0u));
+            take_exact(o, ld16(a.tp, min(c, a.ntp)), c, qx, qy, qz, wj);
+        }
+        // the group's winner by (d2, index): butterfly over the group (every lane ends with it)
+#pragma unroll
+        for (int m = 1; m < G; m <<= 1) {
+            const float od = __uint_as_float(grp_xor<G>(__float_as_uint(o.d0), m));
+            const int oj = (int)grp_xor<G>((uint32_t)wj, m);
+            const uint32_t ow = grp_xor<G>(o.win, m);
+            const float ox = __uint_as_float(grp_xor<G>(__float_as_uint(o.wx), m));
+            const float oy = __uint_as_float(grp_xor<G>(__float_as_uint(o.wy), m));
+            const float oz = __uint_as_float(grp_xor<G>(__float_as_uint(o.wz), m));
+            const bool t = ow != ~0u && (o.win == ~0u || od < o.d0 || (od == o.d0 && oj < wj));
+            o.d0 = t ? od : o.d0;
+            wj = t ? oj : wj;
+            o.win = t ? ow : o.win;
+            o.wx = t ? ox : o.wx;
+            o.wy = t ? oy : o.wy;
+            o.wz = t ? oz : o.wz;
+        }
+    }
     o.dnext = k.t3 == kKeyMax ? INFINITY : __uint_as_float(k.t3 & ~0xffu);
     return o;
 }
@@ -1085,19 +1174,8 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
             outside = dout * dout > a.r2 * 1.0001f;
         }
         const bool scanq = !outside;
-        // the octant's 4 x-rows (y = by + (r & 1), z = bz + (r >> 1)), cells [xa, xb]
-        const int xa = max(bx, 0), xb = min(bx + 1, g.n[0] - 1);
         uint32_t rs[4], rn[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int y = by + (r & 1), z = bz + (r >> 1);
-            const bool in = scanq && xa <= xb && y >= 0 && y < g.n[1] && z >= 0 && z < g.n[2];
-            const int64_t cc = in ? dense_id(g, xa, y, z) : 0;
-            rs[r] = in ? g.cstart[cc] : 0u;
-            rn[r] = in ? g.cstart[cc + (xb - xa + 1)] : 0u;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) rn[r] -= rs[r];
+        octant_rows<G>(g, scanq, bx, by, bz, sub, rs, rn);
         const uint32_t len = rn[0] + rn[1] + rn[2] + rn[3];
         const uint32_t Lw = (uint32_t)__builtin_amdgcn_readfirstlane(wave_max_u((int)len));  // wave-uniform
         OctResult o;
