@@ -29,7 +29,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kWaves = 4;              // waves per block
 // k <= 8 configuration: list length per (row, class), query blocks per wave, waves/SIMD
 #ifndef PCP_BF_L8
-#define PCP_BF_L8 6
+#define PCP_BF_L8 5
 #endif
 #ifndef PCP_BF_QB8
 #define PCP_BF_QB8 1
@@ -40,6 +40,9 @@ constexpr int kWaves = 4;              // waves per block
 constexpr int kBlock = 64 * kWaves;
 #ifndef PCP_BF_TILE
 #define PCP_BF_TILE 1024
+#endif
+#ifndef PCP_BF_DEPTH  // MFMA sub-tiles in flight ahead of the hit test (software pipeline depth)
+#define PCP_BF_DEPTH 1
 #endif
 #ifndef PCP_BF_UNROLL  // sub-tile steps per unrolled loop body
 #define PCP_BF_UNROLL 4
@@ -250,27 +253,40 @@ __global__ __launch_bounds__(kBlock, W) void k_bf_mfma(BfArgs a) {
         const int tb = (int)(tt * kTile);
         // B fragment of sub-tile s: word 64 s + 16 grp + cls (k-major group: conflict-free)
         auto bfrag_at = [&](int sub) { return tf[sub * 64 + grp * 16 + cls]; };
-        // software pipeline: the MFMAs of sub-tile s+1 are in flight while the scores of
-        // sub-tile s are tested, so the matrix pipe never waits on the selection VALU work
-        f32x4 cn[QB];
-        float bnext;  // B fragment of sub-tile s+2, read from LDS a step ahead of its MFMA
+        // software pipeline, PCP_BF_DEPTH deep: the MFMAs of sub-tiles s+1 .. s+DEPTH are in flight
+        // while the scores of sub-tile s are tested, so the hit test never waits on the result of
+        // the MFMA issued just before it (at depth 1 the compiler pads every step with s_nop wait
+        // states for that MFMA -> VALU dependency, and the matrix pipe idles meanwhile).  The C
+        // operand (-threshold) is taken at issue: deeper means staler, which only lets more
+        // candidates through to the exact re-score.
+        constexpr int DEPTH = PCP_BF_DEPTH;
+        constexpr int NS = kTile / 16;
+        f32x4 cq[DEPTH][QB];  // cq[d]: the MFMA results of sub-tile s + 1 + d
+        float bnext;          // B fragment of sub-tile s + DEPTH + 1, read from LDS a step ahead
         {
-            const float bf0 = bfrag_at(0);
-            bnext = bfrag_at(1);
 #pragma unroll
-            for (int b = 0; b < QB; b++) cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf0, nthr[b], 0, 0, 0);
+            for (int d = 0; d < DEPTH; d++) {
+                const float bf = bfrag_at(d);
+#pragma unroll
+                for (int b = 0; b < QB; b++) cq[d][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bf, nthr[b], 0, 0, 0);
+            }
+            bnext = bfrag_at(DEPTH);
         }
 #pragma unroll kBfUnroll
-        for (int sub = 0; sub < kTile / 16; sub++) {
+        for (int sub = 0; sub < NS; sub++) {
             f32x4 c[QB];
 #pragma unroll
-            for (int b = 0; b < QB; b++) c[b] = cn[b];
-            if (sub + 1 < kTile / 16) {
+            for (int b = 0; b < QB; b++) c[b] = cq[0][b];
+#pragma unroll
+            for (int d = 0; d + 1 < DEPTH; d++)
+#pragma unroll
+                for (int b = 0; b < QB; b++) cq[d][b] = cq[d + 1][b];
+            if (sub + DEPTH < NS) {
                 const float bfrag = bnext;
-                if (sub + 2 < kTile / 16) bnext = bfrag_at(sub + 2);
+                if (sub + DEPTH + 1 < NS) bnext = bfrag_at(sub + DEPTH + 1);
 #pragma unroll
                 for (int b = 0; b < QB; b++)
-                    cn[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfrag, nthr[b], 0, 0, 0);
+                    cq[DEPTH - 1][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(afrag[b], bfrag, nthr[b], 0, 0, 0);
             }
             // one combined test per step; the insertion path runs only when a lane has a hit
             uint32_t sg = 0;
