@@ -48,14 +48,14 @@ struct pcp_icp {
     bool last_verified = false;   // the last launch ran the verify pass
     int32_t* sv = nullptr;        // verify pass: per-wave segments of uncertified queries (sv_seg each)
     uint32_t* sv_count = nullptr;
-    uint32_t* sv_off = nullptr;
+    uint32_t* sv_off = nullptr;   // [nseg_v]: the search list's length (k_list_compact)
     int32_t* svc = nullptr;       // compacted search list
     int64_t sv_seg = 0;
     int64_t nseg_v = 0;           // verify list segments: one per wave, or one per chunk (XCD split)
     int nb_ver = 0;
     int32_t* fb = nullptr;        // fallback lists: one segment of fb_seg entries per octant WG
     uint32_t* fb_count = nullptr; // per octant wave: entries in its segment
-    uint32_t* fb_off = nullptr;   // exclusive scan of fb_count (+ total)
+    uint32_t* fb_off = nullptr;   // [nseg]: the fallback list's length (k_list_compact)
     int32_t* fbc = nullptr;       // compacted fallback list
     int64_t fb_seg = 0;
     double* partials = nullptr;   // (nb_ver + nb_fast + nb_ring) * 24
@@ -124,7 +124,7 @@ struct IcpArgs {
     int64_t nseg_v;     // verify-pass waves
     int32_t* fb;
     uint32_t* fb_count;
-    uint32_t* fb_off;   // nseg + 1: the counts again, scanned in place after the pass
+    uint32_t* fb_off;   // [nseg]: the compacted fallback list's length
     int64_t fb_seg;
     int nb_fast;
     int64_t nseg;       // fallback segments (= waves of the octant kernel)
@@ -804,8 +804,6 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     }
     if (lane == 0) {
         a.sv_count[gw] = svn;
-        a.sv_off[gw] = svn;  // scanned in place into the segment offsets
-        if (gw == 0) a.sv_off[a.nseg_v] = 0u;
     }
     write_wave_partials(s_acc, a.partials + (int64_t)blockIdx.x * kAcc);
 }
@@ -1221,8 +1219,6 @@ __device__ __forceinline__ void octant_run(const IcpArgs& a, const int32_t* list
     }
     if (lane == 0) {  // every wave of the grid writes its count: no zeroing pass needed
         a.fb_count[gw] = fbn;
-        a.fb_off[gw] = fbn;  // scanned in place into the segment offsets
-        if (gw == 0) a.fb_off[a.nseg] = 0u;
     }
 }
 
@@ -1262,7 +1258,6 @@ __global__ void __launch_bounds__(kIcpBlock, MINW) k_icp_octant(IcpArgs a, const
         const int64_t nw = (int64_t)gridDim.x * kOctW;
         for (int64_t sg = nw + (int64_t)blockIdx.x * kOctW + wid; sg < a.nseg; sg += nw) {
             a.fb_count[sg] = 0u;
-            a.fb_off[sg] = 0u;
         }
     }
 }
@@ -1394,15 +1389,33 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_RING_WAVES) k_icp_ring(IcpArgs 
     write_wave_partials(s_acc, partials + (int64_t)blockIdx.x * kAcc);
 }
 
-// concatenate the fallback segments (one wave per segment; segment s starts at base[s], or at
-// s * seg_cap without a base table)
-__global__ void k_fb_compact(const int32_t* fb, const uint32_t* cnt, const uint32_t* off, int64_t nseg,
-                             int64_t seg_cap, int32_t* out, const uint32_t* base = nullptr) {
-    const int64_t seg = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (seg >= nseg) return;
-    const uint32_t n = cnt[seg], o = off[seg];
-    const int64_t b = base ? (int64_t)base[seg] : seg * seg_cap;
-    for (uint32_t k = threadIdx.x & 63; k < n; k += 64) out[o + k] = fb[b + k];
+// Concatenate per-wave list segments (segment s holds cnt[s] entries at s * seg_cap) into one
+// list, in one launch with no separate scan: block b (4 waves: segments 4b .. 4b + 3) finds the
+// exclusive prefix of the counts before its first segment by summing them itself (at most nseg
+// counts, L2-resident), and the block holding the last segment writes the total to *total (where
+// the consumers read the list length).  The list keeps segment order, entry for entry.
+__global__ void __launch_bounds__(256) k_list_compact(const int32_t* __restrict__ seg, const uint32_t* __restrict__ cnt,
+                                                      int64_t nseg, int64_t seg_cap, int32_t* __restrict__ out,
+                                                      uint32_t* __restrict__ total) {
+    __shared__ uint32_t s_part[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t s0 = (int64_t)blockIdx.x * 4;
+    uint32_t acc = 0;
+    for (int64_t i = threadIdx.x; i < s0; i += 256) acc += cnt[i];
+    for (int o = 32; o > 0; o >>= 1) acc += (uint32_t)__shfl_xor((int)acc, o, 64);
+    if (lane == 0) s_part[w] = acc;
+    __syncthreads();
+    const uint32_t base = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+    uint32_t c[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = s0 + k < nseg ? cnt[s0 + k] : 0u;
+    uint32_t off = base;
+#pragma unroll
+    for (int k = 0; k < 3; k++) off += k < w ? c[k] : 0u;
+    const int64_t sg = s0 + w;
+    if (sg < nseg)
+        for (uint32_t k = (uint32_t)lane; k < c[w]; k += 64) out[off + k] = seg[sg * seg_cap + k];
+    if (s0 + 4 >= nseg && threadIdx.x == 0) *total = base + c[0] + c[1] + c[2] + c[3];
 }
 
 // fixed-order reduction of nb partial rows of 24 doubles -> out[24]: thread t sums column
@@ -1900,10 +1913,9 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
         if (verify) {
             a.partials = part_v;
             hipLaunchKernelGGL(k_icp_verify, dim3(icp->nb_ver), dim3(kIcpBlock), 0, ctx->stream, a);
-            PCP_TRY(scan_u32_inplace(ctx, icp->sv_off, a.nseg_v + 1, nullptr));
-            hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)((a.nseg_v + 3) / 4)), dim3(256), 0, ctx->stream,
-                               icp->sv, (const uint32_t*)icp->sv_count, (const uint32_t*)icp->sv_off, a.nseg_v,
-                               a.sv_seg, icp->svc);
+            hipLaunchKernelGGL(k_list_compact, dim3((unsigned)((a.nseg_v + 3) / 4)), dim3(256), 0, ctx->stream,
+                               (const int32_t*)icp->sv, (const uint32_t*)icp->sv_count, a.nseg_v, a.sv_seg, icp->svc,
+                               icp->sv_off + a.nseg_v);
         } else {
             PCP_HIP(ctx, hipMemsetAsync(part_v, 0, (size_t)icp->nb_ver * kAcc * sizeof(double), ctx->stream));
         }
@@ -1927,9 +1939,9 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     }
     if (icp->dbg) PCP_HIP(ctx, hipEventRecord(icp->ev_mid, ctx->stream));
     if (a.g.dense) {  // compact the per-wave fallback segments into one list
-        PCP_TRY(scan_u32_inplace(ctx, icp->fb_off, a.nseg + 1, nullptr));
-        hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)((a.nseg + 3) / 4)), dim3(256), 0, ctx->stream, icp->fb,
-                           (const uint32_t*)icp->fb_count, (const uint32_t*)icp->fb_off, a.nseg, a.fb_seg, icp->fbc);
+        hipLaunchKernelGGL(k_list_compact, dim3((unsigned)((a.nseg + 3) / 4)), dim3(256), 0, ctx->stream,
+                           (const int32_t*)icp->fb, (const uint32_t*)icp->fb_count, a.nseg, a.fb_seg, icp->fbc,
+                           icp->fb_off + a.nseg);
     }
     // 3. exact fallback (or every query on a sparse grid)
     a.partials = part_r;

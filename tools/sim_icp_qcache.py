@@ -106,7 +106,50 @@ def run(K, quant):
     return tot - searched[0]
 
 
+def run_qs(K, e):
+    """Every cached point quantised relative to the query's search-pose position q_s (error <= e):
+    the verify takes the quantised argmin w, gathers only it, and settles when its exact distance
+    is below every other cached point's quantised distance less e (and below D - delta)."""
+    qs = np.zeros((n, 3))
+    D = np.zeros(n)
+    cache = np.zeros((n, K), np.int64)
+    off = np.zeros((n, K, 3))
+    step = 2 * e / math.sqrt(3)
+    searched = []
+    for it, T in enumerate(poses):
+        qt = q64 @ T[:3, :3].T + T[:3, 3]
+        if it == 0:
+            need = np.ones(n, bool)
+        else:
+            dvec = qt - qs
+            delta = np.linalg.norm(dvec, axis=1)
+            dq = np.linalg.norm(off - dvec[:, None, :], axis=2)   # quantised distances at pose t
+            w = dq.argmin(1)
+            dw = np.linalg.norm(t64[cache[np.arange(n), w]] - qt, axis=1)
+            dq_other = np.where(np.arange(K)[None, :] == w[:, None], np.inf, dq)
+            beat = dw < (dq_other.min(1) - e) * (1 - 1e-6) - 4e-5
+            need = ~((dw < D - delta - 4e-5) & beat)
+        idx = np.nonzero(need)[0]
+        dd, ii = tree.query(qt[idx], k=K + 1, workers=8)
+        c = cert(qt[idx])
+        ok = dd[:, 0] <= c
+        cache[idx] = ii[:, :K]
+        off[idx] = np.round((t64[ii[:, :K]] - qt[idx][:, None, :]) / step) * step
+        D[idx] = np.where(ok, np.minimum(dd[:, K], c), 0.0)
+        qs[idx] = qt[idx]
+        searched.append(len(idx) / n)
+    tot = sum(searched)
+    print(f"q_s-relative quant K={K} e={e * 1e3:.2f} mm: searched per launch " + " ".join(f"{x:.3f}" for x in searched))
+    print(f"   later searches {tot - searched[0]:.3f} x n")
+    return tot - searched[0]
+
+
 base = run(3, False)
+if os.environ.get("SIM_QS_ONLY"):
+    for K, e in ((3, h / 256 * 0.866), (4, h / 128 * 0.866), (4, h / 256 * 0.866), (5, h / 128 * 0.866)):
+        r = run_qs(K, e)
+        print(f"   {r / base:.3f} of the current engine's later searches")
+    sys.exit(0)
 for K in (3, 5, 7, 9):
     r = run(K, True)
     print(f"   quant K={K}: {r / base:.3f} of the current engine's later searches")
