@@ -74,6 +74,10 @@ struct pcp_icp {
     int last_launches = 0;
     uint32_t last_fallback = 0;
     uint32_t last_searched = 0;   // queries the verify pass could not certify (searched)
+    hipGraphExec_t gexec = nullptr;  // the verify .. fallback section of a device-pose launch (icp_launch)
+    hipStream_t gstream = nullptr;   // its capture stream
+    float graph_r2 = 0.f;            // the rmax^2 it was captured with
+    bool graph_off = false;          // capture failed: plain launches
 };
 
 namespace pcp {
@@ -133,6 +137,7 @@ struct IcpArgs {
     int oct_g;          // octant pass lanes per query: 1, 2, 4, 8, or 0 = by the list's density
     int ring_g;         // fallback pass lanes per query: 1, 2, 4, 8, or 0 = PCP_RING_G / by length
     const float* pose;  // device poses (current, previous: 24 floats) overriding R/t, Rp/tq, or null
+    const uint32_t* launch_dev;  // device copy of `launch` (k_pose_set), so a captured launch graph replays
 };
 
 // sorted query i as {x, y, z, 0}
@@ -143,6 +148,7 @@ __device__ __forceinline__ float4 ldq(const IcpArgs& a, int64_t i) {
 
 // the pose as the kernels use it: from the device copy when the loop is device-resident
 __device__ __forceinline__ void load_pose(IcpArgs& a) {
+    if (a.launch_dev) a.launch = *a.launch_dev;
     if (a.pose) {
 #pragma unroll
         for (int k = 0; k < 9; k++) a.R[k] = a.pose[k];
@@ -1800,7 +1806,8 @@ __host__ __device__ double det3(const double M[9]) {
 struct HostPose {
     float R[9], t[3];
 };
-__global__ void k_pose_set(const double* T, HostPose hp, float* pose, float* hist) {
+__global__ void k_pose_set(const double* T, HostPose hp, float* pose, float* hist, uint32_t launch) {
+    *(uint32_t*)(pose + 24) = launch;
     for (int k = 0; k < 12; k++) pose[12 + k] = pose[k];
     for (int r = 0; r < 3; r++) {
         for (int c = 0; c < 3; c++) pose[3 * r + c] = T ? (float)T[4 * r + c] : hp.R[3 * r + c];
@@ -1854,8 +1861,10 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
         }
     }
     hipLaunchKernelGGL(k_pose_set, dim3(1), dim3(1), 0, ctx->stream, T_dev, hp, icp->pose_dev,
-                       icp->pose_hist + (icp->launches & (icp->narrow ? 63 : kHist - 1)) * 12);
+                       icp->pose_hist + (icp->launches & (icp->narrow ? 63 : kHist - 1)) * 12,
+                       (uint32_t)icp->launches);
     a.pose = icp->pose_dev;  // every kernel reads the pose (and the previous one) from HBM
+    a.launch_dev = (const uint32_t*)(icp->pose_dev + 24);  // ... and the launch index
     for (int k = 0; k < 9; k++) a.R[k] = hp.R[k];
     for (int k = 0; k < 3; k++) a.t[k] = hp.t[k];
     a.r2 = rmax * rmax;
@@ -1908,6 +1917,61 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     PCP_HIP(ctx, hipEventRecord(e0, ctx->stream));
     const bool verify = a.g.dense && icp->launches > 0;  // the first launch has nothing cached
     icp->last_verified = verify;
+    // A device-pose launch after the first is the same five kernels every time (verify, list
+    // concatenation, octant search, list concatenation, fallback) with the same arguments: the
+    // launch index is read from the device (k_pose_set) and the pose was already.  So the section
+    // is captured once per handle into a HIP graph and replayed -- one launch instead of five.
+    if (T_dev && verify && !icp->dbg && !corr_idx && !args_out && !icp->graph_off) {
+        a.oct_g = icp->oct_g_list;
+        a.ring_g = icp->ring_g;
+        auto section = [&](hipStream_t st) {
+            IcpArgs b = a;
+            b.partials = part_v;
+            hipLaunchKernelGGL(k_icp_verify, dim3(icp->nb_ver), dim3(kIcpBlock), 0, st, b);
+            hipLaunchKernelGGL(k_list_compact, dim3((unsigned)((b.nseg_v + 3) / 4)), dim3(256), 0, st,
+                               (const int32_t*)icp->sv, (const uint32_t*)icp->sv_count, b.nseg_v, b.sv_seg, icp->svc,
+                               icp->sv_off + b.nseg_v);
+            b.partials = part_o;
+            hipLaunchKernelGGL(k_icp_octant<PCP_OCT_WAVES_LIST>, dim3(icp->nb_fast_l), dim3(kIcpBlock), 0, st, b,
+                               (const int32_t*)icp->svc, (const uint32_t*)(icp->sv_off + b.nseg_v));
+            hipLaunchKernelGGL(k_list_compact, dim3((unsigned)((b.nseg + 3) / 4)), dim3(256), 0, st,
+                               (const int32_t*)icp->fb, (const uint32_t*)icp->fb_count, b.nseg, b.fb_seg, icp->fbc,
+                               icp->fb_off + b.nseg);
+            b.partials = part_r;
+            hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, st, b, part_r,
+                               (const int32_t*)icp->fbc, (const uint32_t*)(icp->fb_off + b.nseg));
+        };
+        if (icp->gexec && icp->graph_r2 != a.r2) {  // captured for another rmax (replays are stream-ordered)
+            (void)hipStreamSynchronize(ctx->stream);
+            (void)hipGraphExecDestroy(icp->gexec);
+            icp->gexec = nullptr;
+        }
+        if (!icp->gexec) {
+            hipError_t e = icp->gstream ? hipSuccess : hipStreamCreateWithFlags(&icp->gstream, hipStreamNonBlocking);
+            hipGraph_t gr = nullptr;
+            if (e == hipSuccess) e = hipStreamBeginCapture(icp->gstream, hipStreamCaptureModeThreadLocal);
+            if (e == hipSuccess) {
+                section(icp->gstream);
+                e = hipStreamEndCapture(icp->gstream, &gr);
+            }
+            if (e == hipSuccess) e = hipGraphInstantiate(&icp->gexec, gr, nullptr, nullptr, 0);
+            if (gr) (void)hipGraphDestroy(gr);
+            if (e != hipSuccess) {  // launch the kernels one by one from now on
+                icp->gexec = nullptr;
+                icp->graph_off = true;
+                (void)hipGetLastError();
+            }
+            icp->graph_r2 = a.r2;
+        }
+        if (icp->gexec) PCP_HIP(ctx, hipGraphLaunch(icp->gexec, ctx->stream));
+        else section(ctx->stream);
+        PCP_HIP(ctx, hipEventRecord(e1, ctx->stream));
+        hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kAcc * kRedGroups), 0, ctx->stream, icp->partials,
+                           icp->nb_ver + icp->nb_fast + icp->nb_ring, acc_dev, (const uint32_t*)(icp->fb_off + a.nseg));
+        icp->launches++;
+        PCP_LAUNCH_CHECK(ctx);
+        return PCP_OK;
+    }
     if (a.g.dense) {
         // 1. settle what the candidate caches can; the rest -> search list
         if (verify) {
@@ -2136,7 +2200,7 @@ int icp_make(pcp_ctx* ctx, const pcp_index* target, QXyz* q3, int32_t* qi, int64
     icp->nseg_v = nwaves_v;
     int rc = dmalloc(ctx, &icp->partials, (size_t)(icp->nb_ver + icp->nb_fast + icp->nb_ring) * kAcc);
     if (!rc) rc = dmalloc(ctx, &icp->acc, kAcc);
-    if (!rc) rc = dmalloc(ctx, &icp->pose_dev, 24);
+    if (!rc) rc = dmalloc(ctx, &icp->pose_dev, 32);  // 24 pose floats + the launch index
     // 12-byte cache records when every position (and the far sentinel) fits 26 bits
     icp->narrow = target->n + 1 < (int64_t)kPos26;
     const int rw = icp->narrow ? 3 : 4;  // words per record
@@ -2155,7 +2219,7 @@ int icp_make(pcp_ctx* ctx, const pcp_index* target, QXyz* q3, int32_t* qi, int64
                          : hipMemsetAsync(icp->cand + r0 * rw, 0xff, (size_t)nr * 16, ctx->stream);
     if (!rc && (me != hipSuccess ||
                 hipMemsetAsync(icp->pose_hist, 0, kHist * 12 * sizeof(float), ctx->stream) != hipSuccess ||
-                hipMemsetAsync(icp->pose_dev, 0, 24 * sizeof(float), ctx->stream) != hipSuccess))
+                hipMemsetAsync(icp->pose_dev, 0, 32 * sizeof(float), ctx->stream) != hipSuccess))
         rc = set_error(ctx, PCP_ERR_HIP, "memset");
     if (!rc) rc = dmalloc(ctx, &icp->sv, (size_t)icp->nseg_v * icp->sv_seg + 1);
     if (!rc) rc = dmalloc(ctx, &icp->sv_count, (size_t)icp->nseg_v);
@@ -2270,6 +2334,11 @@ int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, i
         icp->cand = w;
         icp->narrow = false;
     }
+    if (icp->gexec) {  // captured with the old lanes / flags
+        (void)hipStreamSynchronize(icp->ctx->stream);
+        (void)hipGraphExecDestroy(icp->gexec);
+        icp->gexec = nullptr;
+    }
     icp->oct_g_first = oct_lanes_first ? oct_lanes_first : 1;
     icp->oct_g_list = oct_lanes_list;
     icp->ring_g = ring_lanes;
@@ -2280,6 +2349,11 @@ int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, i
 int pcp_icp_destroy(pcp_icp* icp) {
     if (!icp) return PCP_ERR_ARG;
     (void)hipSetDevice(icp->owner->device);
+    if (icp->gexec) {  // (after its last replay has run)
+        (void)hipStreamSynchronize(icp->ctx->stream);
+        (void)hipGraphExecDestroy(icp->gexec);
+    }
+    if (icp->gstream) (void)hipStreamDestroy(icp->gstream);
     pcp::dfree(icp->owner, icp->q);
     pcp::dfree(icp->owner, icp->qidx);
     pcp::dfree(icp->owner, icp->partials);

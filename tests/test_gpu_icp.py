@@ -58,12 +58,13 @@ def test_correspondence_bit_exact(ctx, cell):
         assert np.allclose(gacc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * scale)
 
 
-@pytest.mark.parametrize("create", ["separate", "combined"])
+@pytest.mark.parametrize("create", ["separate", "combined", "combined_auto_cell"])
 def test_registration_exact_every_iteration(ctx, create):
     """A registration through both create paths (pcp_index_build_f32 + pcp_icp_create, and
     pcp_icp_create_with_target, whose query sort runs on a second stream during the target's cell
-    sort): correspondences bit-exact and accumulators equal to the oracle's direct sums at every
-    iteration."""
+    sort -- with a given cell size, and with the automatic one, whose query sort starts only after
+    the cell-size refinement): correspondences bit-exact and accumulators equal to the oracle's
+    direct sums at every iteration."""
     from pointcloudprocess_amd import ops, synth
     T_true = synth.rigid()
     tgt, q = _pair(250_000, 41, T_true)
@@ -71,8 +72,10 @@ def test_registration_exact_every_iteration(ctx, create):
         index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
         icp = ops.ICP(index, q.to(ctx.device))
     else:
-        icp = ops.ICP.with_target(ctx, tgt.to(ctx.device), q.to(ctx.device), 0.1)
+        icp = ops.ICP.with_target(ctx, tgt.to(ctx.device), q.to(ctx.device), 0.1 if create == "combined" else 0.0)
         index = icp.index
+        if create == "combined_auto_cell":
+            assert 0.01 < index.cell_size() < 1.0
     oi = ora.F32Index(tgt.numpy())
     T = np.eye(4)
     for it in range(10):
@@ -311,6 +314,36 @@ def test_device_loop_matches_oracle_and_host_loop(ctx):
     # solve can flip the fp32 cast of the pose and with it a few correspondences
     herr, hT = icp.run(np.eye(4), 0.25, 20)
     assert np.abs(hT - T).max() < 1e-6 and abs(herr - st[1]) < 1e-6
+
+
+def test_device_loop_graph_replay_equals_plain_launches(ctx):
+    """Device-pose launches after the first replay one captured HIP graph of the verify .. fallback
+    section (the launch index is read from the device).  Its accumulators equal, bit for bit, those
+    of plain launches at the same poses on a second engine (the host-pose path with correspondence
+    output never uses the graph), and those plain launches' correspondences equal the oracle's."""
+    from pointcloudprocess_amd import ops, synth
+    T_true = synth.rigid()
+    tgt, q = _pair(200_000, 61, T_true)
+    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
+    icp = ops.ICP(index, q.to(ctx.device))
+    T_dev, stats = icp.new_pose()
+    poses, accs = [], []
+    for _ in range(12):
+        poses.append(T_dev.cpu().numpy().reshape(4, 4).copy())
+        acc = icp.step_dev(T_dev, 0.25)
+        accs.append(acc.cpu().numpy().copy())
+        icp.solve_dev(acc, T_dev, stats)
+    icp2 = ops.ICP(index, q.to(ctx.device))
+    oi = ora.F32Index(tgt.numpy())
+    for it, T in enumerate(poses):
+        acc2, ci, _ = icp2.step(T, 0.25, corr=True)
+        assert np.array_equal(acc2.cpu().numpy(), accs[it]), f"iteration {it}"
+        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+        ei, _ = oi.correspond(q.numpy(), R, t, 0.25)
+        assert np.array_equal(ci.cpu().numpy(), ei), f"iteration {it}"
+    icp2.close()
+    icp.close()
+    index.close()
 
 
 def test_device_loop_failure_latches(ctx):
