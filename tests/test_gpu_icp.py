@@ -75,7 +75,7 @@ def test_registration_exact_every_iteration(ctx, create):
         icp = ops.ICP.with_target(ctx, tgt.to(ctx.device), q.to(ctx.device), 0.1 if create == "combined" else 0.0)
         index = icp.index
         if create == "combined_auto_cell":
-            assert 0.01 < index.cell_size() < 1.0
+            assert 0.01 < index.cell_size < 1.0
     oi = ora.F32Index(tgt.numpy())
     T = np.eye(4)
     for it in range(10):
