@@ -75,7 +75,6 @@ struct pcp_icp {
     uint32_t last_fallback = 0;
     uint32_t last_searched = 0;   // queries the verify pass could not certify (searched)
     hipGraphExec_t gexec = nullptr;  // the verify .. fallback section of a device-pose launch (icp_launch)
-    hipStream_t gstream = nullptr;   // its capture stream
     float graph_r2 = 0.f;            // the rmax^2 it was captured with
     bool graph_off = false;          // capture failed: plain launches
 };
@@ -98,6 +97,9 @@ constexpr int kIcpBlock = 256;
 #define PCP_RING_WAVES 6
 #endif
 constexpr int kAcc = 24;
+#ifndef PCP_ICP_GRAPH  // 0: every launch enqueues its kernels one by one (A/B builds)
+#define PCP_ICP_GRAPH 1
+#endif
 
 struct IcpArgs {
     GridDesc g;
@@ -1921,7 +1923,7 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     // concatenation, octant search, list concatenation, fallback) with the same arguments: the
     // launch index is read from the device (k_pose_set) and the pose was already.  So the section
     // is captured once per handle into a HIP graph and replayed -- one launch instead of five.
-    if (T_dev && verify && !icp->dbg && !corr_idx && !args_out && !icp->graph_off) {
+    if (PCP_ICP_GRAPH && T_dev && verify && !icp->dbg && !corr_idx && !args_out && !icp->graph_off) {
         a.oct_g = icp->oct_g_list;
         a.ring_g = icp->ring_g;
         auto section = [&](hipStream_t st) {
@@ -1946,13 +1948,14 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
             (void)hipGraphExecDestroy(icp->gexec);
             icp->gexec = nullptr;
         }
-        if (!icp->gexec) {
-            hipError_t e = icp->gstream ? hipSuccess : hipStreamCreateWithFlags(&icp->gstream, hipStreamNonBlocking);
+        if (!icp->gexec) {  // captured on the context's side stream (capture enqueues nothing)
+            hipStream_t cap = nullptr;
+            hipError_t e = side_stream(ctx, &cap) == PCP_OK ? hipSuccess : hipErrorInvalidValue;
             hipGraph_t gr = nullptr;
-            if (e == hipSuccess) e = hipStreamBeginCapture(icp->gstream, hipStreamCaptureModeThreadLocal);
+            if (e == hipSuccess) e = hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
             if (e == hipSuccess) {
-                section(icp->gstream);
-                e = hipStreamEndCapture(icp->gstream, &gr);
+                section(cap);
+                e = hipStreamEndCapture(cap, &gr);
             }
             if (e == hipSuccess) e = hipGraphInstantiate(&icp->gexec, gr, nullptr, nullptr, 0);
             if (gr) (void)hipGraphDestroy(gr);
@@ -2353,7 +2356,6 @@ int pcp_icp_destroy(pcp_icp* icp) {
         (void)hipStreamSynchronize(icp->ctx->stream);
         (void)hipGraphExecDestroy(icp->gexec);
     }
-    if (icp->gstream) (void)hipStreamDestroy(icp->gstream);
     pcp::dfree(icp->owner, icp->q);
     pcp::dfree(icp->owner, icp->qidx);
     pcp::dfree(icp->owner, icp->partials);

@@ -1,4 +1,4 @@
-# Round-5 records, in parts (each call stays well inside gpurun's limit):
+# Round-6 records, in parts (each call stays well inside gpurun's limit):
 #   PART=tests  the GPU suite + smoke
 #   PART=pmc    FETCH_SIZE / WRITE_SIZE passes (separate runs) of the C4, C5, C3 and C2 lines,
 #               summarised into profiles/$PTAG/pmc_traffic*.json keyed on the sources' sha1 and the
@@ -9,7 +9,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-final}; mkdir -p $O
-P=profiles/${PTAG:-r05_final}; mkdir -p $P
+P=profiles/${PTAG:-r06_final}; mkdir -p $P
 case ${PART} in
 tests)
   timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $O/gpu_tests.log 2>&1
