@@ -83,6 +83,8 @@ def parse():
                          "caller order), 'cells' in the index's own cell order, instead of the generator's random "
                          "order; the headline is 'native'")
     ap.add_argument("--config", choices=("C1", "C2", "C3", "C4", "C5"), default="C4")
+    ap.add_argument("--icp-graph", action="store_true",
+                    help="replay one captured HIP graph per ICP launch (PCP_ICP_OPT_GRAPH; identical results)")
     ap.add_argument("--icp-lanes", type=str, default="",
                     help="profiling: 'first,list,ring' lanes per query of the ICP passes (0 = the library's choice)")
     return ap.parse_args()
@@ -244,6 +246,7 @@ def main():
     from pointcloudprocess_amd import ops, synth
     if args.icp_lanes:  # profiling: fixed lanes per query (results are identical for every choice)
         D.GpuEngine.lane_options = tuple(int(v) for v in args.icp_lanes.split(","))
+    D.GpuEngine.graph = bool(args.icp_graph)
 
     # a fatal signal prints the Python stack (faulthandler) and, first, the faulting native
     # library and frames (libpcp's dladdr report, which then chains to faulthandler)

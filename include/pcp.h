@@ -276,6 +276,11 @@ int pcp_icp_create_with_target(pcp_ctx* ctx, const float* target_dev, size_t tar
 /* not an ablation: keep 16-byte cache records although the target fits the 12-byte form
  * (< 2^26 - 2 points); only before the handle's first launch.  Results are identical. */
 #define PCP_ICP_OPT_WIDE_CACHE 128
+/* not an ablation: device-pose launches after the first replay ONE captured HIP graph of the
+ * verify .. fallback section instead of enqueueing its five kernels (results are identical).
+ * Off by default: the device loop is host-asynchronous, so enqueueing is never what the GPU
+ * waits for, and the replayed section measured 0.5 % slower per iteration. */
+#define PCP_ICP_OPT_GRAPH 256
 int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, int ring_lanes, int ablate);
 int pcp_icp_destroy(pcp_icp* icp);
 /* One iteration at pose T (row-major 4x4 double, cast to fp32 for the kernel):

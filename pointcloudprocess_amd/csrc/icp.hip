@@ -77,6 +77,7 @@ struct pcp_icp {
     hipGraphExec_t gexec = nullptr;  // the verify .. fallback section of a device-pose launch (icp_launch)
     float graph_r2 = 0.f;            // the rmax^2 it was captured with
     bool graph_off = false;          // capture failed: plain launches
+    bool graph = false;              // PCP_ICP_OPT_GRAPH
 };
 
 namespace pcp {
@@ -97,9 +98,6 @@ constexpr int kIcpBlock = 256;
 #define PCP_RING_WAVES 6
 #endif
 constexpr int kAcc = 24;
-#ifndef PCP_ICP_GRAPH  // 0: every launch enqueues its kernels one by one (A/B builds)
-#define PCP_ICP_GRAPH 1
-#endif
 
 struct IcpArgs {
     GridDesc g;
@@ -1921,9 +1919,11 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     icp->last_verified = verify;
     // A device-pose launch after the first is the same five kernels every time (verify, list
     // concatenation, octant search, list concatenation, fallback) with the same arguments: the
-    // launch index is read from the device (k_pose_set) and the pose was already.  So the section
-    // is captured once per handle into a HIP graph and replayed -- one launch instead of five.
-    if (PCP_ICP_GRAPH && T_dev && verify && !icp->dbg && !corr_idx && !args_out && !icp->graph_off) {
+    // launch index is read from the device (k_pose_set) and the pose was already.  With
+    // PCP_ICP_OPT_GRAPH the section is captured once per handle into a HIP graph and replayed --
+    // one launch instead of five (measured: host enqueue is not what the loop waits for, and the
+    // replayed section ran 0.5 % slower, so it is off by default).
+    if (icp->graph && T_dev && verify && !icp->dbg && !corr_idx && !args_out && !icp->graph_off) {
         a.oct_g = icp->oct_g_list;
         a.ring_g = icp->ring_g;
         auto section = [&](hipStream_t st) {
@@ -2345,7 +2345,8 @@ int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, i
     icp->oct_g_first = oct_lanes_first ? oct_lanes_first : 1;
     icp->oct_g_list = oct_lanes_list;
     icp->ring_g = ring_lanes;
-    icp->dbg = ablate & ~PCP_ICP_OPT_WIDE_CACHE;
+    icp->dbg = ablate & ~(PCP_ICP_OPT_WIDE_CACHE | PCP_ICP_OPT_GRAPH);
+    icp->graph = (ablate & PCP_ICP_OPT_GRAPH) != 0;
     return PCP_OK;
 }
 

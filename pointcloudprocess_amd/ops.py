@@ -340,13 +340,16 @@ class ICP:
         return cls(index, q, _handle=hq)
 
     WIDE_CACHE = 128  # PCP_ICP_OPT_WIDE_CACHE
+    GRAPH = 256       # PCP_ICP_OPT_GRAPH
 
-    def set_options(self, oct_lanes_first=1, oct_lanes_list=0, ring_lanes=0, ablate=0, wide_cache=False):
+    def set_options(self, oct_lanes_first=1, oct_lanes_list=0, ring_lanes=0, ablate=0, wide_cache=False,
+                    graph=False):
         """Test / profiling controls (pcp_icp_set_options): lanes per query of the octant pass
         (first launch, later lists; 0 = by density) and of the fallback pass (0 = by length);
         `ablate` switches passes off (results are then wrong); `wide_cache` keeps 16-byte cache
-        records (before the first step; results are identical)."""
-        flags = int(ablate) | (self.WIDE_CACHE if wide_cache else 0)
+        records (before the first step); `graph` replays one captured HIP graph per device-pose
+        launch (results are identical in both cases)."""
+        flags = int(ablate) | (self.WIDE_CACHE if wide_cache else 0) | (self.GRAPH if graph else 0)
         self.ctx.check(self.ctx.lib.pcp_icp_set_options(self.h, int(oct_lanes_first), int(oct_lanes_list),
                                                         int(ring_lanes), flags))
 

@@ -317,8 +317,8 @@ def test_device_loop_matches_oracle_and_host_loop(ctx):
 
 
 def test_device_loop_graph_replay_equals_plain_launches(ctx):
-    """Device-pose launches after the first replay one captured HIP graph of the verify .. fallback
-    section (the launch index is read from the device).  Its accumulators equal, bit for bit, those
+    """With PCP_ICP_OPT_GRAPH, device-pose launches after the first replay one captured HIP graph of
+    the verify .. fallback section (the launch index is read from the device).  Its accumulators equal, bit for bit, those
     of plain launches at the same poses on a second engine (the host-pose path with correspondence
     output never uses the graph), and those plain launches' correspondences equal the oracle's."""
     from pointcloudprocess_amd import ops, synth
@@ -326,6 +326,7 @@ def test_device_loop_graph_replay_equals_plain_launches(ctx):
     tgt, q = _pair(200_000, 61, T_true)
     index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
     icp = ops.ICP(index, q.to(ctx.device))
+    icp.set_options(graph=True)
     T_dev, stats = icp.new_pose()
     poses, accs = [], []
     for _ in range(12):
