@@ -85,9 +85,6 @@ def parse():
     ap.add_argument("--config", choices=("C1", "C2", "C3", "C4", "C5"), default="C4")
     ap.add_argument("--icp-graph", action="store_true",
                     help="replay one captured HIP graph per ICP launch (PCP_ICP_OPT_GRAPH; identical results)")
-    ap.add_argument("--icp-pieces", type=int, default=1,
-                    help="pipelined ICP launches: verify of one piece of the queries beside the search of the "
-                         "previous one (PCP_ICP_OPT_PIECES, 1 = off)")
     ap.add_argument("--icp-lanes", type=str, default="",
                     help="profiling: 'first,list,ring' lanes per query of the ICP passes (0 = the library's choice)")
     return ap.parse_args()
@@ -250,7 +247,6 @@ def main():
     if args.icp_lanes:  # profiling: fixed lanes per query (results are identical for every choice)
         D.GpuEngine.lane_options = tuple(int(v) for v in args.icp_lanes.split(","))
     D.GpuEngine.graph = bool(args.icp_graph)
-    D.GpuEngine.pieces = int(args.icp_pieces)
 
     # a fatal signal prints the Python stack (faulthandler) and, first, the faulting native
     # library and frames (libpcp's dladdr report, which then chains to faulthandler)

@@ -281,11 +281,6 @@ int pcp_icp_create_with_target(pcp_ctx* ctx, const float* target_dev, size_t tar
  * Off by default: the device loop is host-asynchronous, so enqueueing is never what the GPU
  * waits for, and the replayed section measured 0.5 % slower per iteration. */
 #define PCP_ICP_OPT_GRAPH 256
-/* not an ablation: pipelined device-pose launches -- the queries cut into k pieces (2 <= k <= 8),
- * the verify pass of piece p + 1 running beside the search of piece p on a second stream.  Only
- * before the handle's first launch.  Correspondences are identical; the accumulators' partial
- * sums are grouped differently (equal to rounding).  PCP_ICP_OPT_PIECES(1) = off (the default). */
-#define PCP_ICP_OPT_PIECES(k) (((((k) - 1) & 7)) << 9)
 int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, int ring_lanes, int ablate);
 int pcp_icp_destroy(pcp_icp* icp);
 /* One iteration at pose T (row-major 4x4 double, cast to fp32 for the kernel):

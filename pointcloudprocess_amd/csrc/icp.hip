@@ -78,12 +78,6 @@ struct pcp_icp {
     float graph_r2 = 0.f;            // the rmax^2 it was captured with
     bool graph_off = false;          // capture failed: plain launches
     bool graph = false;              // PCP_ICP_OPT_GRAPH
-    int pieces = 1;                  // PCP_ICP_OPT_PIECES: pipelined verify / search pieces
-    int64_t prow_v = 0, prow_o = 0;  // pieces mode: partial rows of the verify / search launches
-    int64_t prow_total = 0;          // ... in all (with the fallback pass's)
-    int64_t pseg_total = 0;          // search segments of the last pipelined launch
-    uint32_t* piece_cnt = nullptr;   // per piece: its search list's length
-    hipEvent_t pev[9] = {};          // per piece: its list is ready; [K]: every search is done
 };
 
 namespace pcp {
@@ -144,8 +138,6 @@ struct IcpArgs {
     int ring_g;         // fallback pass lanes per query: 1, 2, 4, 8, or 0 = PCP_RING_G / by length
     const float* pose;  // device poses (current, previous: 24 floats) overriding R/t, Rp/tq, or null
     const uint32_t* launch_dev;  // device copy of `launch` (k_pose_set), so a captured launch graph replays
-    int64_t v_c0, v_c1;  // verify pass: its 64-query chunk range (v_c1 = 0: every chunk)
-    int64_t lane_nq;     // octant pass: the query count its density rule measures the list against
 };
 
 // sorted query i as {x, y, z, 0}
@@ -717,13 +709,11 @@ __global__ void __launch_bounds__(kIcpBlock, PCP_VER_WAVES) k_icp_verify(IcpArgs
     load_pose(a);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * kW + wid;
-    // the chunks of this launch: all, or a piece [v_c0, v_c1) (pipelined launches)
-    const int64_t c_lo = a.v_c1 > 0 ? a.v_c0 : 0;
-    const int64_t nch = (a.v_c1 > 0 ? a.v_c1 : (a.nq + 63) / 64) - c_lo;
-    // contiguous ranges: wave w owns chunks c_lo + [w*nch/nwaves, (w+1)*nch/nwaves)
+    const int64_t nch = (a.nq + 63) / 64;
+    // contiguous ranges: wave w owns chunks [w*nch/nwaves, (w+1)*nch/nwaves)
     const int64_t nwaves = (int64_t)gridDim.x * kW;
-    const int64_t cstart_ = c_lo + gw * nch / nwaves;
-    const int64_t nsteps = c_lo + (gw + 1) * nch / nwaves - cstart_;
+    const int64_t cstart_ = gw * nch / nwaves;
+    const int64_t nsteps = (gw + 1) * nch / nwaves - cstart_;
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
     __syncthreads();
     uint32_t svn = 0;
@@ -1258,7 +1248,7 @@ __global__ void __launch_bounds__(kIcpBlock, MINW) k_icp_octant(IcpArgs a, const
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n = list ? (int64_t)*list_n : a.nq;
     if (lane < kAcc) s_acc[wid][lane] = 0.0;
-    const int G = a.oct_g ? a.oct_g : octant_lanes(n, a.lane_nq);  // uniform over the grid
+    const int G = a.oct_g ? a.oct_g : octant_lanes(n, a.nq);  // uniform over the grid
     if (G == 1)
         octant_run<1>(a, list, n, s_acc);
     else if (G == 2)
@@ -1851,76 +1841,6 @@ __global__ void k_icp_solve_dev(const double* acc, int do_scale, double* T, doub
     for (int k = 0; k < 16; k++) T[k] = Tn[k];
 }
 
-// Pipelined launch (PCP_ICP_OPT_PIECES): the sorted queries are cut into K pieces of whole
-// chunks.  The verify pass of piece p + 1 runs on the context's stream while the octant search of
-// piece p's list runs on the side stream, so the HBM-bound verify and the address-bound search
-// share the GPU instead of following each other.  The first verify piece and the last search
-// piece run alone on the full grid; the overlapped ones on half grids each.  Every launch writes
-// its own partial rows and list segments (offset pointers), so the reduction and the fallback list
-// see exactly the rows and entries of the sequential form, only split differently; the results are
-// the sequential form's correspondences, and accumulators equal to rounding.
-int icp_pieces(pcp_icp* icp, IcpArgs a, double* part, double* acc_dev) {
-    pcp_ctx* ctx = icp->ctx;
-    const int K = icp->pieces;
-    hipStream_t side = nullptr;
-    PCP_TRY(side_stream(ctx, &side));
-    const int64_t nch = (icp->nq + 63) / 64;
-    const int nbv_half = std::max(1, icp->nb_ver / 2), nbo_half = std::max(1, icp->nb_fast_l / 2);
-    int64_t row = 0, vseg = 0, oseg = 0;
-    for (int p = 0; p < K; p++) {
-        const int64_t c0 = nch * p / K, c1 = nch * (p + 1) / K;
-        // verify piece p (context stream) -> its list, compacted at svc + c0 * 64
-        IcpArgs b = a;
-        const int nbv = p == 0 ? icp->nb_ver : nbv_half;
-        b.v_c0 = c0;
-        b.v_c1 = c1;
-        b.partials = part + row * kAcc;
-        b.sv = icp->sv + vseg * icp->sv_seg;
-        b.sv_count = icp->sv_count + vseg;
-        if (c1 > c0)
-            hipLaunchKernelGGL(k_icp_verify, dim3(nbv), dim3(kIcpBlock), 0, ctx->stream, b);
-        else
-            PCP_HIP(ctx, hipMemsetAsync(b.partials, 0, (size_t)nbv * kAcc * sizeof(double), ctx->stream));
-        const int64_t nwv = (int64_t)nbv * (kIcpBlock / 64);
-        if (c1 > c0)
-            hipLaunchKernelGGL(k_list_compact, dim3((unsigned)((nwv + 3) / 4)), dim3(256), 0, ctx->stream,
-                               (const int32_t*)b.sv, (const uint32_t*)b.sv_count, nwv, icp->sv_seg, icp->svc + c0 * 64,
-                               icp->piece_cnt + p);
-        else
-            PCP_HIP(ctx, hipMemsetAsync(icp->piece_cnt + p, 0, sizeof(uint32_t), ctx->stream));
-        row += nbv;
-        vseg += nwv;
-        PCP_HIP(ctx, hipEventRecord(icp->pev[p], ctx->stream));
-        // octant search of piece p's list (side stream, after its verify and list)
-        PCP_HIP(ctx, hipStreamWaitEvent(side, icp->pev[p], 0));
-        const int nbo = p == K - 1 ? icp->nb_fast_l : nbo_half;
-        IcpArgs o = a;
-        o.oct_g = icp->oct_g_list;
-        o.lane_nq = std::max<int64_t>(1, std::min<int64_t>(c1 * 64, icp->nq) - c0 * 64);
-        o.fb = icp->fb + oseg * icp->fb_seg;
-        o.fb_count = icp->fb_count + oseg;
-        o.nb_fast = nbo;                               // no rows past its own grid to clear
-        o.nseg = (int64_t)nbo * (kIcpBlock / 64);      // nor segments
-        o.partials = part + (icp->prow_v + (oseg / (kIcpBlock / 64))) * kAcc;
-        hipLaunchKernelGGL(k_icp_octant<PCP_OCT_WAVES_LIST>, dim3(nbo), dim3(kIcpBlock), 0, side, o,
-                           (const int32_t*)(icp->svc + c0 * 64), (const uint32_t*)(icp->piece_cnt + p));
-        oseg += o.nseg;
-    }
-    // the fallback list over every search piece's segments, then the fallback pass
-    PCP_HIP(ctx, hipEventRecord(icp->pev[K], side));
-    PCP_HIP(ctx, hipStreamWaitEvent(ctx->stream, icp->pev[K], 0));
-    hipLaunchKernelGGL(k_list_compact, dim3((unsigned)((oseg + 3) / 4)), dim3(256), 0, ctx->stream,
-                       (const int32_t*)icp->fb, (const uint32_t*)icp->fb_count, oseg, icp->fb_seg, icp->fbc,
-                       icp->fb_off + oseg);
-    IcpArgs r = a;
-    r.partials = part + (icp->prow_v + icp->prow_o) * kAcc;
-    r.ring_g = icp->ring_g;
-    hipLaunchKernelGGL(k_icp_ring, dim3(icp->nb_ring), dim3(kIcpBlock), 0, ctx->stream, r, r.partials,
-                       (const int32_t*)icp->fbc, (const uint32_t*)(icp->fb_off + oseg));
-    icp->pseg_total = oseg;
-    return PCP_OK;
-}
-
 // T (host) or T_dev (device pose, read by k_pose_from_T) -- exactly one is non-null
 int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, int32_t* corr_idx,
                float* corr_d2, const double* T_dev = nullptr, IcpArgs* args_out = nullptr) {
@@ -1933,7 +1853,6 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     a.qidx = icp->qidx;
     a.nq = icp->nq;
     a.nchunks = (icp->nq + kIcpBlock - 1) / kIcpBlock;
-    a.lane_nq = icp->nq;
     HostPose hp{};
     if (!T_dev) {
         for (int r = 0; r < 3; r++) {
@@ -2004,15 +1923,6 @@ int icp_launch(pcp_icp* icp, const double T[16], float rmax, double* acc_dev, in
     // PCP_ICP_OPT_GRAPH the section is captured once per handle into a HIP graph and replayed --
     // one launch instead of five (measured: host enqueue is not what the loop waits for, and the
     // replayed section ran 0.5 % slower, so it is off by default).
-    if (icp->pieces > 1 && T_dev && verify && !icp->dbg && !corr_idx && !args_out) {
-        PCP_TRY(icp_pieces(icp, a, part_v, acc_dev));
-        PCP_HIP(ctx, hipEventRecord(e1, ctx->stream));
-        hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kAcc * kRedGroups), 0, ctx->stream, icp->partials,
-                           icp->prow_total, acc_dev, (const uint32_t*)(icp->fb_off + icp->pseg_total));
-        icp->launches++;
-        PCP_LAUNCH_CHECK(ctx);
-        return PCP_OK;
-    }
     if (icp->graph && T_dev && verify && !icp->dbg && !corr_idx && !args_out && !icp->graph_off) {
         a.oct_g = icp->oct_g_list;
         a.ring_g = icp->ring_g;
@@ -2416,50 +2326,6 @@ int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, i
     const bool widen = (ablate & PCP_ICP_OPT_WIDE_CACHE) && icp->narrow;
     if (widen && icp->launches > 0)
         return pcp::set_error(ctx, PCP_ERR_ARG, "PCP_ICP_OPT_WIDE_CACHE only before the handle's first launch");
-    const int K = ((ablate >> 9) & 7) + 1;
-    if (K != icp->pieces && icp->launches > 0)
-        return pcp::set_error(ctx, PCP_ERR_ARG, "PCP_ICP_OPT_PIECES only before the handle's first launch");
-    if (K != icp->pieces && K > 1) {  // list segments, partial rows and events of the pipelined form
-        using pcp::kIcpBlock;
-        using pcp::kAcc;
-        const int64_t wv = (int64_t)icp->nb_ver * (kIcpBlock / 64), wo = (int64_t)icp->nb_fast_l * (kIcpBlock / 64);
-        const int64_t vsegs = wv + (K - 1) * (std::max(1, icp->nb_ver / 2) * (int64_t)(kIcpBlock / 64));
-        const int64_t osegs = wo + (K - 1) * (std::max(1, icp->nb_fast_l / 2) * (int64_t)(kIcpBlock / 64));
-        const int64_t prv = icp->nb_ver + (int64_t)(K - 1) * std::max(1, icp->nb_ver / 2);
-        const int64_t pro = icp->nb_fast_l + (int64_t)(K - 1) * std::max(1, icp->nb_fast_l / 2);
-        const int64_t rows = std::max<int64_t>(prv + pro + icp->nb_ring, icp->nb_ver + icp->nb_fast + icp->nb_ring);
-        const int64_t fsegs = std::max<int64_t>(osegs, (int64_t)icp->nb_fast * (kIcpBlock / 64));
-        int32_t *sv = nullptr, *fb = nullptr;
-        uint32_t *svn = nullptr, *fbn = nullptr, *fbo = nullptr, *pc = nullptr;
-        double* part = nullptr;
-        hipEvent_t ev[9] = {};
-        int rc = pcp::dmalloc(ctx, &sv, (size_t)(vsegs * icp->sv_seg + 1));
-        if (!rc) rc = pcp::dmalloc(ctx, &svn, (size_t)vsegs);
-        if (!rc) rc = pcp::dmalloc(ctx, &fb, (size_t)std::max<int64_t>(fsegs * icp->fb_seg, icp->nq) + 1);
-        if (!rc) rc = pcp::dmalloc(ctx, &fbn, (size_t)fsegs);
-        if (!rc) rc = pcp::dmalloc(ctx, &fbo, (size_t)fsegs + 1);
-        if (!rc) rc = pcp::dmalloc(ctx, &pc, (size_t)K + 1);
-        if (!rc) rc = pcp::dmalloc(ctx, &part, (size_t)rows * kAcc);
-        for (int e = 0; e <= K && !rc; e++)
-            if (pcp::event_get(ctx, &ev[e]) != hipSuccess) rc = pcp::set_error(ctx, PCP_ERR_HIP, "hipEventCreate");
-        if (rc) {
-            pcp::dfree(ctx, sv); pcp::dfree(ctx, svn); pcp::dfree(ctx, fb); pcp::dfree(ctx, fbn);
-            pcp::dfree(ctx, fbo); pcp::dfree(ctx, pc); pcp::dfree(ctx, part);
-            for (int e = 0; e <= K; e++) if (ev[e]) pcp::event_put(ctx, ev[e]);
-            return rc;
-        }
-        pcp::dfree(ctx, icp->sv); pcp::dfree(ctx, icp->sv_count); pcp::dfree(ctx, icp->fb);
-        pcp::dfree(ctx, icp->fb_count); pcp::dfree(ctx, icp->fb_off); pcp::dfree(ctx, icp->piece_cnt);
-        pcp::dfree(ctx, icp->partials);
-        for (auto& e : icp->pev) if (e) { pcp::event_put(ctx, e); e = nullptr; }
-        icp->sv = sv; icp->sv_count = svn; icp->fb = fb; icp->fb_count = fbn; icp->fb_off = fbo;
-        icp->piece_cnt = pc; icp->partials = part;
-        for (int e = 0; e <= K; e++) icp->pev[e] = ev[e];
-        icp->prow_v = prv;
-        icp->prow_o = pro;
-        icp->prow_total = prv + pro + icp->nb_ring;
-    }
-    icp->pieces = K;
     if (widen) {  // re-create the records in the 16-byte form
         uint32_t* w = nullptr;
         if (int rc = pcp::dmalloc(ctx, &w, (size_t)(icp->nq + 1) * 4)) return rc;
@@ -2479,7 +2345,7 @@ int pcp_icp_set_options(pcp_icp* icp, int oct_lanes_first, int oct_lanes_list, i
     icp->oct_g_first = oct_lanes_first ? oct_lanes_first : 1;
     icp->oct_g_list = oct_lanes_list;
     icp->ring_g = ring_lanes;
-    icp->dbg = ablate & ~(PCP_ICP_OPT_WIDE_CACHE | PCP_ICP_OPT_GRAPH | PCP_ICP_OPT_PIECES(8));
+    icp->dbg = ablate & ~(PCP_ICP_OPT_WIDE_CACHE | PCP_ICP_OPT_GRAPH);
     icp->graph = (ablate & PCP_ICP_OPT_GRAPH) != 0;
     return PCP_OK;
 }
@@ -2506,8 +2372,6 @@ int pcp_icp_destroy(pcp_icp* icp) {
     pcp::dfree(icp->owner, icp->fb_count);
     pcp::dfree(icp->owner, icp->fb_off);
     pcp::dfree(icp->owner, icp->fbc);
-    pcp::dfree(icp->owner, icp->piece_cnt);
-    for (auto& e : icp->pev) if (e) pcp::event_put(icp->owner, e);
     pcp::dfree(icp->owner, icp->pose_dev);
     pcp::event_put(icp->owner, icp->ev0);
     pcp::event_put(icp->owner, icp->ev1);

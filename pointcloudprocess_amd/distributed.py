@@ -244,7 +244,6 @@ class GpuEngine:
     # passed to ICP.set_options on every new handle; None = the library's own choices
     lane_options = None
     graph = False  # bench.py --icp-graph: PCP_ICP_OPT_GRAPH on every new handle
-    pieces = 1     # bench.py --icp-pieces: PCP_ICP_OPT_PIECES on every new handle
 
     def __init__(self, ctx, target_xyz, query_xyz, cell_size=0.0):
         self.target = target_xyz.contiguous()
@@ -255,9 +254,8 @@ class GpuEngine:
         else:  # (an A/B build of an older tree, PCP_LIB)
             self.index = ops.GridIndex(ctx, self.target, cell_size=cell_size)
             self.icp = ops.ICP(self.index, query_xyz.contiguous())
-        if GpuEngine.lane_options is not None or GpuEngine.graph or GpuEngine.pieces != 1:
-            self.icp.set_options(*(GpuEngine.lane_options or (1, 0, 0)), graph=GpuEngine.graph,
-                                 pieces=GpuEngine.pieces)
+        if GpuEngine.lane_options is not None or GpuEngine.graph:
+            self.icp.set_options(*(GpuEngine.lane_options or (1, 0, 0)), graph=GpuEngine.graph)
         self.device = ctx.device
         self.nq = query_xyz.shape[0]
 

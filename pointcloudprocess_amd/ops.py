@@ -343,18 +343,13 @@ class ICP:
     GRAPH = 256       # PCP_ICP_OPT_GRAPH
 
     def set_options(self, oct_lanes_first=1, oct_lanes_list=0, ring_lanes=0, ablate=0, wide_cache=False,
-                    graph=False, pieces=1):
+                    graph=False):
         """Test / profiling controls (pcp_icp_set_options): lanes per query of the octant pass
         (first launch, later lists; 0 = by density) and of the fallback pass (0 = by length);
         `ablate` switches passes off (results are then wrong); `wide_cache` keeps 16-byte cache
         records (before the first step); `graph` replays one captured HIP graph per device-pose
-        launch (results are identical in both cases); `pieces` (2..8, before the first step)
-        pipelines device-pose launches: the verify pass of one piece of the queries beside the
-        search of the previous piece (PCP_ICP_OPT_PIECES)."""
-        if not 1 <= int(pieces) <= 8:
-            raise ValueError("pieces must be 1..8")
-        flags = (int(ablate) | (self.WIDE_CACHE if wide_cache else 0) | (self.GRAPH if graph else 0)
-                 | ((int(pieces) - 1) << 9))
+        launch (results are identical in both cases)."""
+        flags = int(ablate) | (self.WIDE_CACHE if wide_cache else 0) | (self.GRAPH if graph else 0)
         self.ctx.check(self.ctx.lib.pcp_icp_set_options(self.h, int(oct_lanes_first), int(oct_lanes_list),
                                                         int(ring_lanes), flags))
 

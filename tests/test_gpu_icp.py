@@ -347,41 +347,6 @@ def test_device_loop_graph_replay_equals_plain_launches(ctx):
     index.close()
 
 
-@pytest.mark.parametrize("pieces", [2, 3, 5])
-def test_device_loop_pipelined_pieces_match_oracle(ctx, pieces):
-    """PCP_ICP_OPT_PIECES: device-pose launches run the verify pass of one piece of the queries
-    beside the search of the previous piece (two streams).  At every iteration's pose the
-    correspondence count equals the oracle's exactly and the accumulators its direct sums to the
-    usual 1e-7; the registration ends within 1e-5 of the oracle's pose."""
-    from pointcloudprocess_amd import ops, synth
-    T_true = synth.rigid()
-    tgt, q = _pair(300_000, 71, T_true)
-    index = ops.GridIndex(ctx, tgt.to(ctx.device), cell_size=0.1)
-    icp = ops.ICP(index, q.to(ctx.device))
-    icp.set_options(pieces=pieces)
-    oi = ora.F32Index(tgt.numpy())
-    T_dev, stats = icp.new_pose()
-    for it in range(12):
-        T = T_dev.cpu().numpy().reshape(4, 4)
-        acc = icp.step_dev(T_dev, 0.25).cpu().numpy().copy()
-        R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
-        ei, ed = oi.correspond(q.numpy(), R, t, 0.25)
-        eacc = ora.icp_accumulate(tgt.numpy(), q.numpy(), R, t, ei, ed)
-        assert acc[0] == eacc[0], f"iteration {it}"
-        assert np.allclose(acc[:23], eacc[:23], rtol=1e-7, atol=1e-8 * np.abs(eacc[:23]).max()), f"iteration {it}"
-        icp.solve_dev(icp.acc, T_dev, stats)
-    icp.close()
-    icp2 = ops.ICP(index, q.to(ctx.device))
-    icp2.set_options(pieces=pieces)
-    T2, st2 = icp2.new_pose()
-    icp2.run_dev(T2, st2, 0.25, 20)
-    eerr, eT = ora.icp(tgt.numpy(), q.numpy(), np.eye(4), 0.25, 20)
-    assert np.abs(T2.cpu().numpy().reshape(4, 4) - eT).max() < 1e-5
-    assert abs(float(st2[1]) - eerr) < 1e-5
-    icp2.close()
-    index.close()
-
-
 def test_device_loop_failure_latches(ctx):
     from pointcloudprocess_amd import ops
     tgt = torch.rand((1000, 3)) * 10

@@ -19,13 +19,6 @@ for st in ${STEPS}; do
 case $st in
 micro)
   timeout -k 10 120 tools/sort_micro > $O/sort_micro.log 2>&1 ;;
-c4pieces)
-  # interleaved A/B of pipelined ICP launches (--icp-pieces K) against sequential ones (K = 1)
-  for rep in 1 2 3; do
-    for K in 1 ${PIECES:-2 4}; do
-      timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 --icp-pieces $K >> $O/c4_pieces_$K.jsonl 2>> $O/c4_pieces.err
-    done
-  done ;;
 c4bench)
   timeout -k 10 300 python3 -u bench.py --no-cpu --steps ${NSTEPS:-5} --warmup 2 >> $O/c4_bench.jsonl 2>> $O/c4_bench.err ;;
 c5bench)
