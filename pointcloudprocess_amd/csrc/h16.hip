@@ -248,12 +248,13 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
                     if (blk + 64u * s >= M) break;  // (uniform) steps past the list are never read
                     const uint32_t j = blk + 64u * s + (uint32_t)lane;
                     const bool ok = j < M;
-                    // the row of list entry j: the largest r with P[r] <= j (binary search over
-                    // the uniform row starts; P[8] then settles the last row)
-                    int r = j >= P[4] ? 4 : 0;
-                    r += j >= (r ? P[6] : P[2]) ? 2 : 0;
-                    r += j >= (r == 0 ? P[1] : r == 2 ? P[3] : r == 4 ? P[5] : P[7]) ? 1 : 0;
-                    r += (r == 7 && j >= P[8]) ? 1 : 0;
+                    // the row of list entry j: the largest r with P[r] <= j = the number of row
+                    // starts P[1..8] at or below j (compares against uniform values, summed: no
+                    // divergent branches; a binary search over selects of P compiled to ~40
+                    // exec-mask branch instructions per step)
+                    int r = 0;
+#pragma unroll
+                    for (int k = 1; k < 9; k++) r += j >= P[k] ? 1 : 0;
                     const uint4 row = s_row[r];
                     const uint32_t kk = ok ? j + row.x : 0u;
                     const uint2 pr = a.rec[kk];
