@@ -193,30 +193,19 @@ __global__ void k_brick_final(int32_t* brick, int64_t nb, const uint32_t* bits) 
 // Cell starts without a count array or a scan.  cstart[c] = first sorted position whose key
 // is >= c, c in [0, ncells].  The cells are cut into chunks of kChunk; k_chunk_lo finds each
 // chunk's first position from the run starts (a run start fills the chunk boundaries of the
-// key gap before it; p = n is a virtual run start closing the table) and counts the runs
-// (non-empty cells, for the auto cell-size check); k_cell_starts then resolves one chunk per
+// key gap before it; p = n is a virtual run start closing the table); k_cell_starts then resolves one chunk per
 // block in LDS (run starts scattered, suffix minimum) and writes it out coalesced.
 constexpr int kChunk = 4096;
 
-__global__ void k_chunk_lo(const uint32_t* key, int64_t n, int64_t nchunk, uint32_t* lo,
-                           unsigned long long* runs) {
-    __shared__ unsigned long long s_cnt;
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    unsigned long long c = 0;
+__global__ void k_chunk_lo(const uint32_t* key, int64_t n, int64_t nchunk, uint32_t* lo) {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= n; p += (int64_t)gridDim.x * blockDim.x) {
         const int64_t kc = p < n ? (int64_t)key[p] : nchunk * kChunk;
         const int64_t kp = p > 0 ? (int64_t)key[p - 1] : -1;
         if (kc == kp) continue;
-        if (p < n) c++;
         const int64_t b0 = kp < 0 ? 0 : kp / kChunk + 1;  // chunks whose first cell is in (kp, kc]
         const int64_t b1 = min(kc / kChunk, nchunk);
         for (int64_t b = b0; b <= b1; b++) lo[b] = (uint32_t)p;
     }
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt, c);
-    __syncthreads();
-    if (threadIdx.x == 0 && s_cnt) atomicAdd(runs, s_cnt);
 }
 
 __global__ void __launch_bounds__(256) k_cell_starts(const uint32_t* __restrict__ key, const uint32_t* __restrict__ lo,
@@ -301,25 +290,58 @@ __global__ void k_cell_keys_rec(GridDesc g, const float* cxyz, size_t stride_f, 
 // internal index.  A stable LSD sort then yields cell order with ties in input order
 // (deterministic); dense mode also flags the point's brick for the two-level search.
 template <typename T>
-__global__ void k_cell_keys(GridDesc g, const T* cxyz, int64_t n, uint32_t* key, uint32_t* val, int32_t* mark) {
+__global__ void k_cell_keys(GridDesc g, const T* cxyz, size_t stride_t, int64_t n, uint32_t* key, uint32_t* val,
+                            int32_t* mark) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         int cx, cy, cz;
-        cell_of_point<T>(g, cxyz + 3 * i, cx, cy, cz);
+        cell_of_point<T>(g, cxyz + stride_t * i, cx, cy, cz);
         key[i] = (uint32_t)cell_id(g, cx, cy, cz);
         val[i] = (uint32_t)i;
         if (mark) mark[brick_of(g, cx, cy, cz)] = 1;
     }
 }
 
+// The automatic cell size's occupancy probe: the number of non-empty cells of geometry g
+// without sorting -- every point stores a 1 into its cell's byte of a flag array (plain byte
+// stores: every writer stores the same value, and a bitmap's atomics serialised on the few
+// words a row of cells shares; a lane whose cell equals the previous lane's skips its store),
+// then k_count_flags sums the bytes.  The same count as the runs of the sorted keys.
+template <typename T>
+__global__ void k_cell_flags(GridDesc g, const T* cxyz, size_t stride_t, int64_t n, uint8_t* flags) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int cx, cy, cz;
+        cell_of_point<T>(g, cxyz + stride_t * i, cx, cy, cz);
+        const uint32_t k = (uint32_t)cell_id(g, cx, cy, cz);
+        const uint32_t prev = (uint32_t)__shfl_up((int)k, 1, 64);
+        if ((threadIdx.x & 63) == 0 || prev != k) flags[k] = 1;
+    }
+}
+// nv 16-byte vectors of 0/1 bytes
+__global__ void k_count_flags(const uint4* flags, int64_t nv, unsigned long long* count) {
+    __shared__ unsigned long long s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    unsigned long long c = 0;
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nv; w += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 v = flags[w];
+        c += (unsigned)(__popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w));
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_cnt) atomicAdd(count, s_cnt);
+}
+
 // points in cell order: w = internal j (fp64, FLANN tie order) or caller index bits (fp32)
 template <typename T>
-__global__ void k_gather(const T* cxyz, const uint32_t* val, const int32_t* mapping, int64_t n,
+__global__ void k_gather(const T* cxyz, size_t stride_t, const uint32_t* val, const int32_t* mapping, int64_t n,
                          typename Real<T>::V4* pts, int32_t* sorted_j, int is_f64) {
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
          k += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t i = val[k];
-        const T* p = cxyz + 3 * (int64_t)i;
+        const T* p = cxyz + stride_t * i;
         typename Real<T>::V4 v;
         v.x = p[0]; v.y = p[1]; v.z = p[2];
         if (is_f64) v.w = (T)(double)i;
@@ -375,10 +397,11 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     int rc;
     T* cxyz = nullptr;
     double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
-    // ---- fp32 (ICP target): bbox + non-finite count in one pass; an all-finite cloud is keyed
-    // straight from the caller's array (no compaction, identity mapping)
-    bool direct = false;
-    if (!is_f64 && !indices && n_in > 0 && stride % sizeof(T) == 0) {
+    // ---- bbox + non-finite count in one pass; an all-finite cloud without an indices subset is
+    // keyed and gathered straight from the caller's array (no compaction: the identity mapping,
+    // which the compaction of an all-finite cloud would produce)
+    bool direct = false, have_bbox = false;
+    if (!indices && n_in > 0 && stride % sizeof(T) == 0) {
         const unsigned nbk = grid_for(n_in, kB, 1024);
         double* part = nullptr;
         unsigned long long* d_bad = nullptr;
@@ -396,14 +419,17 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         dfree(ctx, part);
         dfree(ctx, d_bad);
         if (e != hipSuccess) return fail(hip_fail(ctx, e, "bbox", __FILE__, __LINE__));
-        if (bad == 0) {
-            direct = true;
+        if (bad < (unsigned long long)n_in) {  // the bbox of the finite points = the compacted cloud's
+            have_bbox = true;
             for (int a = 0; a < 3; a++) { mn[a] = INFINITY; mx[a] = -INFINITY; }
             for (unsigned b = 0; b < nbk; b++)
                 for (int a = 0; a < 3; a++) {
                     mn[a] = std::fmin(mn[a], hp[6 * b + a]);
                     mx[a] = std::fmax(mx[a], hp[6 * b + 3 + a]);
                 }
+        }
+        if (bad == 0) {
+            direct = true;
             ix->n = n_in;
             ix->identity = 1;
         }
@@ -438,8 +464,8 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     }
     const int64_t n = ix->n;
 
-    // ---- bbox
-    if (n > 0 && !direct) {
+    // ---- bbox (of an indices subset)
+    if (n > 0 && !have_bbox) {
         const unsigned nbk = grid_for(n, kB, 1024);
         double* part;
         if ((rc = dmalloc(ctx, &part, 6 * (size_t)nbk))) { dfree(ctx, cxyz); return fail(rc); }
@@ -523,6 +549,30 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             hooked = true;                                  // work that needs only it (overlaps the sort)
             if ((rc = (*on_geom)(g))) break;
         }
+        if (auto_h && attempt < 2 && n > 0) {
+            // the automatic cell size, refined from this geometry's measured occupancy before
+            // any sort (a count of the non-empty cells by byte flags)
+            const int64_t nv = (ncells + 15) / 16;  // 16-byte vectors of cell flags
+            uint4* cflag = nullptr;
+            unsigned long long* d_ne = nullptr;
+            if ((rc = dmalloc(ctx, &cflag, nv)) || (rc = dmalloc(ctx, &d_ne, 1))) { dfree(ctx, cflag); break; }
+            hipError_t e = hipMemsetAsync(cflag, 0, (size_t)nv * sizeof(uint4), st);
+            if (e == hipSuccess) e = hipMemsetAsync(d_ne, 0, sizeof(unsigned long long), st);
+            hipLaunchKernelGGL(k_cell_flags<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, direct ? xyz : cxyz,
+                               direct ? stride / sizeof(T) : (size_t)3, n, (uint8_t*)cflag);
+            hipLaunchKernelGGL(k_count_flags, dim3(grid_for(nv, kB, 1024)), dim3(kB), 0, st, cflag, nv, d_ne);
+            unsigned long long ne = 0;
+            if (e == hipSuccess) e = hipMemcpyAsync(&ne, d_ne, sizeof(ne), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            dfree(ctx, cflag);
+            dfree(ctx, d_ne);
+            if (e != hipSuccess) { rc = hip_fail(ctx, e, "occupancy", __FILE__, __LINE__); break; }
+            const double occ = (double)n / std::max(1.0, (double)ne);
+            bool redo = false;
+            if (occ > 12.0) { h *= std::sqrt(4.0 / occ); redo = true; }   // surface-like data
+            else if (occ < 1.5) { h *= std::cbrt(4.0 / occ); redo = true; }  // sparser than assumed
+            if (redo) continue;
+        }
         // + 1 pad entry: the ICP octant pass loads a row's starts as one 3-word vector at the row's
         // first cell, whose third word lies one past the table for a 1-cell row at the last cell
         if ((rc = dmalloc(ctx, &count, ncells + 2))) break;
@@ -542,8 +592,8 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             size_t tmp_bytes = 0;
             void* tmp = nullptr;
             if (is_f64) {
-                hipLaunchKernelGGL(k_cell_keys<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, cxyz, n, skey, rank,
-                                   g.dense ? ix->brick : nullptr);
+                hipLaunchKernelGGL(k_cell_keys<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, g, direct ? xyz : cxyz,
+                                   direct ? stride / sizeof(T) : (size_t)3, n, skey, rank, g.dense ? ix->brick : nullptr);
                 PCP_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, skey, key1, rank, val1, (size_t)n, 0u,
                                                        bits, st));
                 if (!(rc = dmalloc(ctx, (char**)&tmp, tmp_bytes)))
@@ -572,32 +622,19 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         }
         if (g.dense && is_f64)
             hipLaunchKernelGGL(k_brick_flag, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, ix->brick, g.nbricks);
-        // ---- chunk boundaries of the sorted keys (+ the number of non-empty cells)
+        // ---- chunk boundaries of the sorted keys
         const int64_t nchunk = (ncells + 1 + kChunk - 1) / kChunk;
         uint32_t* lo = nullptr;
-        unsigned long long* d_ne = nullptr;
-        if ((rc = dmalloc(ctx, &lo, nchunk + 1)) || (rc = dmalloc(ctx, &d_ne, 1))) {
-            dfree(ctx, lo); dfree(ctx, key1); dfree(ctx, val1);
+        if ((rc = dmalloc(ctx, &lo, nchunk + 1))) {
+            dfree(ctx, key1); dfree(ctx, val1);
             break;
         }
-        PCP_HIP(ctx, hipMemsetAsync(d_ne, 0, sizeof(unsigned long long), st));
         hipLaunchKernelGGL(k_chunk_lo, dim3(grid_for(n + 1, kB, 1024)), dim3(kB), 0, st, (const uint32_t*)key1, n,
-                           nchunk, lo, d_ne);
-        if (auto_h && attempt < 2 && n > 0) {
-            unsigned long long ne = 0;
-            hipMemcpyAsync(&ne, d_ne, sizeof(ne), hipMemcpyDeviceToHost, st);
-            hipStreamSynchronize(st);
-            double occ = (double)n / std::max(1.0, (double)ne);
-            bool redo = false;
-            if (occ > 12.0) { h *= std::sqrt(4.0 / occ); redo = true; }   // surface-like data
-            else if (occ < 1.5) { h *= std::cbrt(4.0 / occ); redo = true; }  // sparser than assumed
-            if (redo) { dfree(ctx, lo); dfree(ctx, d_ne); dfree(ctx, key1); dfree(ctx, val1); continue; }
-        }
+                           nchunk, lo);
         // ---- cell starts straight from the sorted keys (no count array, no scan)
         hipLaunchKernelGGL(k_cell_starts, dim3((unsigned)nchunk), dim3(kB), 0, st, (const uint32_t*)key1,
                            (const uint32_t*)lo, ncells + 1, count);
         dfree(ctx, lo);
-        dfree(ctx, d_ne);
         g.cstart = count;
         if (g.dense && is_f64 && n > 0)
             hipLaunchKernelGGL(k_brick_rows, dim3(grid_for(g.nbricks, kB)), dim3(kB), 0, st, g, ix->brick);
@@ -607,7 +644,8 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
         if (is_f64) {
             if ((rc = dmalloc(ctx, &ix->sorted_j, n + 1))) { dfree(ctx, key1); dfree(ctx, val1); break; }
             if (n > 0)
-                hipLaunchKernelGGL(k_gather<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, cxyz, (const uint32_t*)val1,
+                hipLaunchKernelGGL(k_gather<T>, dim3(grid_for(n, kB)), dim3(kB), 0, st, direct ? xyz : cxyz,
+                                   direct ? stride / sizeof(T) : (size_t)3, (const uint32_t*)val1,
                                    (const int32_t*)ix->mapping, n, (V4*)ix->pts, ix->sorted_j, is_f64);
         }
         dfree(ctx, key1);

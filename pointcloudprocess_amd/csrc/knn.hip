@@ -80,6 +80,9 @@ __host__ __device__ inline double cell_margin64(const GridDesc& g) {
 #ifndef PCP_NORMALS_NEAR_DEFAULT  // tiled normals: 1 = the lane-per-query near pass before the far pass
 #define PCP_NORMALS_NEAR_DEFAULT 1
 #endif
+#ifndef PCP_T_NOPCA  // profiling builds only: the tile skips its mean/covariance passes (planes wrong)
+#define PCP_T_NOPCA 0
+#endif
 template <int K>
 struct KnnVisitor {
     static constexpr int U = K <= 16 ? PCP_KNN_BATCH : 2;
@@ -1514,6 +1517,14 @@ __global__ __launch_bounds__(64, 2) void k_normals_tile(GridDesc g, const double
             const int jq = (int)q.w;
             const int64_t oi = identity ? jq : mapping[jq];
             if (oi >= n_out) continue;
+#if PCP_T_NOPCA
+            {
+                pcp_plane pl{};
+                pl.normal_x = (float)D[0]; pl.normal_y = (float)D[1]; pl.distance = (float)P[K - 1];
+                out[oi] = pl;
+                continue;
+            }
+#endif
             // mean, sequential in kNN order (calculate_feature.cpp:131-142); the records again in
             // batches of unconditional loads (P[i] is a valid position for every i)
             double xa = 0, ya = 0, za = 0;
