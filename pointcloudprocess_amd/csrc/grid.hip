@@ -545,10 +545,6 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             g.brick = ix->brick;
             ncells = (int64_t)nslots * 64;
         }
-        if (on_geom && *on_geom && !auto_h && !hooked) {  // the geometry is final: let the caller start
-            hooked = true;                                  // work that needs only it (overlaps the sort)
-            if ((rc = (*on_geom)(g))) break;
-        }
         if (auto_h && attempt < 2 && n > 0) {
             // the automatic cell size, refined from this geometry's measured occupancy before
             // any sort (a count of the non-empty cells by byte flags)
@@ -572,6 +568,10 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             if (occ > 12.0) { h *= std::sqrt(4.0 / occ); redo = true; }   // surface-like data
             else if (occ < 1.5) { h *= std::cbrt(4.0 / occ); redo = true; }  // sparser than assumed
             if (redo) continue;
+        }
+        if (on_geom && *on_geom && !hooked) {  // the geometry is final (a given cell size, or the
+            hooked = true;                      // refinement is done): let the caller start work
+            if ((rc = (*on_geom)(g))) break;    // that needs only it (overlaps the sort)
         }
         // + 1 pad entry: the ICP octant pass loads a row's starts as one 3-word vector at the row's
         // first cell, whose third word lies one past the table for a 1-cell row at the last cell
@@ -662,7 +662,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     dfree(ctx, rank);
     dfree(ctx, skey);
     dfree(ctx, cxyz);
-    if (!rc && on_geom && *on_geom && !hooked) rc = (*on_geom)(ix->g);  // auto cell size: after the refinement
+    if (!rc && on_geom && *on_geom && !hooked) rc = (*on_geom)(ix->g);  // (not reached: the loop hooks before its sort)
     if (rc) return fail(rc);
     PCP_HIP(ctx, hipGetLastError());
     PCP_HIP(ctx, hipStreamSynchronize(st));
