@@ -135,6 +135,9 @@ __global__ void k_h16_plane_default(pcp_plane* out, int64_t n) {
 // candidate steps per block (2 x 64): a smaller block is more blocks per neighbourhood but less
 // LDS per wave -- 5 waves/SIMD at 128 candidates against 3 at 256 (measured: 256 / 192 / 128 / 64
 // candidates 2030 / 2165 / 2240 / 2257 Mpts/s, profiles/r05_c5/)
+#ifndef PCP_H16_TRIG32  // planes: the eigen angle in fp32 + fp64 Newton polish of l3 (0: fp64 acos / cos)
+#define PCP_H16_TRIG32 1
+#endif
 #ifndef PCP_MX_STEPS
 #define PCP_MX_STEPS 2
 #endif
@@ -436,9 +439,33 @@ __device__ inline bool h16_plane(const double C[9], double xa, double ya, double
         const double p = sqrt(q);
         const double det = b00 * (b11 * b22 - a12 * a12) - a01 * (a01 * b22 - a12 * a02) + a02 * (a01 * a12 - b11 * a02);
         const double r = fmin(fmax(det / (2.0 * p * p * p), -1.0), 1.0);
+#if PCP_H16_TRIG32
+        // The angle and its cosines in fp32 (the fp64 acos and two cos were most of the pass's ~750
+        // instructions), then l3 polished by two fp64 Newton steps on det(C - l I).  acos(r) comes
+        // from 2 asin(sqrt((1 - |r|) / 2)) with 1 - |r| taken in fp64, so the fp32 angle keeps a
+        // relative error ~1e-7 up to |r| -> 1: at r -> 1 (l2 -> l3) l3 then starts within ~1e-7
+        // of the l2 - l3 gap from its root (Newton squares that ratio per step; l2 = l3 itself is
+        // the Jacobi fallback below), and at r -> -1 (l1 -> l2, planes) l3 does not depend on the
+        // angle to first order.
+        const float hs = 2.f * asinf(sqrtf((float)(0.5 * (1.0 - fabs(r)))));  // acos(|r|)
+        const float phif = (r >= 0.0 ? hs : 3.14159265f - hs) * (1.f / 3.f);
+        l1 = m + 2.0 * p * (double)cosf(phif);
+        double l = m + 2.0 * p * (double)cosf(phif + 2.0943951f);  // + 2 pi / 3
+        const double tr = a00 + a11 + a22;
+        const double c1 = a00 * a11 + a00 * a22 + a11 * a22 - p1;  // sum of the principal 2x2 minors
+        const double dc = a00 * (a11 * a22 - a12 * a12) - a01 * (a01 * a22 - a12 * a02) + a02 * (a01 * a12 - a11 * a02);
+#pragma unroll
+        for (int it = 0; it < 2; it++) {
+            const double f = ((tr - l) * l - c1) * l + dc;  // det(C - l I) = -l^3 + tr l^2 - c1 l + det C
+            const double fp = (2.0 * tr - 3.0 * l) * l - c1;
+            l = fp != 0.0 ? l - f / fp : l;
+        }
+        l3 = l;
+#else
         const double phi = acos(r) / 3.0;
         l1 = m + 2.0 * p * cos(phi);
         l3 = m + 2.0 * p * cos(phi + 2.0943951023931954923);  // + 2 pi / 3
+#endif
         l2 = 3.0 * m - l1 - l3;
         ok = (l2 - l3) > 1e-4 * (l1 - l3);
         if (ok) {
