@@ -196,6 +196,16 @@ __global__ void k_brick_final(int32_t* brick, int64_t nb, const uint32_t* bits) 
 // key gap before it; p = n is a virtual run start closing the table); k_cell_starts then resolves one chunk per
 // block in LDS (run starts scattered, suffix minimum) and writes it out coalesced.
 constexpr int kChunk = 4096;
+// grids of the streaming passes over every point (bbox, chunk bounds): enough waves in flight per
+// CU to cover the loads' latency (at 1024 blocks the 200M-point passes ran at 1-4 TB/s)
+#ifndef PCP_SCAN_BLOCKS
+#define PCP_SCAN_BLOCKS 16384
+#endif
+#ifndef PCP_BBOX_BLOCKS
+#define PCP_BBOX_BLOCKS 4096
+#endif
+constexpr int64_t kScanBlocks = PCP_SCAN_BLOCKS;
+constexpr int64_t kBboxBlocks = PCP_BBOX_BLOCKS;
 
 __global__ void k_chunk_lo(const uint32_t* key, int64_t n, int64_t nchunk, uint32_t* lo) {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= n; p += (int64_t)gridDim.x * blockDim.x) {
@@ -402,7 +412,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
     // which the compaction of an all-finite cloud would produce)
     bool direct = false, have_bbox = false;
     if (!indices && n_in > 0 && stride % sizeof(T) == 0) {
-        const unsigned nbk = grid_for(n_in, kB, 1024);
+        const unsigned nbk = grid_for(n_in, kB, kBboxBlocks);
         double* part = nullptr;
         unsigned long long* d_bad = nullptr;
         if ((rc = dmalloc(ctx, &part, 6 * (size_t)nbk)) || (rc = dmalloc(ctx, &d_bad, 1))) {
@@ -466,7 +476,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
 
     // ---- bbox (of an indices subset)
     if (n > 0 && !have_bbox) {
-        const unsigned nbk = grid_for(n, kB, 1024);
+        const unsigned nbk = grid_for(n, kB, kBboxBlocks);
         double* part;
         if ((rc = dmalloc(ctx, &part, 6 * (size_t)nbk))) { dfree(ctx, cxyz); return fail(rc); }
         hipLaunchKernelGGL(k_minmax<T>, dim3(nbk), dim3(kB), 0, st, cxyz, n, part);
@@ -629,7 +639,7 @@ int build_impl(pcp_ctx* ctx, const T* xyz, size_t stride, int64_t n_in, const in
             dfree(ctx, key1); dfree(ctx, val1);
             break;
         }
-        hipLaunchKernelGGL(k_chunk_lo, dim3(grid_for(n + 1, kB, 1024)), dim3(kB), 0, st, (const uint32_t*)key1, n,
+        hipLaunchKernelGGL(k_chunk_lo, dim3(grid_for(n + 1, kB, kScanBlocks)), dim3(kB), 0, st, (const uint32_t*)key1, n,
                            nchunk, lo);
         // ---- cell starts straight from the sorted keys (no count array, no scan)
         hipLaunchKernelGGL(k_cell_starts, dim3((unsigned)nchunk), dim3(kB), 0, st, (const uint32_t*)key1,
