@@ -109,6 +109,23 @@ def test_knn_nonfinite_and_indices(ctx):
     assert np.array_equal(gi.cpu().numpy(), ei) and np.array_equal(gd.cpu().numpy(), ed)
 
 
+@pytest.mark.parametrize("finite", [0, 1])
+def test_knn_all_or_all_but_one_nonfinite(ctx, finite):
+    """The build's bbox + non-finite pass with no finite point (an empty index) or exactly one:
+    rows padded with -1 / inf like the oracle's."""
+    from pointcloudprocess_amd import ops
+    xyz = np.full((50, 3), np.nan)
+    if finite:
+        xyz[7] = [1.0, 2.0, 3.0]
+    q = np.zeros((2, 3))
+    ix = ops.GridIndex(ctx, _dev(ctx, xyz))
+    t = ora.KdTree(xyz)
+    assert ix.size == t.size == finite
+    gi, gd = ops.knn(ix, _dev(ctx, q), 4)
+    ei, ed = t.knn(q, 4)
+    assert np.array_equal(gi.cpu().numpy(), ei) and np.array_equal(gd.cpu().numpy(), ed)
+
+
 def test_knn_aos48_and_small(ctx):
     from pointcloudprocess_amd import ops
     xyz = _cloud(5, 13)
