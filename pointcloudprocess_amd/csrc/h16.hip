@@ -142,6 +142,10 @@ __global__ void k_h16_plane_default(pcp_plane* out, int64_t n) {
 #define PCP_MX_STEPS 2
 #endif
 constexpr int kMxSteps = PCP_MX_STEPS;
+#ifndef PCP_MX_COUNT_STEPS  // the count pass's steps per block (it stages nothing in LDS)
+#define PCP_MX_COUNT_STEPS 4
+#endif
+constexpr int kMxCountSteps = PCP_MX_COUNT_STEPS;
 constexpr int kMxC = kMxSteps * 64;      // candidates per block
 constexpr int kMxF = 9;                  // moment feature rows: x y z xx xy xz yy yz zz, each word = (hi, lo) f16
 constexpr int kMxFS = kMxC + 4;          // feature row stride (words)
@@ -190,6 +194,9 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
     __shared__ float2 s_rdz[9];  // per neighbour row: its dy h, dz h
     __shared__ float s_p[FILL ? 4 : 1][FILL ? kMxPS : 1];                          // P x y z, |P|^2
     __shared__ __attribute__((aligned(16))) uint32_t s_f[FILL ? kMxF : 1][FILL ? kMxFS : 1];  // moments
+    // candidate steps per block: the fill's LDS-sized blocks, the count's own (no LDS staging)
+    constexpr int kS = FILL ? kMxSteps : kMxCountSteps;
+    constexpr int kC = kS * 64;
     const GridDesc& g = a.g;
     const int lane = threadIdx.x;
     const float hf = a.hf, hh = 0.5f * a.hf, r2 = a.r2;
@@ -243,11 +250,11 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
             wave_sync();
             // the block's candidates: P (query-cell-centre frame) in registers (the rows' B
             // operands) and, for the fill, P and the moment features in LDS
-            float bx[kMxSteps], by[kMxSteps], bz[kMxSteps], bp[kMxSteps];
-            int32_t cidv[kMxSteps];
+            float bx[kS], by[kS], bz[kS], bp[kS];
+            int32_t cidv[kS];
             auto load_block = [&](uint32_t blk) {
 #pragma unroll
-                for (int s = 0; s < kMxSteps; s++) {
+                for (int s = 0; s < kS; s++) {
                     if (blk + 64u * s >= M) break;  // (uniform) steps past the list are never read
                     const uint32_t j = blk + 64u * s + (uint32_t)lane;
                     const bool ok = j < M;
@@ -293,7 +300,7 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
                     }
                 }
             };
-            const uint32_t nblk = (M + kMxC - 1) / kMxC;
+            const uint32_t nblk = (M + kC - 1) / kC;
             if (nblk == 1) {
                 load_block(0u);
                 wave_sync();
@@ -338,12 +345,12 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
                         }
                     }
                     // the block's products first (independent chains in flight), then the rows
-                    mx_f4 Ds[kMxSteps];
+                    mx_f4 Ds[kS];
 #pragma unroll
-                    for (int s = 0; s < kMxSteps; s++)
+                    for (int s = 0; s < kS; s++)
                         if (64u * s < mb) Ds[s] = mx_rows<G>(ax, ay, az, bx[s], by[s], bz[s], bp[s], Cg);
 #pragma unroll
-                    for (int s = 0; s < kMxSteps; s++) {
+                    for (int s = 0; s < kS; s++) {
                         if (64u * s >= mb) break;
                         const mx_f4 D = Ds[s];
 #pragma unroll
@@ -367,17 +374,17 @@ __global__ __launch_bounds__(64, kMxWaves) void k_h16_mx(H16Args a, int32_t* __r
                 for (uint32_t b = 0; b < nblk; b++) {
                     if (nblk > 1) {  // (uniform) a neighbourhood larger than one block
                         wave_sync();
-                        load_block(b * (uint32_t)kMxC);
+                        load_block(b * (uint32_t)kC);
                         wave_sync();
                     }
-                    const uint32_t mb = min(M - b * (uint32_t)kMxC, (uint32_t)kMxC);
+                    const uint32_t mb = min(M - b * (uint32_t)kC, (uint32_t)kC);
                     group_rows(std::integral_constant<int, 0>{}, C0, mb);
                     group_rows(std::integral_constant<int, 1>{}, C1, mb);
                     group_rows(std::integral_constant<int, 2>{}, C2, mb);
                     group_rows(std::integral_constant<int, 3>{}, C3, mb);
                     if constexpr (FILL) {
 #pragma unroll
-                        for (int s = 0; s < kMxSteps; s++) {
+                        for (int s = 0; s < kS; s++) {
                             if (64u * s >= mb) break;
                             // sums: the hit matrix in the transposed layout, then moments x hits,
                             // 16 candidates per product: K = 32 runs over (candidate, hi / lo)
